@@ -1,0 +1,137 @@
+"""Native build driver for the hfrep gfx950 kernel library.
+
+Compiles every ``csrc/*.hip`` kernel translation unit with ``hipcc --offload-arch=gfx950``
+and the torch op bindings (``csrc/bindings.cpp``), then links them IN-TREE into
+``ops/_hfrep_native.so``.  The library registers ``torch.ops.hfrep.*`` when loaded with
+``torch.ops.load_library`` (see ``ops/_native.py``).
+
+No hipify, no torch JIT cache: the objects live under ``build/native`` and the shared object
+lives next to the Python code so it travels with the repository snapshot to the GPU box.
+
+Usage::
+
+    python -m hfrep.build_native          # incremental
+    python build_native.py --force        # full rebuild
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT_SO = os.path.join(HERE, "ops", "_hfrep_native.so")
+BUILD_DIR = os.path.join(os.path.dirname(HERE), "build", "native")
+ARCH = os.environ.get("HFREP_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (expected /opt/rocm/bin/hipcc)")
+
+
+def _torch_paths():
+    import torch  # noqa: F401  (only for include/lib paths)
+    from torch.utils import cpp_extension
+
+    incs = cpp_extension.include_paths()
+    libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return incs, libdir, abi
+
+
+def _flags():
+    incs, libdir, abi = _torch_paths()
+    common = ["-O3", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-I{CSRC}"]
+    kern = common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-ffp-contract=fast"]
+    bind = common + [f"--offload-arch={ARCH}", "-DUSE_ROCM", "-D__HIP_PLATFORM_AMD__", "-DTORCH_EXTENSION_NAME=hfrep_native",
+                     "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-unused-result", "-Wno-deprecated-declarations"]
+    bind += [f"-I{p}" for p in incs] + [f"-I{sysconfig.get_paths()['include']}"]
+    link = ["-shared", "-fPIC", f"--offload-arch={ARCH}", f"-L{libdir}", f"-Wl,-rpath,{libdir}",
+            "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip"]
+    return kern, bind, link
+
+
+def _sources():
+    hips = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+    cpps = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".cpp"))
+    headers = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h"))
+    return hips, cpps, headers
+
+
+def _digest(paths, extra: str) -> str:
+    h = hashlib.sha256(extra.encode())
+    for p in paths:
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:20]
+
+
+def _compile(src, obj, flags, headers):
+    stamp = obj + ".stamp"
+    dig = _digest([src] + headers, " ".join(flags))
+    if os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == dig:
+        return obj, False
+    cmd = [_hipcc()] + flags + ["-c", src, "-o", obj]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+    with open(stamp, "w") as fh:
+        fh.write(dig)
+    return obj, True
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    kern, bind, link = _flags()
+    hips, cpps, headers = _sources()
+    if force:
+        for f in os.listdir(BUILD_DIR):
+            os.remove(os.path.join(BUILD_DIR, f))
+    jobs = jobs or min(8, os.cpu_count() or 4, 16)
+    tasks = [(s, os.path.join(BUILD_DIR, os.path.basename(s) + ".o"), kern) for s in hips]
+    tasks += [(s, os.path.join(BUILD_DIR, os.path.basename(s) + ".o"), bind) for s in cpps]
+    changed = False
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = [ex.submit(_compile, s, o, f, headers) for s, o, f in tasks]
+        objs = []
+        for fut in futs:
+            o, c = fut.result()
+            objs.append(o)
+            changed |= c
+    if changed or not os.path.exists(OUT_SO) or force:
+        tmp = OUT_SO + ".tmp"
+        cmd = [_hipcc()] + objs + link + ["-o", tmp]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+        os.replace(tmp, OUT_SO)
+        meta = {"arch": ARCH, "sources": [os.path.basename(s) for s in hips + cpps]}
+        with open(OUT_SO + ".json", "w") as fh:
+            json.dump(meta, fh)
+        if verbose:
+            print(f"[hfrep.build_native] linked {OUT_SO} ({len(objs)} objects)")
+    elif verbose:
+        print(f"[hfrep.build_native] up to date: {OUT_SO}")
+    return OUT_SO
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    a = ap.parse_args(argv)
+    build(force=a.force, jobs=a.jobs)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

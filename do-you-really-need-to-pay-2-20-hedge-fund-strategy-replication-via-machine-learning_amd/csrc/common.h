@@ -1,0 +1,159 @@
+// Shared device helpers for the hfrep gfx950 (CDNA4) kernel library.
+//
+// Everything here is written for MI355X only: wave64, MFMA 32x32 tiles, LDS.
+// No CUDA shims and no dual-platform paths.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace hfrep {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------------------
+// bf16 helpers (storage type is raw uint16_t so host code never needs hip_bf16)
+// ---------------------------------------------------------------------------
+typedef uint16_t bf16_t;
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// round-to-nearest-even; NaN stays NaN (quiet bit forced)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+template <typename T> struct Cvt;
+template <> struct Cvt<float> {
+  __device__ __forceinline__ static float to_f(float v) { return v; }
+  __device__ __forceinline__ static float from_f(float v) { return v; }
+};
+template <> struct Cvt<bf16_t> {
+  __device__ __forceinline__ static float to_f(bf16_t v) { return bf2f(v); }
+  __device__ __forceinline__ static bf16_t from_f(float v) { return f2bf(v); }
+};
+template <typename T> __device__ __forceinline__ float ld_f(const T* p) { return Cvt<T>::to_f(*p); }
+template <typename T> __device__ __forceinline__ void st_f(T* p, float v) { *p = Cvt<T>::from_f(v); }
+
+// ---------------------------------------------------------------------------
+// activations (Keras semantics).  act codes shared with the host side:
+//   0 = linear, 1 = sigmoid, 2 = tanh, 3 = leaky_relu(0.2), 4 = relu
+// ---------------------------------------------------------------------------
+enum Act : int { ACT_LINEAR = 0, ACT_SIGMOID = 1, ACT_TANH = 2, ACT_LRELU = 3, ACT_RELU = 4 };
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanhf_(float x) {
+  // tanh via exp: accurate to ~1 ulp of fp32 over the useful range, saturates cleanly
+  float ax = fabsf(x);
+  float e = __expf(-2.0f * ax);
+  float t = (1.0f - e) / (1.0f + e);
+  return copysignf(t, x);
+}
+
+__device__ __forceinline__ float act_f(int act, float x) {
+  switch (act) {
+    case ACT_SIGMOID: return sigmoidf_(x);
+    case ACT_TANH: return tanhf_(x);
+    case ACT_LRELU: return x >= 0.f ? x : 0.2f * x;
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    default: return x;
+  }
+}
+// derivative expressed through the activation OUTPUT y (all supported acts allow it)
+__device__ __forceinline__ float act_dy(int act, float y) {
+  switch (act) {
+    case ACT_SIGMOID: return y * (1.f - y);
+    case ACT_TANH: return 1.f - y * y;
+    case ACT_LRELU: return y >= 0.f ? 1.f : 0.2f;
+    case ACT_RELU: return y > 0.f ? 1.f : 0.f;
+    default: return 1.f;
+  }
+}
+// second derivative expressed through y: needed by the tangent (double-backward) LSTM
+__device__ __forceinline__ float act_d2y(int act, float y) {
+  switch (act) {
+    case ACT_SIGMOID: return y * (1.f - y) * (1.f - 2.f * y);
+    case ACT_TANH: return -2.f * y * (1.f - y * y);
+    default: return 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wave / block reductions (wave64)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+// sum over the 32 lanes of one half-wave (lanes l and l^k for k<32)
+__device__ __forceinline__ float halfwave_sum(float v) {
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int NWAVES>
+__device__ __forceinline__ float block_sum(float v, float* red /* LDS, >= NWAVES floats */) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NWAVES; ++i) s += red[i];
+  __syncthreads();
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// MFMA fragment types
+// ---------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+// 32x32 accumulator row index of register r for lane l (dtype independent on gfx950)
+__device__ __forceinline__ int acc32_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 counter RNG (device side).  Deterministic in (seed, offset).
+// ---------------------------------------------------------------------------
+struct Philox {
+  __device__ __forceinline__ static void round(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3,
+                                               uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+    uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+  __device__ __forceinline__ static uint4 gen(uint64_t seed, uint64_t ctr_hi, uint32_t ctr_lo) {
+    uint32_t c0 = ctr_lo, c1 = 0, c2 = (uint32_t)ctr_hi, c3 = (uint32_t)(ctr_hi >> 32);
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      round(c0, c1, c2, c3, k0, k1);
+      k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+  }
+};
+__device__ __forceinline__ float u32_to_unit(uint32_t x) {  // (0,1]
+  return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+}  // namespace hfrep
+
+#define HFREP_CHECK_HIP(expr)                                                                  \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess) {                                                                    \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__); \
+    }                                                                                          \
+  } while (0)
