@@ -1,0 +1,186 @@
+"""Device-dispatching primitive API used by the explicit engine and the trainers.
+
+CPU tensors run the PyTorch reference (:mod:`hfrep.ops.reference`); GPU tensors run the gfx950
+kernels in ``_hfrep_native.so`` (``torch.ops.hfrep``).  There is no silent fallback on GPU: if the
+library is missing, :func:`hfrep.ops._native.use_native_for` raises (see its docstring).
+
+Shapes: activations are (..., features) with the feature axis contiguous; Dense/LSTM kernels
+are Keras-layout (in, out) fp32 master weights; activations may be fp32 or bf16 (the compute
+dtype of the explicit engine); gradients are always fp32.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native
+from . import reference as R
+
+
+def _nat(t: torch.Tensor) -> bool:
+    return _native.use_native_for(t)
+
+
+def _ops():
+    return _native.native()
+
+
+def _2d(x: torch.Tensor) -> torch.Tensor:
+    return x.reshape(-1, x.shape[-1])
+
+
+# ---------------------------------------------------------------------------------------
+# dense / GEMM family
+# ---------------------------------------------------------------------------------------
+def linear(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: int) -> torch.Tensor:
+    """act(x @ W + b) on the last axis. Output dtype = x dtype."""
+    if _nat(x):
+        y = _ops().linear(_2d(x.contiguous()), W, b, int(act))
+        return y.reshape(*x.shape[:-1], W.shape[1])
+    y = torch.matmul(x, W.to(x.dtype))
+    if b is not None:
+        y = y + b.to(x.dtype)
+    return R.apply_act(y, act)
+
+
+def linear_dgrad(dz: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    """dz @ W^T (input gradient)."""
+    if _nat(dz):
+        return _ops().linear_dgrad(_2d(dz.contiguous()), W).reshape(*dz.shape[:-1], W.shape[0])
+    return torch.matmul(dz, W.t().to(dz.dtype))
+
+
+def linear_wgrad_(x: torch.Tensor, dz: torch.Tensor, gW: torch.Tensor, gb: torch.Tensor | None) -> None:
+    """gW += x^T dz (summed over all leading axes); gb += sum(dz)."""
+    if _nat(dz):
+        _ops().linear_wgrad_(_2d(x.contiguous()), _2d(dz.contiguous()), gW, gb)
+        return
+    x2, d2 = _2d(x).to(gW.dtype), _2d(dz).to(gW.dtype)
+    gW.add_(x2.t() @ d2)
+    if gb is not None:
+        gb.add_(d2.sum(0))
+
+
+# ---------------------------------------------------------------------------------------
+# elementwise activations
+# ---------------------------------------------------------------------------------------
+def act_forward(x: torch.Tensor, act: int) -> torch.Tensor:
+    if _nat(x):
+        return _ops().act_fwd(x.contiguous(), int(act))
+    return R.apply_act(x, act)
+
+
+def act_backward(dy: torch.Tensor, y: torch.Tensor, act: int) -> torch.Tensor:
+    """dy * f'(x) written through y = f(x)."""
+    if act == 0:
+        return dy
+    if _nat(dy):
+        return _ops().act_bwd(dy.contiguous(), y.contiguous(), int(act))
+    return dy * R.act_dy(y, act)
+
+
+def act_tangent_backward(dy, dyd, y, zd, act: int):
+    """Adjoint of z for y = f(z), ydot = f'(z) zdot:  dy f'(z) + dyd f''(z) zdot."""
+    first = act_backward(dy, y, act) if dy is not None else None
+    if act in (0, 3, 4):  # piecewise linear: f'' = 0
+        return first if first is not None else torch.zeros_like(dyd)
+    if _nat(dyd):
+        sec = _ops().act_tangent_bwd(dyd.contiguous(), y.contiguous(), zd.contiguous(), int(act))
+    else:
+        sec = dyd * R.act_d2y(y, act) * zd
+    return sec if first is None else first + sec
+
+
+# ---------------------------------------------------------------------------------------
+# LSTM recurrences (persistent kernels on GPU)
+# ---------------------------------------------------------------------------------------
+def lstm_seq_fwd(zx, U, act: int, save: bool):
+    if _nat(zx):
+        hs, gates, cs = _ops().lstm_fwd(zx.contiguous(), U, int(act), bool(save))
+        return hs, (gates if save else None), (cs if save else None)
+    return R.lstm_seq_fwd(zx, U.to(zx.dtype), act, save)
+
+
+def lstm_seq_bwd(dh_seq, gates, cs, U, act: int):
+    if _nat(dh_seq):
+        return _ops().lstm_bwd(dh_seq.contiguous(), gates, cs, U, int(act))
+    return R.lstm_seq_bwd(dh_seq, gates, cs, U.to(dh_seq.dtype), act)
+
+
+def lstm_seq_tfwd(dzx, gates, cs, U, act: int):
+    if _nat(dzx):
+        return tuple(_ops().lstm_tfwd(dzx.contiguous(), gates, cs, U, int(act)))
+    return R.lstm_seq_tfwd(dzx, gates, cs, U.to(dzx.dtype), act)
+
+
+def lstm_seq_tbwd(dh_seq, dhd_seq, gates, cs, zds, cds, U, act: int):
+    if _nat(dhd_seq):
+        return tuple(_ops().lstm_tbwd(dh_seq.contiguous(), dhd_seq.contiguous(), gates, cs, zds, cds, U, int(act)))
+    return R.lstm_seq_tbwd(dh_seq, dhd_seq, gates, cs, zds, cds, U.to(dhd_seq.dtype), act)
+
+
+def shift_prev(h_seq: torch.Tensor) -> torch.Tensor:
+    """h_{t-1} for every t (zeros at t=0).  (B, T, H)"""
+    if _nat(h_seq):
+        return _ops().shift_prev(h_seq.contiguous())
+    return R.shift_prev(h_seq)
+
+
+# ---------------------------------------------------------------------------------------
+# LayerNorm
+# ---------------------------------------------------------------------------------------
+def layer_norm_fwd(x, gamma, beta, eps: float):
+    if _nat(x):
+        y, xhat, rstd = _ops().layernorm_fwd(x.contiguous(), gamma, beta, float(eps))
+        return y, xhat, rstd
+    return R.layer_norm_fwd(x, gamma.to(x.dtype), beta.to(x.dtype), eps)
+
+
+def layer_norm_bwd_(dy, xhat, rstd, gamma, ggamma, gbeta):
+    """Returns dx; accumulates dgamma/dbeta into the gradient views."""
+    if _nat(dy):
+        return _ops().layernorm_bwd_(dy.contiguous(), xhat, rstd, gamma, ggamma, gbeta)
+    dx, dg, db = R.layer_norm_bwd(dy, xhat, rstd, gamma.to(dy.dtype))
+    if ggamma is not None:
+        ggamma.add_(dg.to(ggamma.dtype))
+        gbeta.add_(db.to(gbeta.dtype))
+    return dx
+
+
+# ---------------------------------------------------------------------------------------
+# temporal conv helpers (im2col on the feature axis)
+# ---------------------------------------------------------------------------------------
+def im2col_causal(x: torch.Tensor, k: int, dil: int) -> torch.Tensor:
+    """(B, T, C) -> (B, T, k*C) with column block j holding x[t - (k-1-j)*dil] (zero padded)."""
+    B, T, C = x.shape
+    pad = (k - 1) * dil
+    xp = torch.nn.functional.pad(x, (0, 0, pad, 0))
+    cols = [xp[:, j * dil:j * dil + T] for j in range(k)]
+    return torch.cat(cols, dim=2)
+
+
+def col2im_causal(dcols: torch.Tensor, k: int, dil: int, C: int) -> torch.Tensor:
+    B, T, _ = dcols.shape
+    pad = (k - 1) * dil
+    dxp = dcols.new_zeros(B, T + pad, C)
+    for j in range(k):
+        dxp[:, j * dil:j * dil + T] += dcols[:, :, j * C:(j + 1) * C]
+    return dxp[:, pad:]
+
+
+# ---------------------------------------------------------------------------------------
+# WGAN-GP helpers
+# ---------------------------------------------------------------------------------------
+def gp_coef(g: torch.Tensor, weight: float):
+    """(penalty, v): penalty = mean((1-||g_b||)^2); v = d(weight*penalty)/dg."""
+    if _nat(g):
+        pen, v = _ops().gp_coef(g.contiguous(), float(weight))
+        return pen, v
+    return R.gp_coef(g, weight)
+
+
+def interpolate(real: torch.Tensor, fake: torch.Tensor, alpha: torch.Tensor) -> torch.Tensor:
+    """alpha (B,) per-sample: alpha*real + (1-alpha)*fake (GAN/MTSS_WGAN_GP.py:197-199)."""
+    if _nat(real):
+        return _ops().interpolate(real.contiguous(), fake.contiguous(), alpha.contiguous())
+    a = alpha.reshape(-1, *([1] * (real.dim() - 1))).to(real.dtype)
+    return a * real + (1 - a) * fake

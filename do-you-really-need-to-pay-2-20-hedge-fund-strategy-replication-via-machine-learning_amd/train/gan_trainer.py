@@ -1,0 +1,267 @@
+"""One training loop for the whole GAN zoo, with the loss as a strategy.
+
+Reference loops (all hand-rolled ``train_on_batch`` sequences):
+
+* ``gan``     — GAN/GAN.py:160-204, GAN/MTSS_GAN.py:159-203: D on real (label 1), D on G(z)
+  (label 0), then G through the frozen D (label 1); BCE; one Adam shared by both compiled models.
+* ``wgan``    — GAN/WGAN.py:166-212, GAN/MTSS_WGAN.py:165-211: n_critic x [D on real (-1), D on
+  G(z) (+1), clip every critic weight to +-c], then G on the LAST critic noise (label -1).
+* ``wgan_gp`` — GAN/WGAN_GP.py:255-288, GAN/MTSS_WGAN_GP.py:254-287: n_critic x one critic
+  update on [W(real,-1) + W(G(z),+1) + lambda * GP(x_hat)], then G on the last critic noise.
+
+MI355X-first differences (semantics preserved):
+
+* everything stays on the device: batches are gathered and noise is drawn by in-kernel Philox
+  (no host RNG, no H2D copies, no ``generator.predict`` round trip — GAN/WGAN.py:188);
+* gradients are produced by the explicit engine (``Sequential.efwd/ebwd/etfwd/etbwd``); the GP
+  critic update is the reverse-over-tangent Hessian-vector product (no autograd graph);
+* losses are accumulated on device and read back only at log intervals (the reference prints —
+  and therefore syncs — every iteration, GAN/MTSS_WGAN_GP.py:284);
+* data parallel: each rank samples its own batch; the flat gradient buffer of each model is
+  all-reduced (averaged) before the fused optimizer launch (``hfrep.parallel``).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..models import gan as zoo
+from ..ops import functional as Fn
+from ..ops import reference as R
+from ..utils.rng import DeviceRNG
+from .optim import KerasOptimizer
+
+
+@dataclass
+class GANConfig:
+    arch: str = "lstm"            # mlp | lstm | conv
+    loss: str = "wgan_gp"         # gan | wgan | wgan_gp
+    window: int = 48              # T
+    features: int = 35            # F
+    batch_size: int = 32          # per-rank batch
+    epochs: int = 5000            # reference "epochs" = iterations
+    n_critic: int | None = None   # default from the zoo entry
+    lr: float | None = None
+    clip: float | None = None
+    gp_weight: float | None = None
+    hidden: int = 100
+    lrelu_after_first: bool = False   # production generator variant
+    seed: int = 123
+    dtype: str = "float32"        # compute dtype of activations: float32 | bfloat16
+    log_every: int = 100
+    extra: dict = field(default_factory=dict)
+
+    def entry(self) -> zoo.ZooEntry:
+        return zoo.ZOO[(self.arch, self.loss)]
+
+
+_DT = {"float32": torch.float32, "fp32": torch.float32, "bfloat16": torch.bfloat16, "bf16": torch.bfloat16,
+       "float64": torch.float64}
+
+
+class GANTrainer:
+    def __init__(self, cfg: GANConfig, dataset, device="cpu", process_group=None, rank: int = 0, world: int = 1,
+                 param_dtype=torch.float32):
+        self.cfg = cfg
+        e = cfg.entry()
+        self.device = torch.device(device)
+        self.dtype = _DT[cfg.dtype]
+        self._acc = torch.float64 if self.dtype == torch.float64 else torch.float32
+        self.n_critic = cfg.n_critic if cfg.n_critic is not None else e.n_critic
+        self.lr = cfg.lr if cfg.lr is not None else e.lr
+        self.clip = cfg.clip if cfg.clip is not None else e.clip
+        self.gp_weight = cfg.gp_weight if cfg.gp_weight is not None else e.gp_weight
+        T, F = cfg.window, cfg.features
+        gkw = dict(seed=cfg.seed, dtype=param_dtype)
+        if cfg.arch != "mlp":
+            self.generator = e.generator(T, F, cfg.hidden, lrelu_after_first=cfg.lrelu_after_first, **gkw)
+        else:
+            self.generator = e.generator(T, F, cfg.hidden, **gkw)
+        self.critic = e.critic(T, F, cfg.hidden, seed=cfg.seed + 1, dtype=param_dtype)
+        self.generator.to(self.device)
+        self.critic.to(self.device)
+        # one optimizer instance shared by the critic and the combined model, as in the reference
+        if e.optimizer == "adam":
+            self.opt = KerasOptimizer.adam(self.lr, beta_1=0.5, device=self.device)
+        else:
+            self.opt = KerasOptimizer.rmsprop(self.lr, device=self.device)
+        self.pg, self.rank, self.world = process_group, rank, world
+        if isinstance(dataset, np.ndarray):
+            dataset = torch.from_numpy(np.ascontiguousarray(dataset, dtype=np.float32))
+        self.dataset = dataset.to(self.device, torch.float32).contiguous()
+        assert self.dataset.shape[1:] == (T, F), f"dataset windows {tuple(self.dataset.shape[1:])} != {(T, F)}"
+        self.rng = DeviceRNG(cfg.seed, self.device, stream=rank)
+        self.iteration = 0
+        self._d_acc = torch.zeros(4, device=self.device)  # last d_loss terms: total, real, fake, gp
+        self._g_acc = torch.zeros(1, device=self.device)
+        self.grad_sync = None  # set by hfrep.parallel.DataParallel
+        if world > 1 and process_group is not None:
+            from ..parallel.dp import GradSync
+
+            self.grad_sync = GradSync(process_group, world)
+            self.grad_sync.broadcast_params([self.generator, self.critic])
+
+    # ------------------------------------------------------------------------------------
+    def _batch(self, B):
+        real = self.rng.sample_windows(self.dataset, B, out_dtype=self.dtype)
+        noise = self.rng.normal((B, self.cfg.window, self.cfg.features), dtype=self.dtype)
+        return real, noise
+
+    def _sync(self, model):
+        if self.grad_sync is not None:
+            self.grad_sync.all_reduce_(model.flat.grad)
+
+    def _apply(self, model, clip=0.0):
+        self._sync(model)
+        self.opt.apply(model.flat, clip=clip)
+        model.zero_grad()
+
+    # ---- critic losses --------------------------------------------------------------------
+    def _bce_step(self, x, label: float):
+        C = self.critic
+        p, tape = C.efwd(x, save=True)
+        pf = p.to(self._acc)
+        n = pf.numel()
+        o = pf.clamp(R.KERAS_EPS, 1 - R.KERAS_EPS)
+        loss = -(label * torch.log(o + R.KERAS_EPS) + (1 - label) * torch.log(1 - o + R.KERAS_EPS)).mean()
+        inside = ((pf > R.KERAS_EPS) & (pf < 1 - R.KERAS_EPS)).to(pf.dtype)
+        dp = -(label / (o + R.KERAS_EPS) - (1 - label) / (1 - o + R.KERAS_EPS)) * inside / n
+        C.ebwd(tape, dp.to(p.dtype))
+        self._apply(C)
+        return loss
+
+    def _wgan_step(self, x, label: float, clip: float):
+        C = self.critic
+        s, tape = C.efwd(x, save=True)
+        loss = label * s.to(self._acc).mean()
+        ds = torch.full_like(s, label / s.numel())
+        C.ebwd(tape, ds)
+        self._apply(C, clip=clip)
+        return loss
+
+    def _gp_step(self, real, noise):
+        fake = self.generator.predict(noise)
+        alpha = self.rng.uniform((real.shape[0],))
+        out = self.critic_gp_grads(real, fake, alpha)
+        self._apply(self.critic)
+        return out
+
+    def critic_gp_grads(self, real, fake, alpha):
+        """Accumulate d/dtheta_C of W(real,-1) + W(fake,+1) + lambda*GP(x_hat) into C.flat.grad."""
+        C = self.critic
+        B = real.shape[0]
+        xh = Fn.interpolate(real, fake, alpha)
+        # W terms on [real; fake]
+        xrf = torch.cat([real, fake], 0)
+        s, tape = C.efwd(xrf, save=True)
+        ds = torch.empty_like(s)
+        ds[:B] = -1.0 / B
+        ds[B:] = 1.0 / B
+        C.ebwd(tape, ds)
+        # gradient penalty: g = dD/dx_hat (input gradient only), v = dGP/dg, then the
+        # theta-gradient of <v, g> as reverse-over-tangent
+        sh, tape_h = C.efwd(xh, save=True)
+        g = C.ebwd(tape_h, torch.ones_like(sh), need_dx=True, wgrad=False)
+        pen, v = Fn.gp_coef(g, self.gp_weight)
+        sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
+        C.etbwd(tape_h, ttape, None, torch.ones_like(sd))
+        sf = s.to(self._acc)
+        w_real = -sf[:B].mean()
+        w_fake = sf[B:].mean()
+        return torch.stack([w_real + w_fake + self.gp_weight * pen, w_real, w_fake, pen])
+
+    # ---- generator ------------------------------------------------------------------------
+    def _generator_step(self, noise):
+        loss = self.generator_grads(noise)
+        self._apply(self.generator)
+        return loss
+
+    def generator_grads(self, noise):
+        """Accumulate d/dtheta_G of the generator loss through the frozen critic."""
+        G, C = self.generator, self.critic
+        fake, tg = G.efwd(noise, save=True)
+        s, tc = C.efwd(fake, save=True)
+        if self.cfg.loss == "gan":
+            pf = s.to(self._acc)
+            n = pf.numel()
+            o = pf.clamp(R.KERAS_EPS, 1 - R.KERAS_EPS)
+            loss = -torch.log(o + R.KERAS_EPS).mean()
+            inside = ((pf > R.KERAS_EPS) & (pf < 1 - R.KERAS_EPS)).to(pf.dtype)
+            ds = (-(1.0 / (o + R.KERAS_EPS)) * inside / n).to(s.dtype)
+        else:
+            loss = -s.to(self._acc).mean()
+            ds = torch.full_like(s, -1.0 / s.numel())
+        dfake = C.ebwd(tc, ds, need_dx=True, wgrad=False)
+        G.ebwd(tg, dfake)
+        return loss
+
+    # ---- one reference "epoch" (= iteration) ----------------------------------------------------
+    @torch.no_grad()
+    def train_step(self):
+        cfg, B = self.cfg, self.cfg.batch_size
+        if cfg.loss == "gan":
+            real, noise = self._batch(B)
+            fake = self.generator.predict(noise)
+            lr_ = self._bce_step(real, 1.0)
+            lf_ = self._bce_step(fake, 0.0)
+            d = 0.5 * (lr_ + lf_)
+            self._d_acc = torch.stack([d, lr_, lf_, torch.zeros_like(d)])
+            noise2 = self.rng.normal((B, cfg.window, cfg.features), dtype=self.dtype)
+            self._g_acc = self._generator_step(noise2).reshape(1)
+        elif cfg.loss == "wgan":
+            for _ in range(self.n_critic):
+                real, noise = self._batch(B)
+                fake = self.generator.predict(noise)
+                lr_ = self._wgan_step(real, -1.0, 0.0)
+                lf_ = self._wgan_step(fake, 1.0, self.clip)
+                self._d_acc = torch.stack([0.5 * (lr_ + lf_), lr_, lf_, torch.zeros_like(lr_)])
+            self._g_acc = self._generator_step(noise).reshape(1)
+        else:
+            for _ in range(self.n_critic):
+                real, noise = self._batch(B)
+                self._d_acc = self._gp_step(real, noise)
+            self._g_acc = self._generator_step(noise).reshape(1)
+        self.iteration += 1
+
+    def losses(self) -> dict:
+        d = self._d_acc.detach().float().cpu().numpy()
+        return {"iteration": self.iteration, "d_loss": float(d[0]), "d_real": float(d[1]), "d_fake": float(d[2]),
+                "gp": float(d[3]), "g_loss": float(self._g_acc.detach().float().cpu()[0])}
+
+    def windows_per_iteration(self) -> int:
+        """Windows consumed per iteration on this rank (SURVEY §6 seq/s definition)."""
+        B = self.cfg.batch_size
+        nc = 2 if self.cfg.loss == "gan" else self.n_critic
+        return nc * B + B
+
+    def train(self, epochs: int | None = None, log=None, verbose: bool = True):
+        epochs = self.cfg.epochs if epochs is None else epochs
+        t0 = time.time()
+        hist = []
+        for ep in range(epochs):
+            self.train_step()
+            if (ep + 1) % self.cfg.log_every == 0 or ep == epochs - 1:
+                rec = self.losses()
+                rec["elapsed_s"] = time.time() - t0
+                hist.append(rec)
+                if log is not None:
+                    log(rec)
+                elif verbose and self.rank == 0:
+                    print("%d [D loss: %f] [G loss: %f]" % (ep, rec["d_loss"], rec["g_loss"]))
+        return hist
+
+    # ---- generation ---------------------------------------------------------------------------
+    @torch.no_grad()
+    def generate(self, n: int, window: int | None = None, batch: int = 4096, seed: int | None = None) -> np.ndarray:
+        """N(0,1) noise -> generator windows; LSTM generators accept any window length."""
+        T = window or self.cfg.window
+        rng = DeviceRNG(self.cfg.seed if seed is None else seed, self.device, stream=10_000 + self.rank)
+        out = []
+        for s in range(0, n, batch):
+            b = min(batch, n - s)
+            z = rng.normal((b, T, self.cfg.features), dtype=self.dtype)
+            out.append(self.generator.predict(z).float().cpu())
+        return torch.cat(out).numpy()

@@ -1,0 +1,50 @@
+"""Shared pytest setup.
+
+* ``gpu`` marker: tests that need a real MI355X (run with ``-m gpu`` on the GPU box).
+* ``data`` fixture: the reference dataset (cleaned_data + raw data/) if present; tests that
+  need it skip when it is absent (e.g. on the GPU box, where only the repo snapshot exists).
+"""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import hfrep  # noqa: E402  (registers the package)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD MI355X GPU (gfx950) and the native kernel library")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+@pytest.fixture(scope="session")
+def data_root():
+    from hfrep.data.io import data_root as _dr
+
+    r = _dr()
+    if r is None or not os.path.isdir(os.path.join(r, "data")):
+        pytest.skip("reference dataset not available")
+    return r
+
+
+@pytest.fixture(scope="session")
+def cleaned(data_root):
+    from hfrep.data.io import load_cleaned
+
+    return load_cleaned(data_root)
+
+
+@pytest.fixture
+def cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from hfrep.ops import _native
+
+    _native.native()  # must load on a GPU box
+    return torch.device("cuda")

@@ -1,0 +1,133 @@
+"""Explicit differentiation engine vs the autograd oracle (fp64, CPU).
+
+The trainers never build autograd graphs: gradients come from hand-derived reverse passes and,
+for the WGAN-GP critic, a reverse-over-tangent Hessian-vector product.  These tests pin every
+model of the zoo against ``torch.autograd`` (double backward for the gradient penalty, the
+semantics of ``K.gradients`` in GAN/MTSS_WGAN_GP.py:205).
+"""
+import numpy as np
+import pytest
+import torch
+
+from hfrep.models import gan as zoo
+from hfrep.ops import reference as R
+from hfrep.train.gan_trainer import GANConfig, GANTrainer
+
+T, F, B = 6, 5, 4
+KEYS = list(zoo.ZOO.keys())
+
+
+def _trainer(arch, loss, **kw):
+    cfg = GANConfig(arch=arch, loss=loss, window=T, features=F, batch_size=B, hidden=7, dtype="float64", **kw)
+    ds = np.random.RandomState(0).rand(20, T, F)
+    tr = GANTrainer(cfg, ds, param_dtype=torch.float64)
+    # perturb biases/LN params so every code path is exercised with non-trivial values
+    with torch.no_grad():
+        for m in (tr.generator, tr.critic):
+            m.flat.add_(0.05 * torch.randn(m.flat.shape, dtype=torch.float64, generator=torch.Generator().manual_seed(5)))
+    return tr
+
+
+def _inputs(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    real = torch.rand(B, T, F, dtype=torch.float64, generator=g)
+    noise = torch.randn(B, T, F, dtype=torch.float64, generator=g)
+    alpha = torch.rand(B, dtype=torch.float64, generator=g)
+    return real, noise, alpha
+
+
+@pytest.mark.parametrize("key", [k for k in KEYS if zoo.ZOO[k].loss == "wgan_gp"])
+def test_gp_critic_gradient_matches_double_backward(key):
+    tr = _trainer(*key)
+    C, G = tr.critic, tr.generator
+    real, noise, alpha = _inputs()
+    with torch.no_grad():
+        fake = G.predict(noise)
+    C.zero_grad()
+    with torch.no_grad():
+        losses = tr.critic_gp_grads(real, fake, alpha)
+    explicit = C.flat.grad.clone()
+
+    C.flat.grad = None
+    xh = (alpha[:, None, None] * real + (1 - alpha[:, None, None]) * fake).requires_grad_(True)
+    s_r, s_f = C(real), C(fake)
+    s_h = C(xh)
+    g, = torch.autograd.grad(s_h.sum(), xh, create_graph=True)
+    gp = R.gradient_penalty_from_grad(g)
+    L = -s_r.mean() + s_f.mean() + tr.gp_weight * gp
+    oracle, = torch.autograd.grad(L, C.flat)
+    C.flat.grad = torch.zeros_like(C.flat)
+    torch.testing.assert_close(explicit, oracle, rtol=1e-9, atol=1e-11)
+    assert abs(losses[0].item() - L.item()) < 1e-10
+
+
+@pytest.mark.parametrize("key", KEYS)
+def test_generator_gradient_matches_autograd(key):
+    tr = _trainer(*key)
+    C, G = tr.critic, tr.generator
+    _, noise, _ = _inputs(1)
+    G.zero_grad()
+    with torch.no_grad():
+        loss = tr.generator_grads(noise)
+    explicit = G.flat.grad.clone()
+    G.flat.grad = None
+    s = C(G(noise))
+    L = R.binary_crossentropy(torch.ones(B, 1, dtype=torch.float64), s) if key[1] == "gan" else -s.mean()
+    oracle, = torch.autograd.grad(L, G.flat)
+    G.flat.grad = torch.zeros_like(G.flat)
+    C.flat.grad = torch.zeros_like(C.flat)
+    torch.testing.assert_close(explicit, oracle, rtol=1e-9, atol=1e-11)
+    assert abs(loss.item() - L.item()) < 1e-10
+
+
+@pytest.mark.parametrize("key", [k for k in KEYS if zoo.ZOO[k].loss in ("gan", "wgan")])
+def test_critic_first_order_gradient(key):
+    tr = _trainer(*key)
+    C = tr.critic
+    real, _, _ = _inputs(2)
+    for label in (1.0, 0.0) if key[1] == "gan" else (-1.0, 1.0):
+        C.zero_grad()
+        s, tape = C.efwd(real, save=True)
+        if key[1] == "gan":
+            o = s.clamp(R.KERAS_EPS, 1 - R.KERAS_EPS)
+            inside = ((s > R.KERAS_EPS) & (s < 1 - R.KERAS_EPS)).double()
+            ds = -(label / (o + R.KERAS_EPS) - (1 - label) / (1 - o + R.KERAS_EPS)) * inside / s.numel()
+        else:
+            ds = torch.full_like(s, label / s.numel())
+        with torch.no_grad():
+            C.ebwd(tape, ds)
+        explicit = C.flat.grad.clone()
+        C.flat.grad = None
+        s2 = C(real)
+        y = torch.full((B, 1), label, dtype=torch.float64)
+        L = R.binary_crossentropy(y, s2) if key[1] == "gan" else R.wasserstein_loss(y, s2)
+        oracle, = torch.autograd.grad(L, C.flat)
+        C.flat.grad = torch.zeros_like(C.flat)
+        torch.testing.assert_close(explicit, oracle, rtol=1e-9, atol=1e-11)
+
+
+def test_param_counts_match_reference():
+    # SURVEY §2.2 table, T=48, F=35
+    expect = {("mlp", "gan"): (17635, 13801), ("mlp", "wgan"): (17635, 14201), ("mlp", "wgan_gp"): (17635, 18501),
+              ("lstm", "gan"): (138735, 134901), ("lstm", "wgan"): (138735, 135301),
+              ("lstm", "wgan_gp"): (138735, 139601)}
+    for key, (g, c) in expect.items():
+        e = zoo.ZOO[key]
+        assert e.generator(48, 35).count_params() == g, key
+        assert e.critic(48, 35).count_params() == c, key
+    # production generator / north-star config
+    assert zoo.lstm_generator(168, 36, lrelu_after_first=True).count_params() == 139236
+    assert zoo.lstm_critic_gp(168, 36).count_params() == 152001
+    assert zoo.lstm_generator(24, 32).count_params() == 137232
+    assert zoo.lstm_critic_gp(24, 32).count_params() == 136001
+
+
+def test_keras_init_semantics():
+    m = zoo.lstm_critic_gp(8, 3, hidden=5)
+    U = m.view(m.layers[0], "recurrent_kernel").double()
+    # orthogonal (H, 4H): rows orthonormal
+    torch.testing.assert_close(U @ U.t(), torch.eye(5, dtype=torch.float64), atol=1e-6, rtol=0)
+    b = m.view(m.layers[0], "bias")
+    assert torch.all(b[5:10] == 1) and torch.all(b[:5] == 0) and torch.all(b[10:] == 0)
+    names = [n for n, _ in m.named_weights()]
+    assert names[0].endswith("/kernel:0") and "lstm_cell" in names[1]
