@@ -1,10 +1,10 @@
 // torch op registrations for the hfrep gfx950 kernel library (namespace torch.ops.hfrep).
 //
-// Every op validates device/dtype/contiguity on the host, then launches on the current
-// HIP stream of the tensor's device, so ops are capturable into hipGraphs and compose with
-// torch's stream semantics.  Only the CUDA (=HIP on ROCm) dispatch key is implemented: on a
-// CPU tensor the op raises, which is how the Python layer guarantees the native path is the
-// one that runs on a GPU box (it never silently falls back).
+// Every op validates device/dtype/contiguity/shape on the host, allocates outputs through the
+// torch caching allocator (graph-capture safe) and launches on the current HIP stream of the
+// tensor's device, so ops are capturable into hipGraphs and compose with torch stream semantics.
+// Only the CUDA (=HIP on ROCm) dispatch key is implemented: a CPU tensor raises, which is how the
+// Python layer guarantees the native path is the one that runs on a GPU box (no silent fallback).
 #include <torch/extension.h>
 #include <torch/library.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
@@ -14,57 +14,296 @@
 
 namespace {
 
-inline hipStream_t cur_stream(const at::Tensor& t) {
+using at::Tensor;
+using c10::optional;
+
+inline hipStream_t cur_stream(const Tensor& t) {
   return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
 }
 
+#define GUARD(t) c10::hip::HIPGuardMasqueradingAsCUDA _guard((t).device())
+#define CHECK_GPU(t) TORCH_CHECK((t).is_cuda() && (t).is_contiguous(), #t " must be a contiguous GPU tensor")
 #define CHECK_F32(t) TORCH_CHECK((t).is_cuda() && (t).scalar_type() == at::kFloat && (t).is_contiguous(), #t " must be a contiguous fp32 GPU tensor")
 
-void rmsprop_(at::Tensor p, at::Tensor g, at::Tensor ms, double lr, double rho, double eps, double clip,
-              double gscale) {
+inline int dt_of(const Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return hfrep::DT_BF16;
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "hfrep kernels support float32 and bfloat16 activations, got ",
+              t.scalar_type());
+  return hfrep::DT_F32;
+}
+inline void same_dt(const Tensor& a, const Tensor& b) {
+  TORCH_CHECK(a.scalar_type() == b.scalar_type(), "dtype mismatch: ", a.scalar_type(), " vs ", b.scalar_type());
+}
+inline const void* ptr_or_null(const optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+// ------------------------------------------------------------------------------------ GEMM
+Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act) {
+  CHECK_GPU(x); CHECK_F32(W);
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && x.size(1) == W.size(0), "linear: shape mismatch");
+  if (b.has_value()) { CHECK_F32(*b); TORCH_CHECK(b->numel() == W.size(1), "linear: bias size"); }
+  GUARD(x);
+  const int M = x.size(0), K = x.size(1), N = W.size(1);
+  Tensor y = at::empty({M, N}, x.options());
+  hfrep::launch_linear(dt_of(x), x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
+                       y.data_ptr(), M, N, K, 0, (int)act, cur_stream(x));
+  return y;
+}
+
+Tensor linear_dgrad(Tensor dz, Tensor W) {
+  CHECK_GPU(dz); CHECK_F32(W);
+  TORCH_CHECK(dz.dim() == 2 && W.dim() == 2 && dz.size(1) == W.size(1), "linear_dgrad: shape mismatch");
+  GUARD(dz);
+  const int M = dz.size(0), K = dz.size(1), N = W.size(0);
+  Tensor dx = at::empty({M, N}, dz.options());
+  // dx = dz . W^T : W stored (N, K) row-major -> w_trans
+  hfrep::launch_linear(dt_of(dz), dz.data_ptr(), W.data_ptr<float>(), nullptr, dx.data_ptr(), M, N, K, 1, 0,
+                       cur_stream(dz));
+  return dx;
+}
+
+void linear_wgrad_(Tensor x, Tensor dz, Tensor gW, optional<Tensor> gb, int64_t shiftT) {
+  CHECK_GPU(x); CHECK_GPU(dz); same_dt(x, dz);
+  TORCH_CHECK(gW.is_cuda() && gW.scalar_type() == at::kFloat && gW.is_contiguous(), "gW must be contiguous fp32");
+  TORCH_CHECK(x.dim() == 2 && dz.dim() == 2 && x.size(0) == dz.size(0), "wgrad: rows mismatch");
+  TORCH_CHECK(gW.numel() == x.size(1) * dz.size(1), "wgrad: gW size");
+  if (gb.has_value()) { CHECK_F32(*gb); TORCH_CHECK(gb->numel() == dz.size(1), "wgrad: gb size"); }
+  GUARD(x);
+  const int M = x.size(0), K = x.size(1), N = dz.size(1);
+  Tensor ws = at::empty({(int64_t)hfrep::wgrad_workspace_floats(M, K, N)}, x.options().dtype(at::kFloat));
+  hfrep::launch_wgrad(dt_of(x), x.data_ptr(), dz.data_ptr(), gW.data_ptr<float>(),
+                      gb.has_value() ? gb->data_ptr<float>() : nullptr, M, K, N, (int)shiftT, ws.data_ptr<float>(),
+                      cur_stream(x));
+}
+
+// ------------------------------------------------------------------------------------ elementwise
+Tensor act_fwd(Tensor x, int64_t act) {
+  CHECK_GPU(x); GUARD(x);
+  Tensor y = at::empty_like(x);
+  hfrep::launch_act_fwd(dt_of(x), x.data_ptr(), y.data_ptr(), x.numel(), (int)act, cur_stream(x));
+  return y;
+}
+Tensor act_bwd(Tensor dy, Tensor y, int64_t act) {
+  CHECK_GPU(dy); CHECK_GPU(y); same_dt(dy, y);
+  TORCH_CHECK(dy.numel() == y.numel(), "act_bwd: size");
+  GUARD(dy);
+  Tensor dx = at::empty_like(dy);
+  hfrep::launch_act_bwd(dt_of(dy), dy.data_ptr(), y.data_ptr(), dx.data_ptr(), dy.numel(), (int)act, cur_stream(dy));
+  return dx;
+}
+Tensor act_tangent_bwd(Tensor dyd, Tensor y, Tensor zd, int64_t act) {
+  CHECK_GPU(dyd); CHECK_GPU(y); CHECK_GPU(zd); same_dt(dyd, y); same_dt(dyd, zd);
+  TORCH_CHECK(dyd.numel() == y.numel() && y.numel() == zd.numel(), "act_tangent_bwd: size");
+  GUARD(dyd);
+  Tensor out = at::empty_like(dyd);
+  hfrep::launch_act_tangent_bwd(dt_of(dyd), dyd.data_ptr(), y.data_ptr(), zd.data_ptr(), out.data_ptr(), dyd.numel(),
+                                (int)act, cur_stream(dyd));
+  return out;
+}
+
+// ------------------------------------------------------------------------------------ LSTM
+void check_lstm_U(const Tensor& U, int64_t H) {
+  CHECK_F32(U);
+  TORCH_CHECK(U.dim() == 2 && U.size(0) == H && U.size(1) == 4 * H, "recurrent kernel must be (H, 4H)");
+}
+
+std::tuple<Tensor, Tensor, Tensor> lstm_fwd(Tensor zx, Tensor U, int64_t act, bool save) {
+  CHECK_GPU(zx);
+  TORCH_CHECK(zx.dim() == 3 && zx.size(2) % 4 == 0, "zx must be (B, T, 4H)");
+  const int B = zx.size(0), Tn = zx.size(1), H = zx.size(2) / 4;
+  check_lstm_U(U, H);
+  GUARD(zx);
+  Tensor hs = at::empty({B, Tn, H}, zx.options());
+  Tensor gates = save ? at::empty({B, Tn, 4 * H}, zx.options()) : at::empty({0}, zx.options());
+  Tensor cs = save ? at::empty({B, Tn, H}, zx.options()) : at::empty({0}, zx.options());
+  const bool ok = hfrep::launch_lstm_fwd(dt_of(zx), zx.data_ptr(), U.data_ptr<float>(), hs.data_ptr(),
+                                         save ? gates.data_ptr() : nullptr, save ? cs.data_ptr() : nullptr, B, Tn, H,
+                                         (int)act, cur_stream(zx));
+  TORCH_CHECK(ok, "lstm_fwd: hidden size ", H, " not instantiated (supported: 100, 64, 32)");
+  return {hs, gates, cs};
+}
+
+Tensor lstm_bwd(Tensor dH, Tensor gates, Tensor cs, Tensor U, int64_t act) {
+  CHECK_GPU(dH); CHECK_GPU(gates); CHECK_GPU(cs); same_dt(dH, gates); same_dt(dH, cs);
+  const int B = gates.size(0), Tn = gates.size(1), H = gates.size(2) / 4;
+  TORCH_CHECK(dH.sizes() == cs.sizes() && cs.size(2) == H, "lstm_bwd: shapes");
+  check_lstm_U(U, H);
+  GUARD(dH);
+  Tensor dZ = at::empty_like(gates);
+  const bool ok = hfrep::launch_lstm_bwd(dt_of(dH), dH.data_ptr(), gates.data_ptr(), cs.data_ptr(),
+                                         U.data_ptr<float>(), dZ.data_ptr(), B, Tn, H, (int)act, cur_stream(dH));
+  TORCH_CHECK(ok, "lstm_bwd: hidden size ", H, " not instantiated");
+  return dZ;
+}
+
+std::tuple<Tensor, Tensor, Tensor> lstm_tfwd(Tensor dzx, Tensor gates, Tensor cs, Tensor U, int64_t act) {
+  CHECK_GPU(dzx); CHECK_GPU(gates); CHECK_GPU(cs); same_dt(dzx, gates); same_dt(dzx, cs);
+  TORCH_CHECK(dzx.sizes() == gates.sizes(), "lstm_tfwd: shapes");
+  const int B = gates.size(0), Tn = gates.size(1), H = gates.size(2) / 4;
+  check_lstm_U(U, H);
+  GUARD(dzx);
+  Tensor hds = at::empty({B, Tn, H}, dzx.options());
+  Tensor zds = at::empty_like(gates);
+  Tensor cds = at::empty({B, Tn, H}, dzx.options());
+  const bool ok = hfrep::launch_lstm_tfwd(dt_of(dzx), dzx.data_ptr(), gates.data_ptr(), cs.data_ptr(),
+                                          U.data_ptr<float>(), hds.data_ptr(), zds.data_ptr(), cds.data_ptr(), B, Tn,
+                                          H, (int)act, cur_stream(dzx));
+  TORCH_CHECK(ok, "lstm_tfwd: hidden size ", H, " not instantiated");
+  return {hds, zds, cds};
+}
+
+std::tuple<Tensor, Tensor> lstm_tbwd(optional<Tensor> dH, Tensor dHd, Tensor gates, Tensor cs, Tensor zds, Tensor cds,
+                                     Tensor U, int64_t act) {
+  CHECK_GPU(dHd); CHECK_GPU(gates); CHECK_GPU(cs); CHECK_GPU(zds); CHECK_GPU(cds);
+  same_dt(dHd, gates); same_dt(dHd, zds); same_dt(dHd, cds);
+  if (dH.has_value()) { CHECK_GPU(*dH); same_dt(*dH, dHd); }
+  const int B = gates.size(0), Tn = gates.size(1), H = gates.size(2) / 4;
+  check_lstm_U(U, H);
+  GUARD(dHd);
+  Tensor dZ = at::empty_like(gates), dZd = at::empty_like(gates);
+  const bool ok = hfrep::launch_lstm_tbwd(dt_of(dHd), ptr_or_null(dH), dHd.data_ptr(), gates.data_ptr(),
+                                          cs.data_ptr(), zds.data_ptr(), cds.data_ptr(), U.data_ptr<float>(),
+                                          dZ.data_ptr(), dZd.data_ptr(), B, Tn, H, (int)act, cur_stream(dHd));
+  TORCH_CHECK(ok, "lstm_tbwd: hidden size ", H, " not instantiated");
+  return {dZ, dZd};
+}
+
+// ------------------------------------------------------------------------------------ LayerNorm
+std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, double eps) {
+  CHECK_GPU(x); CHECK_F32(gamma); CHECK_F32(beta);
+  const int D = x.size(-1);
+  TORCH_CHECK(D <= 256 && gamma.numel() == D && beta.numel() == D, "layernorm: D <= 256 and param sizes");
+  GUARD(x);
+  const int64_t rows = x.numel() / D;
+  Tensor y = at::empty_like(x), xhat = at::empty_like(x);
+  std::vector<int64_t> rs(x.sizes().begin(), x.sizes().end() - 1);
+  rs.push_back(1);
+  Tensor rstd = at::empty(rs, x.options().dtype(at::kFloat));
+  hfrep::launch_layernorm_fwd(dt_of(x), x.data_ptr(), gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
+                              xhat.data_ptr(), rstd.data_ptr<float>(), rows, D, (float)eps, cur_stream(x));
+  return {y, xhat, rstd};
+}
+
+Tensor layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, optional<Tensor> ggamma,
+                      optional<Tensor> gbeta) {
+  CHECK_GPU(dy); CHECK_GPU(xhat); same_dt(dy, xhat); CHECK_F32(rstd); CHECK_F32(gamma);
+  const int D = dy.size(-1);
+  TORCH_CHECK(D <= 256, "layernorm: D <= 256");
+  float* gg = nullptr; float* gbp = nullptr;
+  if (ggamma.has_value()) { CHECK_F32(*ggamma); gg = ggamma->data_ptr<float>(); }
+  if (gbeta.has_value()) { CHECK_F32(*gbeta); gbp = gbeta->data_ptr<float>(); }
+  GUARD(dy);
+  Tensor dx = at::empty_like(dy);
+  hfrep::launch_layernorm_bwd(dt_of(dy), dy.data_ptr(), xhat.data_ptr(), rstd.data_ptr<float>(),
+                              gamma.data_ptr<float>(), dx.data_ptr(), gg, gbp, dy.numel() / D, D, cur_stream(dy));
+  return dx;
+}
+
+// ------------------------------------------------------------------------------------ WGAN-GP helpers
+std::tuple<Tensor, Tensor> gp_coef(Tensor g, double weight) {
+  CHECK_GPU(g); GUARD(g);
+  const int B = g.size(0);
+  const int64_t D = g.numel() / B;
+  Tensor v = at::empty_like(g);
+  Tensor pen = at::zeros({}, g.options().dtype(at::kFloat));
+  hfrep::launch_gp_coef(dt_of(g), g.data_ptr(), v.data_ptr(), pen.data_ptr<float>(), B, D, (float)weight,
+                        cur_stream(g));
+  return {pen, v};
+}
+
+Tensor interpolate(Tensor real, Tensor fake, Tensor alpha) {
+  CHECK_GPU(real); CHECK_GPU(fake); same_dt(real, fake); CHECK_F32(alpha);
+  TORCH_CHECK(real.sizes() == fake.sizes() && alpha.numel() == real.size(0), "interpolate: shapes");
+  GUARD(real);
+  Tensor out = at::empty_like(real);
+  const int B = real.size(0);
+  hfrep::launch_interpolate(dt_of(real), real.data_ptr(), fake.data_ptr(), alpha.data_ptr<float>(), out.data_ptr(), B,
+                            real.numel() / B, cur_stream(real));
+  return out;
+}
+
+// ------------------------------------------------------------------------------------ RNG / sampling
+void philox_fill_(Tensor out, int64_t seed, Tensor ctr, int64_t dist) {
+  CHECK_GPU(out);
+  TORCH_CHECK(ctr.is_cuda() && ctr.scalar_type() == at::kLong && ctr.numel() == 1, "ctr must be a 1-element int64 GPU tensor");
+  GUARD(out);
+  hfrep::launch_philox_fill(dt_of(out), out.data_ptr(), out.numel(), (uint64_t)seed, ctr.data_ptr<int64_t>(), (int)dist,
+                            cur_stream(out));
+}
+
+Tensor sample_windows(Tensor data, int64_t batch, int64_t seed, Tensor ctr, at::ScalarType out_dtype) {
+  CHECK_F32(data);
+  TORCH_CHECK(ctr.is_cuda() && ctr.scalar_type() == at::kLong && ctr.numel() == 1, "ctr must be a 1-element int64 GPU tensor");
+  GUARD(data);
+  std::vector<int64_t> shape(data.sizes().begin(), data.sizes().end());
+  shape[0] = batch;
+  Tensor out = at::empty(shape, data.options().dtype(out_dtype));
+  const int64_t N = data.size(0), D = data.numel() / N;
+  hfrep::launch_sample_windows(dt_of(out), data.data_ptr<float>(), N, D, out.data_ptr(), (int)batch, (uint64_t)seed,
+                               ctr.data_ptr<int64_t>(), cur_stream(data));
+  return out;
+}
+
+// ------------------------------------------------------------------------------------ optimizers
+void rmsprop_(Tensor p, Tensor g, Tensor ms, double lr, double rho, double eps, double clip, double gscale) {
   CHECK_F32(p); CHECK_F32(g); CHECK_F32(ms);
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == ms.numel(), "rmsprop_: size mismatch");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
+  GUARD(p);
   hfrep::launch_rmsprop(p.data_ptr<float>(), g.data_ptr<float>(), ms.data_ptr<float>(), p.numel(), (float)lr,
                         (float)rho, (float)eps, (float)clip, (float)gscale, cur_stream(p));
 }
 
-void adam_(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor step, double lr, double b1, double b2,
-           double eps, double clip, double gscale) {
+void adam_(Tensor p, Tensor g, Tensor m, Tensor v, Tensor step, double lr, double b1, double b2, double eps,
+           double clip, double gscale) {
   CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v); CHECK_F32(step);
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam_: size mismatch");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
+  GUARD(p);
   hfrep::launch_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), p.numel(),
                      step.data_ptr<float>(), (float)lr, (float)b1, (float)b2, (float)eps, (float)clip, (float)gscale,
                      cur_stream(p));
 }
 
-void nadam_(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor step, at::Tensor m_cache, double lr,
-            double b1, double b2, double eps, double gscale) {
+void nadam_(Tensor p, Tensor g, Tensor m, Tensor v, Tensor step, Tensor m_cache, double lr, double b1, double b2,
+            double eps, double gscale) {
   CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v); CHECK_F32(step); CHECK_F32(m_cache);
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
+  GUARD(p);
   hfrep::launch_nadam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), p.numel(),
                       step.data_ptr<float>(), m_cache.data_ptr<float>(), (float)lr, (float)b1, (float)b2, (float)eps,
                       (float)gscale, cur_stream(p));
 }
 
-void step_advance_(at::Tensor step, c10::optional<at::Tensor> m_cache, double b1) {
+void step_advance_(Tensor step, optional<Tensor> m_cache, double b1) {
   CHECK_F32(step);
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(step.device());
+  GUARD(step);
   float* mc = nullptr;
   if (m_cache.has_value()) { CHECK_F32(*m_cache); mc = m_cache->data_ptr<float>(); }
   hfrep::launch_step_advance(step.data_ptr<float>(), mc, (float)b1, cur_stream(step));
 }
 
-void clip_(at::Tensor p, double c) {
+void clip_(Tensor p, double c) {
   CHECK_F32(p);
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
+  GUARD(p);
   hfrep::launch_clip(p.data_ptr<float>(), p.numel(), (float)c, cur_stream(p));
 }
 
 }  // namespace
 
 TORCH_LIBRARY(hfrep, m) {
+  m.def("linear(Tensor x, Tensor W, Tensor? b, int act) -> Tensor");
+  m.def("linear_dgrad(Tensor dz, Tensor W) -> Tensor");
+  m.def("linear_wgrad_(Tensor x, Tensor dz, Tensor(a!) gW, Tensor(b!)? gb, int shiftT=0) -> ()");
+  m.def("act_fwd(Tensor x, int act) -> Tensor");
+  m.def("act_bwd(Tensor dy, Tensor y, int act) -> Tensor");
+  m.def("act_tangent_bwd(Tensor dyd, Tensor y, Tensor zd, int act) -> Tensor");
+  m.def("lstm_fwd(Tensor zx, Tensor U, int act, bool save) -> (Tensor, Tensor, Tensor)");
+  m.def("lstm_bwd(Tensor dH, Tensor gates, Tensor cs, Tensor U, int act) -> Tensor");
+  m.def("lstm_tfwd(Tensor dzx, Tensor gates, Tensor cs, Tensor U, int act) -> (Tensor, Tensor, Tensor)");
+  m.def("lstm_tbwd(Tensor? dH, Tensor dHd, Tensor gates, Tensor cs, Tensor zds, Tensor cds, Tensor U, int act) -> (Tensor, Tensor)");
+  m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, Tensor(a!)? ggamma, Tensor(b!)? gbeta) -> Tensor");
+  m.def("gp_coef(Tensor g, float weight) -> (Tensor, Tensor)");
+  m.def("interpolate(Tensor real, Tensor fake, Tensor alpha) -> Tensor");
+  m.def("philox_fill_(Tensor(a!) out, int seed, Tensor(b!) ctr, int dist) -> ()");
+  m.def("sample_windows(Tensor data, int batch, int seed, Tensor(a!) ctr, ScalarType out_dtype) -> Tensor");
   m.def("rmsprop_(Tensor(a!) p, Tensor g, Tensor(b!) ms, float lr, float rho, float eps, float clip, float gscale) -> ()");
   m.def("adam_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, float lr, float b1, float b2, float eps, float clip, float gscale) -> ()");
   m.def("nadam_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor m_cache, float lr, float b1, float b2, float eps, float gscale) -> ()");
@@ -73,6 +312,22 @@ TORCH_LIBRARY(hfrep, m) {
 }
 
 TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
+  m.impl("linear", &linear);
+  m.impl("linear_dgrad", &linear_dgrad);
+  m.impl("linear_wgrad_", &linear_wgrad_);
+  m.impl("act_fwd", &act_fwd);
+  m.impl("act_bwd", &act_bwd);
+  m.impl("act_tangent_bwd", &act_tangent_bwd);
+  m.impl("lstm_fwd", &lstm_fwd);
+  m.impl("lstm_bwd", &lstm_bwd);
+  m.impl("lstm_tfwd", &lstm_tfwd);
+  m.impl("lstm_tbwd", &lstm_tbwd);
+  m.impl("layernorm_fwd", &layernorm_fwd);
+  m.impl("layernorm_bwd_", &layernorm_bwd_);
+  m.impl("gp_coef", &gp_coef);
+  m.impl("interpolate", &interpolate);
+  m.impl("philox_fill_", &philox_fill_);
+  m.impl("sample_windows", &sample_windows);
   m.impl("rmsprop_", &rmsprop_);
   m.impl("adam_", &adam_);
   m.impl("nadam_", &nadam_);

@@ -6,6 +6,49 @@
 
 namespace hfrep {
 
+// storage dtype codes shared by all launchers
+enum DType : int { DT_F32 = 0, DT_BF16 = 1 };
+
+// ---- lstm.hip (return false if H is not an instantiated hidden size) ----
+bool launch_lstm_fwd(int dt, const void* zx, const float* U, void* hs, void* gates, void* cs, int B, int Tn, int H,
+                     int act, hipStream_t s);
+bool launch_lstm_bwd(int dt, const void* dH, const void* gates, const void* cs, const float* U, void* dZ, int B,
+                     int Tn, int H, int act, hipStream_t s);
+bool launch_lstm_tfwd(int dt, const void* dzx, const void* gates, const void* cs, const float* U, void* hds,
+                      void* zds, void* cds, int B, int Tn, int H, int act, hipStream_t s);
+bool launch_lstm_tbwd(int dt, const void* dH, const void* dHd, const void* gates, const void* cs, const void* zds,
+                      const void* cds, const float* U, void* dZ, void* dZd, int B, int Tn, int H, int act,
+                      hipStream_t s);
+
+// ---- gemm.hip ----
+// C[M,N] = act(A[M,K] . op(W) + bias);  op(W) = W (K,N) or W^T when w_trans (W stored (N,K)).
+// A and C share the activation dtype `dt`; W and bias are fp32 (converted while staging).
+void launch_linear(int dt, const void* A, const float* W, const float* bias, void* C, int M, int N, int K,
+                   int w_trans, int act, hipStream_t s);
+// gW[K,N] += sum_m X[m,:]^T D[m,:]  (and gb[N] += sum_m D[m,:] when gb != nullptr).
+// shiftT > 0: X row m is replaced by row m-1, and by zeros where m % shiftT == 0 (h_{t-1} trick).
+// Uses split-M fp32 slabs in `ws` (size >= wgrad_workspace_floats) and a reduce launch.
+size_t wgrad_workspace_floats(int M, int K, int N);
+void launch_wgrad(int dt, const void* X, const void* D, float* gW, float* gb, int M, int K, int N, int shiftT,
+                  float* ws, hipStream_t s);
+
+// ---- misc.hip ----
+void launch_act_fwd(int dt, const void* x, void* y, int64_t n, int act, hipStream_t s);
+void launch_act_bwd(int dt, const void* dy, const void* y, void* dx, int64_t n, int act, hipStream_t s);
+void launch_act_tangent_bwd(int dt, const void* dyd, const void* y, const void* zd, void* out, int64_t n, int act,
+                            hipStream_t s);
+void launch_layernorm_fwd(int dt, const void* x, const float* gamma, const float* beta, void* y, void* xhat,
+                          float* rstd, int64_t rows, int D, float eps, hipStream_t s);
+void launch_layernorm_bwd(int dt, const void* dy, const void* xhat, const float* rstd, const float* gamma,
+                          void* dx, float* ggamma, float* gbeta, int64_t rows, int D, hipStream_t s);
+void launch_gp_coef(int dt, const void* g, void* v, float* pen, int B, int64_t D, float weight, hipStream_t s);
+void launch_interpolate(int dt, const void* real, const void* fake, const float* alpha, void* out, int B,
+                        int64_t D, hipStream_t s);
+void launch_philox_fill(int dt, void* out, int64_t n, uint64_t seed, int64_t* ctr, int dist, hipStream_t s);
+void launch_sample_windows(int dt, const float* data, int64_t N, int64_t D, void* out, int B, uint64_t seed,
+                           int64_t* ctr, hipStream_t s);
+void launch_cast(int dt_in, const void* in, int dt_out, void* out, int64_t n, hipStream_t s);
+
 // ---- optim.hip ----
 void launch_rmsprop(float* p, const float* g, float* ms, int64_t n, float lr, float rho, float eps, float clip,
                     float gscale, hipStream_t s);

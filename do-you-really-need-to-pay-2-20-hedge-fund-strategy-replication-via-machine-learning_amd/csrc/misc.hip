@@ -1,0 +1,285 @@
+// Bandwidth-bound kernels of the GAN training step (gfx950): activations, LayerNorm,
+// gradient-penalty coefficient, interpolation, in-kernel Philox RNG and window sampling.
+//
+// LayerNorm follows Keras (axis -1, eps 1e-3: GAN/MTSS_WGAN_GP.py:225,228); the GP coefficient
+// kernel is the per-sample ||dD/dx||_2 reduction of GAN/MTSS_WGAN_GP.py:201-216 fused with the
+// derivative of lambda*mean((1-||g||)^2) w.r.t. g; interpolation is RandomWeightedAverage
+// (GAN/MTSS_WGAN_GP.py:191-199) with a per-sample alpha of ANY batch size.
+#include "common.h"
+#include "kernels.h"
+
+namespace hfrep {
+
+static inline int ew_grid(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(b, 4096));
+}
+
+// ------------------------------------------------------------------ activations
+template <typename T>
+__global__ void __launch_bounds__(256) act_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n, int act) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    st_f(y + i, act_f(act, ld_f(x + i)));
+}
+template <typename T>
+__global__ void __launch_bounds__(256) act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ dx,
+                                                      int64_t n, int act) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    st_f(dx + i, ld_f(dy + i) * act_dy(act, ld_f(y + i)));
+}
+template <typename T>
+__global__ void __launch_bounds__(256) act_tbwd_kernel(const T* __restrict__ dyd, const T* __restrict__ y,
+                                                       const T* __restrict__ zd, T* __restrict__ out, int64_t n, int act) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    st_f(out + i, ld_f(dyd + i) * act_d2y(act, ld_f(y + i)) * ld_f(zd + i));
+}
+
+void launch_act_fwd(int dt, const void* x, void* y, int64_t n, int act, hipStream_t s) {
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(act_fwd_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y, n, act);
+  else
+    hipLaunchKernelGGL(act_fwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, s, (const float*)x, (float*)y, n, act);
+}
+void launch_act_bwd(int dt, const void* dy, const void* y, void* dx, int64_t n, int act, hipStream_t s) {
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(act_bwd_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)y,
+                       (bf16_t*)dx, n, act);
+  else
+    hipLaunchKernelGGL(act_bwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, s, (const float*)dy, (const float*)y,
+                       (float*)dx, n, act);
+}
+void launch_act_tangent_bwd(int dt, const void* dyd, const void* y, const void* zd, void* out, int64_t n, int act,
+                            hipStream_t s) {
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(act_tbwd_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, s, (const bf16_t*)dyd,
+                       (const bf16_t*)y, (const bf16_t*)zd, (bf16_t*)out, n, act);
+  else
+    hipLaunchKernelGGL(act_tbwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, s, (const float*)dyd, (const float*)y,
+                       (const float*)zd, (float*)out, n, act);
+}
+
+// ------------------------------------------------------------------ LayerNorm (one wave per row)
+template <typename T>
+__global__ void __launch_bounds__(256) layernorm_fwd_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, T* __restrict__ y,
+                                                            T* __restrict__ xhat, float* __restrict__ rstd_out,
+                                                            int64_t rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += wstride) {
+    const T* xr = x + row * D;
+    float s = 0.f;
+    for (int j = lane; j < D; j += 64) s += ld_f(xr + j);
+    const float mu = wave_sum(s) / D;
+    float v = 0.f;
+    for (int j = lane; j < D; j += 64) { const float d = ld_f(xr + j) - mu; v += d * d; }
+    const float rstd = rsqrtf(wave_sum(v) / D + eps);
+    for (int j = lane; j < D; j += 64) {
+      const float xh = (ld_f(xr + j) - mu) * rstd;
+      st_f(xhat + row * D + j, xh);
+      st_f(y + row * D + j, xh * gamma[j] + beta[j]);
+    }
+    if (lane == 0) rstd_out[row] = rstd;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ xhat,
+                                                            const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                            T* __restrict__ dx, float* __restrict__ ggamma,
+                                                            float* __restrict__ gbeta, int64_t rows, int D) {
+  constexpr int MAXJ = 4;  // D <= 256
+  __shared__ float red_g[4 * MAXJ * 64];
+  __shared__ float red_b[4 * MAXJ * 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float pg[MAXJ] = {0.f, 0.f, 0.f, 0.f}, pb[MAXJ] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += wstride) {
+    const T* dyr = dy + row * D;
+    const T* xr = xhat + row * D;
+    float sg = 0.f, sgx = 0.f;
+    float gv[MAXJ], xv[MAXJ], dv[MAXJ];
+#pragma unroll
+    for (int q = 0; q < MAXJ; ++q) {
+      const int j = lane + 64 * q;
+      gv[q] = 0.f; xv[q] = 0.f; dv[q] = 0.f;
+      if (j < D) {
+        dv[q] = ld_f(dyr + j);
+        xv[q] = ld_f(xr + j);
+        gv[q] = dv[q] * gamma[j];
+        sg += gv[q];
+        sgx += gv[q] * xv[q];
+        pg[q] += dv[q] * xv[q];
+        pb[q] += dv[q];
+      }
+    }
+    const float mg = wave_sum(sg) / D, mgx = wave_sum(sgx) / D;
+    const float rs = rstd[row];
+#pragma unroll
+    for (int q = 0; q < MAXJ; ++q) {
+      const int j = lane + 64 * q;
+      if (j < D) st_f(dx + row * D + j, rs * (gv[q] - mg - xv[q] * mgx));
+    }
+  }
+  if (ggamma == nullptr) return;
+  // reduce the 4 waves' partials through LDS, then one atomic per column per workgroup
+#pragma unroll
+  for (int q = 0; q < MAXJ; ++q) {
+    red_g[(wid * MAXJ + q) * 64 + lane] = pg[q];
+    red_b[(wid * MAXJ + q) * 64 + lane] = pb[q];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < D; j += 256) {
+    const int q = j / 64, l = j % 64;
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { a += red_g[(w * MAXJ + q) * 64 + l]; b += red_b[(w * MAXJ + q) * 64 + l]; }
+    atomicAdd(ggamma + j, a);
+    atomicAdd(gbeta + j, b);
+  }
+}
+
+void launch_layernorm_fwd(int dt, const void* x, const float* gamma, const float* beta, void* y, void* xhat,
+                          float* rstd, int64_t rows, int D, float eps, hipStream_t s) {
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 8192));
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(layernorm_fwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, gamma, beta,
+                       (bf16_t*)y, (bf16_t*)xhat, rstd, rows, D, eps);
+  else
+    hipLaunchKernelGGL(layernorm_fwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)x, gamma, beta,
+                       (float*)y, (float*)xhat, rstd, rows, D, eps);
+}
+
+void launch_layernorm_bwd(int dt, const void* dy, const void* xhat, const float* rstd, const float* gamma, void* dx,
+                          float* ggamma, float* gbeta, int64_t rows, int D, hipStream_t s) {
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 2048));
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(layernorm_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)dy,
+                       (const bf16_t*)xhat, rstd, gamma, (bf16_t*)dx, ggamma, gbeta, rows, D);
+  else
+    hipLaunchKernelGGL(layernorm_bwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)dy, (const float*)xhat,
+                       rstd, gamma, (float*)dx, ggamma, gbeta, rows, D);
+}
+
+// ------------------------------------------------------------------ gradient penalty coefficient
+template <typename T>
+__global__ void __launch_bounds__(256) gp_coef_kernel(const T* __restrict__ g, T* __restrict__ v, float* __restrict__ pen,
+                                                      int B, int64_t D, float weight) {
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  const T* gr = g + (int64_t)b * D;
+  float s = 0.f;
+  for (int64_t j = threadIdx.x; j < D; j += 256) { const float x = ld_f(gr + j); s += x * x; }
+  const float nrm = sqrtf(block_sum<4>(s, red));
+  const float one_m = 1.f - nrm;
+  const float scale = -(2.f * weight / B) * one_m / fmaxf(nrm, 1e-30f);
+  for (int64_t j = threadIdx.x; j < D; j += 256) st_f(v + (int64_t)b * D + j, ld_f(gr + j) * scale);
+  if (threadIdx.x == 0) atomicAdd(pen, one_m * one_m / B);
+}
+
+void launch_gp_coef(int dt, const void* g, void* v, float* pen, int B, int64_t D, float weight, hipStream_t s) {
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(gp_coef_kernel<bf16_t>, dim3(B), dim3(256), 0, s, (const bf16_t*)g, (bf16_t*)v, pen, B, D, weight);
+  else
+    hipLaunchKernelGGL(gp_coef_kernel<float>, dim3(B), dim3(256), 0, s, (const float*)g, (float*)v, pen, B, D, weight);
+}
+
+// ------------------------------------------------------------------ interpolation
+template <typename T>
+__global__ void __launch_bounds__(256) interp_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                     const float* __restrict__ alpha, T* __restrict__ out, int64_t D,
+                                                     int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float al = alpha[i / D];
+    st_f(out + i, al * ld_f(a + i) + (1.f - al) * ld_f(b + i));
+  }
+}
+void launch_interpolate(int dt, const void* real, const void* fake, const float* alpha, void* out, int B, int64_t D,
+                        hipStream_t s) {
+  const int64_t n = (int64_t)B * D;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(interp_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, s, (const bf16_t*)real,
+                       (const bf16_t*)fake, alpha, (bf16_t*)out, D, n);
+  else
+    hipLaunchKernelGGL(interp_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, s, (const float*)real,
+                       (const float*)fake, alpha, (float*)out, D, n);
+}
+
+// ------------------------------------------------------------------ Philox RNG
+template <typename T>
+__global__ void __launch_bounds__(256) philox_fill_kernel(T* __restrict__ out, int64_t n, uint64_t seed,
+                                                          const int64_t* __restrict__ ctr, int dist) {
+  const uint64_t base = (uint64_t)ctr[0];
+  const int64_t nq = (n + 3) / 4;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
+    const uint4 r = Philox::gen(seed, base + (uint64_t)q, 0x5EEDu);
+    float v[4];
+    const float u0 = u32_to_unit(r.x), u1 = u32_to_unit(r.y), u2 = u32_to_unit(r.z), u3 = u32_to_unit(r.w);
+    if (dist == 1) {
+      const float ra = sqrtf(-2.f * __logf(u0)), rb = sqrtf(-2.f * __logf(u2));
+      float sa, ca, sb, cb;
+      __sincosf(6.283185307179586f * u1, &sa, &ca);
+      __sincosf(6.283185307179586f * u3, &sb, &cb);
+      v[0] = ra * ca; v[1] = ra * sa; v[2] = rb * cb; v[3] = rb * sb;
+    } else {
+      v[0] = u0; v[1] = u1; v[2] = u2; v[3] = u3;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = q * 4 + k;
+      if (i < n) st_f(out + i, v[k]);
+    }
+  }
+}
+
+__global__ void ctr_advance_kernel(int64_t* ctr, int64_t by) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) ctr[0] += by;
+}
+
+void launch_philox_fill(int dt, void* out, int64_t n, uint64_t seed, int64_t* ctr, int dist, hipStream_t s) {
+  const int64_t nq = (n + 3) / 4;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(philox_fill_kernel<bf16_t>, dim3(ew_grid(nq)), dim3(256), 0, s, (bf16_t*)out, n, seed, ctr, dist);
+  else
+    hipLaunchKernelGGL(philox_fill_kernel<float>, dim3(ew_grid(nq)), dim3(256), 0, s, (float*)out, n, seed, ctr, dist);
+  hipLaunchKernelGGL(ctr_advance_kernel, dim3(1), dim3(64), 0, s, ctr, nq);
+}
+
+// ------------------------------------------------------------------ batch sampling: out[b] = data[randint(N)]
+template <typename T>
+__global__ void __launch_bounds__(256) sample_windows_kernel(const float* __restrict__ data, int64_t N, int64_t D,
+                                                             T* __restrict__ out, uint64_t seed,
+                                                             const int64_t* __restrict__ ctr) {
+  const int b = blockIdx.x;
+  const uint4 r = Philox::gen(seed, (uint64_t)ctr[0] + (uint64_t)b, 0xB47Cu);
+  const uint64_t idx = (((uint64_t)r.x << 32) | r.y) % (uint64_t)N;
+  const float* src = data + (int64_t)idx * D;
+  T* dst = out + (int64_t)b * D;
+  for (int64_t j = threadIdx.x; j < D; j += 256) st_f(dst + j, src[j]);
+}
+
+void launch_sample_windows(int dt, const float* data, int64_t N, int64_t D, void* out, int B, uint64_t seed,
+                           int64_t* ctr, hipStream_t s) {
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(sample_windows_kernel<bf16_t>, dim3(B), dim3(256), 0, s, data, N, D, (bf16_t*)out, seed, ctr);
+  else
+    hipLaunchKernelGGL(sample_windows_kernel<float>, dim3(B), dim3(256), 0, s, data, N, D, (float*)out, seed, ctr);
+  hipLaunchKernelGGL(ctr_advance_kernel, dim3(1), dim3(64), 0, s, ctr, (int64_t)B);
+}
+
+// ------------------------------------------------------------------ dtype cast
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    st_f(out + i, ld_f(in + i));
+}
+void launch_cast(int dt_in, const void* in, int dt_out, void* out, int64_t n, hipStream_t s) {
+  if (dt_in == DT_BF16 && dt_out == DT_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16_t, float>), dim3(ew_grid(n)), dim3(256), 0, s, (const bf16_t*)in, (float*)out, n);
+  else if (dt_in == DT_F32 && dt_out == DT_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16_t>), dim3(ew_grid(n)), dim3(256), 0, s, (const float*)in, (bf16_t*)out, n);
+  else
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(ew_grid(n)), dim3(256), 0, s, (const float*)in, (float*)out, n);
+}
+
+}  // namespace hfrep

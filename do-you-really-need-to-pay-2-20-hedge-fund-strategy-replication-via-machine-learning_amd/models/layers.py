@@ -211,7 +211,7 @@ class LSTM(Layer):
         dZ = Fn.lstm_seq_bwd(dy, ctx["gates"], ctx["cs"], U, self.act_code)
         if wgrad:
             Fn.linear_wgrad_(ctx["x"], dZ, self.g("kernel"), self.g("bias"))
-            Fn.linear_wgrad_(Fn.shift_prev(ctx["hs"]), dZ, self.g("recurrent_kernel"), None)
+            Fn.linear_wgrad_(ctx["hs"], dZ, self.g("recurrent_kernel"), None, shift_T=ctx["hs"].shape[1])
         return Fn.linear_dgrad(dZ, self.p("kernel")) if need_dx else None
 
     def etfwd(self, ctx, xd):
@@ -226,8 +226,8 @@ class LSTM(Layer):
         dZ, dZd = Fn.lstm_seq_tbwd(dy, dyd, ctx["gates"], ctx["cs"], tctx["zds"], tctx["cds"], U, self.act_code)
         Fn.linear_wgrad_(ctx["x"], dZ, self.g("kernel"), self.g("bias"))
         Fn.linear_wgrad_(tctx["xd"], dZd, self.g("kernel"), None)
-        Fn.linear_wgrad_(Fn.shift_prev(ctx["hs"]), dZ, self.g("recurrent_kernel"), None)
-        Fn.linear_wgrad_(Fn.shift_prev(tctx["hds"]), dZd, self.g("recurrent_kernel"), None)
+        Fn.linear_wgrad_(ctx["hs"], dZ, self.g("recurrent_kernel"), None, shift_T=ctx["hs"].shape[1])
+        Fn.linear_wgrad_(tctx["hds"], dZd, self.g("recurrent_kernel"), None, shift_T=tctx["hds"].shape[1])
         if not need_dx:
             return None, None
         W = self.p("kernel")

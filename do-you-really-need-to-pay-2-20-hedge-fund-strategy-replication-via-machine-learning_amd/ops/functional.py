@@ -49,11 +49,18 @@ def linear_dgrad(dz: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     return torch.matmul(dz, W.t().to(dz.dtype))
 
 
-def linear_wgrad_(x: torch.Tensor, dz: torch.Tensor, gW: torch.Tensor, gb: torch.Tensor | None) -> None:
-    """gW += x^T dz (summed over all leading axes); gb += sum(dz)."""
+def linear_wgrad_(x: torch.Tensor, dz: torch.Tensor, gW: torch.Tensor, gb: torch.Tensor | None,
+                  shift_T: int = 0) -> None:
+    """gW += x^T dz (summed over all leading axes); gb += sum(dz).
+
+    ``shift_T > 0``: x is a (B, T, K) sequence and the product uses x_{t-1} (zero at t=0) — the
+    LSTM recurrent-kernel gradient sum_t h_{t-1}^T dz_t — without materialising the shift.
+    """
     if _nat(dz):
-        _ops().linear_wgrad_(_2d(x.contiguous()), _2d(dz.contiguous()), gW, gb)
+        _ops().linear_wgrad_(_2d(x.contiguous()), _2d(dz.contiguous()), gW, gb, int(shift_T))
         return
+    if shift_T:
+        x = R.shift_prev(x)
     x2, d2 = _2d(x).to(gW.dtype), _2d(dz).to(gW.dtype)
     gW.add_(x2.t() @ d2)
     if gb is not None:
