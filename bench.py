@@ -1,0 +1,125 @@
+"""Headline benchmark: MTSS-WGAN-GP training throughput (24 x 32 windows), seq/s per node.
+
+Metric (BASELINE.json): "seq/sec/node MTSS-WGAN-GP train (24x32 windows) at 1/2/4/8 GPUs".
+One step = one reference training iteration (GAN/MTSS_WGAN_GP.py:254-287): n_critic = 5 critic
+updates with the gradient penalty (second-order pass through the LSTM critic) + 1 generator update,
+each followed by the fused RMSprop(5e-5) launch and — for N > 1 — an RCCL all-reduce of the flat
+gradient bucket.  Windows counted per step: (n_critic * B + B) per rank; ``value`` is
+the whole-job aggregate over all ranks.
+
+Model: the reference architecture at the north-star shape — generator LSTM(100, sigmoid) -> LN ->
+LSTM(100, sigmoid) -> LeakyReLU -> LN -> Dense(32); critic LSTM(100) -> LSTM(100) -> Flatten ->
+Dense(1); random init; synthetic return windows (no dataset/network on the box); compute dtype
+bf16 (MFMA bf16 with fp32 accumulation, fp32 master weights/optimizer).
+
+Usage:
+    python bench.py                         # 1 GPU, defaults
+    torchrun --nproc-per-node N bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch-per-gpu", type=int, default=16384)
+    ap.add_argument("--window", type=int, default=24)
+    ap.add_argument("--features", type=int, default=32)
+    ap.add_argument("--dtype", default="bfloat16")
+    ap.add_argument("--dataset-windows", type=int, default=8192)
+    ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (e.g. for rocprof)")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import hfrep
+    from hfrep.data.windows import synthetic_windows
+    from hfrep.parallel.dp import init_distributed
+    from hfrep.train.gan_trainer import GANConfig, GANTrainer
+
+    rank, local_rank, world, pg = init_distributed()
+    if world != args.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    T, F, B = args.window, args.features, args.batch_per_gpu
+    ds = synthetic_windows(args.dataset_windows, T, F, seed=1234)
+    cfg = GANConfig(arch="lstm", loss="wgan_gp", window=T, features=F, batch_size=B, dtype=args.dtype, seed=123)
+    tr = GANTrainer(cfg, ds, device=dev, process_group=pg, rank=rank, world=world)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        tr.train_step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.train_step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    for _ in range(args.profile_steps):
+        tr.train_step()
+    torch.cuda.synchronize()
+
+    ms = elapsed / args.steps * 1e3
+    per_rank = tr.windows_per_iteration()
+    value = per_rank * world * args.steps / elapsed
+    losses = tr.losses()
+    if rank == 0:
+        finite = all(np.isfinite(v) for k, v in losses.items() if k != "iteration")
+        rec = {
+            "metric": "seq/sec/node MTSS-WGAN-GP train (24x32 windows)",
+            "value": round(value, 2),
+            "unit": "seq/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if args.dtype in ("bfloat16", "bf16") else args.dtype,
+            "data": "synthetic",
+            "config": {
+                "model": "MTSS-WGAN-GP (G: LSTM100(sigmoid)-LN-LSTM100(sigmoid)-LReLU-LN-Dense32; "
+                         "C: LSTM100-LSTM100-Flatten-Dense1; GP lambda=10; n_critic=5; RMSprop 5e-5)",
+                "global_batch": B * world,
+                "batch_per_gpu": B,
+                "seq_len": T,
+                "features": F,
+                "parallelism": f"dp{world}",
+                "windows_per_step": per_rank * world,
+            },
+            "losses_finite": bool(finite),
+            "peak_mem_gb_rank0": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
+        }
+        print(json.dumps(rec))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

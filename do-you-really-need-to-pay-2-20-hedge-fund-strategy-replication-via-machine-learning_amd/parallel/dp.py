@@ -1,0 +1,78 @@
+"""Data-parallel training over RCCL (xGMI) — one process per GPU.
+
+The reference has no parallelism at all.  Here every rank runs the full GAN
+step on its own per-GPU batch (rank-seeded Philox streams), and each model's gradients — ONE
+flat fp32 buffer per model, ~0.55 MB for the LSTM critic — are averaged with a single
+all-reduce before the fused optimizer launch.  At this message size the ring is latency-bound
+(SURVEY §2.4), so there is exactly one bucket per model per step: no per-parameter collectives.
+
+``torch.distributed`` with backend ``nccl`` is RCCL on ROCm; ``gloo`` is used for CPU tests.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank() -> tuple[int, int, int]:
+    """(rank, local_rank, world) from torchrun-style environment variables."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def init_distributed(backend: str | None = None, timeout_s: float = 600.0):
+    """Initialise the default process group from the environment (env://).
+
+    Returns (rank, local_rank, world, group).  With WORLD_SIZE == 1 nothing is initialised.
+    """
+    rank, local_rank, world = env_rank()
+    if world <= 1:
+        return rank, local_rank, world, None
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank)
+        # surface RCCL errors as Python exceptions instead of hanging a collective forever
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    if not dist.is_initialized():
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local_rank)
+        dist.init_process_group(**kw)
+    return rank, local_rank, world, dist.group.WORLD
+
+
+class GradSync:
+    """Averages flat gradient buckets across ranks (one collective per model per step)."""
+
+    def __init__(self, group, world: int):
+        self.group, self.world = group, world
+        self.backend = dist.get_backend(group) if group is not None else None
+
+    def all_reduce_(self, flat_grad: torch.Tensor) -> None:
+        if self.world <= 1:
+            return
+        if self.backend == "nccl":
+            dist.all_reduce(flat_grad, op=dist.ReduceOp.AVG, group=self.group)
+        else:
+            dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.group)
+            flat_grad.div_(self.world)
+
+    def broadcast_params(self, models, src: int = 0) -> None:
+        if self.world <= 1:
+            return
+        for m in models:
+            with torch.no_grad():
+                dist.broadcast(m.flat.data, src=src, group=self.group)
+
+    def all_reduce_scalar(self, x: float, op=dist.ReduceOp.MAX, device=None) -> float:
+        if self.world <= 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=op, group=self.group)
+        return float(t.item())
