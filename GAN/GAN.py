@@ -1,0 +1,14 @@
+"""Compatibility entry point for the reference script ``GAN/GAN.py`` (training loop GAN/GAN.py:160-204).
+
+``python GAN/GAN.py`` runs the reference prologue (cleaned data -> MinMax -> 1000 x 48 windows)
+and trains class ``GAN`` for 5000 iterations at batch 32 on the MI355X (native kernels) or CPU.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import hfrep  # noqa: E402,F401
+from hfrep.compat.legacy_gan import GAN, reference_dataset, script_main  # noqa: E402,F401
+
+if __name__ == "__main__":
+    script_main(GAN)

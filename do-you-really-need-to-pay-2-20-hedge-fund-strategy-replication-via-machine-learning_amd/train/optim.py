@@ -56,7 +56,26 @@ class KerasOptimizer:
     @torch.no_grad()
     def apply(self, flat: torch.Tensor, grad: torch.Tensor | None = None, clip: float = 0.0, gscale: float = 1.0):
         """One ``apply_gradients`` on a flat parameter buffer (+ optional clip to [-clip, clip])."""
-        grad = flat.grad if grad is None else grad
+        self._update(flat, flat.grad if grad is None else grad, clip, gscale)
+        self._advance(flat.device)
+
+    @torch.no_grad()
+    def apply_group(self, flats, clip: float = 0.0, gscale: float = 1.0):
+        """One ``apply_gradients`` over several flat buffers (one iteration tick, like one Keras model)."""
+        for f in flats:
+            self._update(f, f.grad, clip, gscale)
+        self._advance(flats[0].device)
+
+    def _advance(self, device):
+        if device.type == "cuda" and _native.use_native_for(self.iterations):
+            _native.native().step_advance_(self.iterations, self.m_cache if self.kind == "nadam" else None, self.b1)
+            return
+        if self.kind == "nadam":
+            t = float(self.iterations.item())
+            self.m_cache.mul_(self.b1 * (1 - 0.5 * 0.96 ** (0.004 * (t + 1))))
+        self.iterations.add_(1)
+
+    def _update(self, flat, grad, clip, gscale):
         slots = self._slots(flat)
         if flat.device.type == "cuda" and _native.use_native_for(flat):
             ops = _native.native()
@@ -70,7 +89,6 @@ class KerasOptimizer:
                            self.eps, gscale)
                 if clip > 0:
                     ops.clip_(flat, clip)
-            ops.step_advance_(self.iterations, self.m_cache if self.kind == "nadam" else None, self.b1)
             return
         g = grad * gscale if gscale != 1.0 else grad
         if self.kind == "rmsprop":
@@ -98,7 +116,5 @@ class KerasOptimizer:
             vp = v / (1 - self.b2 ** (t + 1))
             mbar = (1 - mt) * gp + mt1 * mp
             flat.sub_(self.lr * mbar / (vp.sqrt() + self.eps))
-            self.m_cache.fill_(sched_new)
         if clip > 0:
             flat.clamp_(-clip, clip)
-        self.iterations.add_(1)
