@@ -167,6 +167,68 @@ std::tuple<Tensor, Tensor> lstm_tbwd(optional<Tensor> dH, Tensor dHd, Tensor gat
   return {dZ, dZd};
 }
 
+// ------------------------------------------------------------------------------------ LSTM v2 (bf16 fused)
+void check_lstm2(const Tensor& x, const Tensor& U, int64_t H) {
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "lstm2 kernels are bf16-only");
+  check_lstm_U(U, H);
+  TORCH_CHECK(hfrep::lstm2_supported((int)H, (int)x.size(2)), "lstm2: unsupported H/K (H must be 100, K <= 128)");
+}
+
+std::tuple<Tensor, Tensor> lstm2_fwd(Tensor x, Tensor W, optional<Tensor> b, Tensor U, int64_t act, bool save) {
+  CHECK_GPU(x); CHECK_F32(W);
+  TORCH_CHECK(x.dim() == 3, "x must be (B, T, K)");
+  const int B = x.size(0), Tn = x.size(1), K = x.size(2), H = U.size(0);
+  check_lstm2(x, U, H);
+  TORCH_CHECK(W.size(0) == K && W.size(1) == 4 * H, "W must be (K, 4H)");
+  if (b.has_value()) { CHECK_F32(*b); TORCH_CHECK(b->numel() == 4 * H, "bias size"); }
+  GUARD(x);
+  Tensor hs = at::empty({B, Tn, H}, x.options());
+  Tensor tape = at::empty({save ? (int64_t)hfrep::lstm2_tape_elems(B, Tn) : 0}, x.options());
+  hfrep::launch_lstm2_fwd(x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
+                          U.data_ptr<float>(), hs.data_ptr(), save ? tape.data_ptr() : nullptr, B, Tn, K, H, (int)act,
+                          cur_stream(x));
+  return {hs, tape};
+}
+
+Tensor lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int64_t act) {
+  CHECK_GPU(dH); CHECK_GPU(tape); same_dt(dH, tape);
+  const int B = dH.size(0), Tn = dH.size(1), H = dH.size(2);
+  check_lstm_U(U, H);
+  TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstm2_tape_elems(B, Tn), "lstm2_bwd: tape size");
+  GUARD(dH);
+  Tensor dZ = at::empty({B, Tn, 4 * H}, dH.options());
+  hfrep::launch_lstm2_bwd(dH.data_ptr(), tape.data_ptr(), U.data_ptr<float>(), dZ.data_ptr(), B, Tn, H, (int)act,
+                          cur_stream(dH));
+  return dZ;
+}
+
+std::tuple<Tensor, Tensor> lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int64_t act) {
+  CHECK_GPU(xd); CHECK_F32(W); CHECK_GPU(tape); same_dt(xd, tape);
+  const int B = xd.size(0), Tn = xd.size(1), K = xd.size(2), H = U.size(0);
+  check_lstm2(xd, U, H);
+  TORCH_CHECK(W.size(0) == K && W.size(1) == 4 * H, "W must be (K, 4H)");
+  TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstm2_tape_elems(B, Tn), "lstm2_tfwd: tape size");
+  GUARD(xd);
+  Tensor hds = at::empty({B, Tn, H}, xd.options());
+  Tensor ttape = at::empty_like(tape);
+  hfrep::launch_lstm2_tfwd(xd.data_ptr(), W.data_ptr<float>(), U.data_ptr<float>(), tape.data_ptr(), hds.data_ptr(),
+                           ttape.data_ptr(), B, Tn, K, H, (int)act, cur_stream(xd));
+  return {hds, ttape};
+}
+
+std::tuple<Tensor, Tensor> lstm2_tbwd(optional<Tensor> dH, Tensor dHd, Tensor tape, Tensor ttape, Tensor U, int64_t act) {
+  CHECK_GPU(dHd); CHECK_GPU(tape); CHECK_GPU(ttape); same_dt(dHd, tape); same_dt(dHd, ttape);
+  if (dH.has_value()) { CHECK_GPU(*dH); same_dt(*dH, dHd); TORCH_CHECK(dH->sizes() == dHd.sizes(), "dH shape"); }
+  const int B = dHd.size(0), Tn = dHd.size(1), H = dHd.size(2);
+  check_lstm_U(U, H);
+  TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstm2_tape_elems(B, Tn) && ttape.numel() == tape.numel(), "tape size");
+  GUARD(dHd);
+  Tensor dZ = at::empty({B, Tn, 4 * H}, dHd.options()), dZd = at::empty({B, Tn, 4 * H}, dHd.options());
+  hfrep::launch_lstm2_tbwd(ptr_or_null(dH), dHd.data_ptr(), tape.data_ptr(), ttape.data_ptr(), U.data_ptr<float>(),
+                           dZ.data_ptr(), dZd.data_ptr(), B, Tn, H, (int)act, cur_stream(dHd));
+  return {dZ, dZd};
+}
+
 // ------------------------------------------------------------------------------------ LayerNorm
 std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, double eps) {
   CHECK_GPU(x); CHECK_F32(gamma); CHECK_F32(beta);
@@ -298,6 +360,10 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstm_bwd(Tensor dH, Tensor gates, Tensor cs, Tensor U, int act) -> Tensor");
   m.def("lstm_tfwd(Tensor dzx, Tensor gates, Tensor cs, Tensor U, int act) -> (Tensor, Tensor, Tensor)");
   m.def("lstm_tbwd(Tensor? dH, Tensor dHd, Tensor gates, Tensor cs, Tensor zds, Tensor cds, Tensor U, int act) -> (Tensor, Tensor)");
+  m.def("lstm2_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
+  m.def("lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int act) -> Tensor");
+  m.def("lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int act) -> (Tensor, Tensor)");
+  m.def("lstm2_tbwd(Tensor? dH, Tensor dHd, Tensor tape, Tensor ttape, Tensor U, int act) -> (Tensor, Tensor)");
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, Tensor(a!)? ggamma, Tensor(b!)? gbeta) -> Tensor");
   m.def("gp_coef(Tensor g, float weight) -> (Tensor, Tensor)");
@@ -322,6 +388,10 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("lstm_bwd", &lstm_bwd);
   m.impl("lstm_tfwd", &lstm_tfwd);
   m.impl("lstm_tbwd", &lstm_tbwd);
+  m.impl("lstm2_fwd", &lstm2_fwd);
+  m.impl("lstm2_bwd", &lstm2_bwd);
+  m.impl("lstm2_tfwd", &lstm2_tfwd);
+  m.impl("lstm2_tbwd", &lstm2_tbwd);
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("layernorm_bwd_", &layernorm_bwd_);
   m.impl("gp_coef", &gp_coef);

@@ -20,6 +20,18 @@ bool launch_lstm_tbwd(int dt, const void* dH, const void* dHd, const void* gates
                       const void* cds, const float* U, void* dZ, void* dZd, int B, int Tn, int H, int act,
                       hipStream_t s);
 
+// ---- lstm2.hip (bf16, fused input projection, blocked tapes; H == 100, K <= 128) ----
+size_t lstm2_tape_elems(int B, int Tn);
+bool lstm2_supported(int H, int K);
+void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float* U, void* hs, void* tape, int B, int Tn,
+                      int K, int H, int act, hipStream_t s);
+void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const void* tape, void* hds, void* ttape, int B,
+                       int Tn, int K, int H, int act, hipStream_t s);
+void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, int B, int Tn, int H, int act,
+                      hipStream_t s);
+void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const void* ttape, const float* U, void* dZ,
+                       void* dZd, int B, int Tn, int H, int act, hipStream_t s);
+
 // ---- gemm.hip ----
 // C[M,N] = act(A[M,K] . op(W) + bias);  op(W) = W (K,N) or W^T when w_trans (W stored (N,K)).
 // A and C share the activation dtype `dt`; W and bias are fp32 (converted while staging).

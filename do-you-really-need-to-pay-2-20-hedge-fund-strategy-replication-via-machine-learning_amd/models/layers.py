@@ -202,28 +202,25 @@ class LSTM(Layer):
         return R.lstm(x, self.w("kernel"), self.w("recurrent_kernel"), self.w("bias"), act=self.act)
 
     def efwd(self, x, save):
-        zx = Fn.linear(x, self.p("kernel"), self.p("bias"), 0)
-        hs, gates, cs = Fn.lstm_seq_fwd(zx, self.p("recurrent_kernel"), self.act_code, save)
-        return hs, ({"x": x, "hs": hs, "gates": gates, "cs": cs} if save else None)
+        hs, tape = Fn.lstm_layer_fwd(x, self.p("kernel"), self.p("bias"), self.p("recurrent_kernel"), self.act_code,
+                                     save)
+        return hs, ({"x": x, "hs": hs, "tape": tape} if save else None)
 
     def ebwd(self, ctx, dy, need_dx, wgrad=True):
         U = self.p("recurrent_kernel")
-        dZ = Fn.lstm_seq_bwd(dy, ctx["gates"], ctx["cs"], U, self.act_code)
+        dZ = Fn.lstm_layer_bwd(dy, ctx["tape"], U, self.act_code)
         if wgrad:
             Fn.linear_wgrad_(ctx["x"], dZ, self.g("kernel"), self.g("bias"))
             Fn.linear_wgrad_(ctx["hs"], dZ, self.g("recurrent_kernel"), None, shift_T=ctx["hs"].shape[1])
         return Fn.linear_dgrad(dZ, self.p("kernel")) if need_dx else None
 
     def etfwd(self, ctx, xd):
-        dzx = Fn.linear(xd, self.p("kernel"), None, 0)
-        hds, zds, cds = Fn.lstm_seq_tfwd(dzx, ctx["gates"], ctx["cs"], self.p("recurrent_kernel"), self.act_code)
-        return hds, {"xd": xd, "hds": hds, "zds": zds, "cds": cds}
+        hds, ttape = Fn.lstm_layer_tfwd(xd, self.p("kernel"), ctx["tape"], self.p("recurrent_kernel"), self.act_code)
+        return hds, {"xd": xd, "hds": hds, "ttape": ttape}
 
     def etbwd(self, ctx, tctx, dy, dyd, need_dx):
         U = self.p("recurrent_kernel")
-        if dy is None:
-            dy = torch.zeros_like(ctx["hs"])
-        dZ, dZd = Fn.lstm_seq_tbwd(dy, dyd, ctx["gates"], ctx["cs"], tctx["zds"], tctx["cds"], U, self.act_code)
+        dZ, dZd = Fn.lstm_layer_tbwd(dy, dyd, ctx["tape"], tctx["ttape"], U, self.act_code)
         Fn.linear_wgrad_(ctx["x"], dZ, self.g("kernel"), self.g("bias"))
         Fn.linear_wgrad_(tctx["xd"], dZd, self.g("kernel"), None)
         Fn.linear_wgrad_(ctx["hs"], dZ, self.g("recurrent_kernel"), None, shift_T=ctx["hs"].shape[1])

@@ -191,3 +191,51 @@ def interpolate(real: torch.Tensor, fake: torch.Tensor, alpha: torch.Tensor) -> 
         return _ops().interpolate(real.contiguous(), fake.contiguous(), alpha.contiguous())
     a = alpha.reshape(-1, *([1] * (real.dim() - 1))).to(real.dtype)
     return a * real + (1 - a) * fake
+
+
+# ---------------------------------------------------------------------------------------
+# LSTM layer-level API (input projection included).  The tape is opaque: a (gates, cells) tuple
+# on the reference / fp32 path, or one blocked bf16 tensor on the fused v2 kernels (csrc/lstm2.hip).
+# ---------------------------------------------------------------------------------------
+def _use_lstm2(x: torch.Tensor, U: torch.Tensor) -> bool:
+    return (x.dtype == torch.bfloat16 and U.shape[0] == 100 and x.shape[-1] <= 128 and _nat(x)
+            and not _native.fallback_allowed())
+
+
+def lstm_layer_fwd(x, W, b, U, act: int, save: bool):
+    """h_seq and a tape for act(x W + b ...) recurrences; x (B, T, K)."""
+    if _use_lstm2(x, U):
+        hs, tape = _ops().lstm2_fwd(x.contiguous(), W, b, U, int(act), bool(save))
+        return hs, (tape if save else None)
+    zx = linear(x, W, b, 0)
+    hs, gates, cs = lstm_seq_fwd(zx, U, act, save)
+    return hs, ((gates, cs) if save else None)
+
+
+def lstm_layer_bwd(dH, tape, U, act: int):
+    """dZ = dL/d(x W + b + h U) for every step."""
+    if isinstance(tape, torch.Tensor):
+        return _ops().lstm2_bwd(dH.contiguous(), tape, U, int(act))
+    gates, cs = tape
+    return lstm_seq_bwd(dH, gates, cs, U, act)
+
+
+def lstm_layer_tfwd(xd, W, tape, U, act: int):
+    if isinstance(tape, torch.Tensor):
+        hds, ttape = _ops().lstm2_tfwd(xd.contiguous(), W, U, tape, int(act))
+        return hds, ttape
+    gates, cs = tape
+    dzx = linear(xd, W, None, 0)
+    hds, zds, cds = lstm_seq_tfwd(dzx, gates, cs, U, act)
+    return hds, (zds, cds)
+
+
+def lstm_layer_tbwd(dH, dHd, tape, ttape, U, act: int):
+    if isinstance(tape, torch.Tensor):
+        return tuple(_ops().lstm2_tbwd(None if dH is None else dH.contiguous(), dHd.contiguous(), tape, ttape, U,
+                                       int(act)))
+    gates, cs = tape
+    zds, cds = ttape
+    if dH is None:
+        dH = torch.zeros_like(dHd)
+    return lstm_seq_tbwd(dH, dHd, gates, cs, zds, cds, U, act)

@@ -240,3 +240,69 @@ def test_trainer_gradients_gpu_vs_cpu(cuda, key):
         rel = (gg - gc).norm() / max(gc.norm(), 1e-30)
         assert rel < 2e-4, f"generator grad rel err {rel:.2e}"
         assert abs(lg.item() - lc.item()) < 1e-4 * max(1, abs(lc.item()))
+
+
+@pytest.mark.parametrize("act", [2, 1, 0])
+@pytest.mark.parametrize("B,T,K", [(70, 24, 32), (33, 12, 100), (64, 7, 35)])
+def test_lstm2_fused_layer(cuda, act, B, T, K):
+    """v2 fused bf16 kernels (input projection in-kernel, blocked tapes) vs the fp64 reference."""
+    from hfrep.ops import functional as Fn
+
+    H = 100
+    g = torch.Generator().manual_seed(20)
+    x = (torch.randn(B, T, K, generator=g) * 0.5).to(torch.bfloat16)
+    W = torch.randn(K, 4 * H, generator=g) * (1.0 / K ** 0.5)
+    b = torch.randn(4 * H, generator=g) * 0.1
+    U = torch.randn(H, 4 * H, generator=g) * (1.0 / H ** 0.5)
+    hs, tape = Fn.lstm_layer_fwd(x.to(cuda), W.to(cuda), b.to(cuda), U.to(cuda), act, True)
+    assert isinstance(tape, torch.Tensor), "bf16 H=100 must take the fused v2 path"
+    zx = x.double() @ W.double() + b.double()
+    rh, rg, rc = R.lstm_seq_fwd(zx, U.double(), act)
+    _close(hs, rh, torch.bfloat16)
+    dH = torch.randn(B, T, H, generator=g).to(torch.bfloat16)
+    dZ = Fn.lstm_layer_bwd(dH.to(cuda), tape, U.to(cuda), act)
+    _close(dZ, R.lstm_seq_bwd(dH.double(), rg, rc, U.double(), act), torch.bfloat16)
+    xd = (torch.randn(B, T, K, generator=g) * 0.3).to(torch.bfloat16)
+    hds, ttape = Fn.lstm_layer_tfwd(xd.to(cuda), W.to(cuda), tape, U.to(cuda), act)
+    th, tz, tc = R.lstm_seq_tfwd(xd.double() @ W.double(), rg, rc, U.double(), act)
+    _close(hds, th, torch.bfloat16)
+    dHd = torch.randn(B, T, H, generator=g).to(torch.bfloat16)
+    for with_dh in (True, False):
+        dZ2, dZd2 = Fn.lstm_layer_tbwd(dH.to(cuda) if with_dh else None, dHd.to(cuda), tape, ttape, U.to(cuda), act)
+        rz, rzd = R.lstm_seq_tbwd(dH.double() if with_dh else torch.zeros(B, T, H, dtype=torch.float64),
+                                  dHd.double(), rg, rc, tz, tc, U.double(), act)
+        _close(dZ2, rz, torch.bfloat16)
+        _close(dZd2, rzd, torch.bfloat16)
+
+
+@pytest.mark.parametrize("key", [("lstm", "wgan_gp"), ("lstm", "wgan")])
+def test_trainer_gradients_bf16_fused(cuda, key):
+    """bf16 training step (fused v2 LSTM kernels) vs the fp64 CPU engine: gradient direction agrees."""
+    from hfrep.train.gan_trainer import GANConfig, GANTrainer
+
+    T, F, B = 24, 32, 64
+    ds = np.random.RandomState(0).rand(64, T, F).astype(np.float32)
+    tg = GANTrainer(GANConfig(arch=key[0], loss=key[1], window=T, features=F, batch_size=B, dtype="bfloat16"), ds,
+                    device=cuda)
+    tc = GANTrainer(GANConfig(arch=key[0], loss=key[1], window=T, features=F, batch_size=B, dtype="float64"), ds,
+                    param_dtype=torch.float64)
+    with torch.no_grad():
+        tc.generator.flat.copy_(tg.generator.flat.double().cpu())
+        tc.critic.flat.copy_(tg.critic.flat.double().cpu())
+    g = torch.Generator().manual_seed(12)
+    real = torch.rand(B, T, F, generator=g)
+    noise = torch.randn(B, T, F, generator=g)
+    alpha = torch.rand(B, generator=g)
+    with torch.no_grad():
+        if key[1] == "wgan_gp":
+            fg = tg.generator.predict(noise.to(cuda, torch.bfloat16))
+            tg.critic_gp_grads(real.to(cuda, torch.bfloat16), fg, alpha.to(cuda))
+            tc.critic_gp_grads(real.to(torch.bfloat16).double(), fg.double().cpu(), alpha.double())
+            a, b = tg.critic.flat.grad.cpu().double(), tc.critic.flat.grad
+            cos = (a @ b) / (a.norm() * b.norm())
+            assert cos > 0.995, f"critic grad cosine {cos:.4f}"
+        tg.generator_grads(noise.to(cuda, torch.bfloat16))
+        tc.generator_grads(noise.to(torch.bfloat16).double())
+        a, b = tg.generator.flat.grad.cpu().double(), tc.generator.flat.grad
+        cos = (a @ b) / (a.norm() * b.norm())
+        assert cos > 0.995, f"generator grad cosine {cos:.4f}"
