@@ -44,8 +44,12 @@ Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act) {
   GUARD(x);
   const int M = x.size(0), K = x.size(1), N = W.size(1);
   Tensor y = at::empty({M, N}, x.options());
-  hfrep::launch_linear(dt_of(x), x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
-                       y.data_ptr(), M, N, K, 0, (int)act, cur_stream(x));
+  if (dt_of(x) == hfrep::DT_BF16 && N > 64)
+    hfrep::launch_linear2(x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
+                          y.data_ptr(), M, N, K, 0, (int)act, cur_stream(x));
+  else
+    hfrep::launch_linear(dt_of(x), x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
+                         y.data_ptr(), M, N, K, 0, (int)act, cur_stream(x));
   return y;
 }
 
@@ -56,8 +60,11 @@ Tensor linear_dgrad(Tensor dz, Tensor W) {
   const int M = dz.size(0), K = dz.size(1), N = W.size(0);
   Tensor dx = at::empty({M, N}, dz.options());
   // dx = dz . W^T : W stored (N, K) row-major -> w_trans
-  hfrep::launch_linear(dt_of(dz), dz.data_ptr(), W.data_ptr<float>(), nullptr, dx.data_ptr(), M, N, K, 1, 0,
-                       cur_stream(dz));
+  if (dt_of(dz) == hfrep::DT_BF16 && N > 64)
+    hfrep::launch_linear2(dz.data_ptr(), W.data_ptr<float>(), nullptr, dx.data_ptr(), M, N, K, 1, 0, cur_stream(dz));
+  else
+    hfrep::launch_linear(dt_of(dz), dz.data_ptr(), W.data_ptr<float>(), nullptr, dx.data_ptr(), M, N, K, 1, 0,
+                         cur_stream(dz));
   return dx;
 }
 
@@ -73,6 +80,32 @@ void linear_wgrad_(Tensor x, Tensor dz, Tensor gW, optional<Tensor> gb, int64_t 
   hfrep::launch_wgrad(dt_of(x), x.data_ptr(), dz.data_ptr(), gW.data_ptr<float>(),
                       gb.has_value() ? gb->data_ptr<float>() : nullptr, M, K, N, (int)shiftT, ws.data_ptr<float>(),
                       cur_stream(x));
+}
+
+// fused LSTM weight gradients (bf16): gW += X^T dZ (+ Xd^T dZd), gU += Hprev^T dZ (+ Hdprev^T dZd), gb += sum dZ
+void lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<Tensor> gb, optional<Tensor> xd,
+                 optional<Tensor> hds, optional<Tensor> dZd) {
+  CHECK_GPU(x); CHECK_GPU(hs); CHECK_GPU(dZ); same_dt(x, dZ); same_dt(hs, dZ);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "lstm_wgrad_: bf16 only");
+  TORCH_CHECK(x.dim() == 3 && hs.dim() == 3 && dZ.dim() == 3, "lstm_wgrad_: (B,T,*) tensors");
+  const int B = x.size(0), Tn = x.size(1), K = x.size(2), Hd = hs.size(2), N = dZ.size(2);
+  TORCH_CHECK(hs.size(0) == B && dZ.size(0) == B && hs.size(1) == Tn && dZ.size(1) == Tn, "lstm_wgrad_: B/T");
+  CHECK_F32(gW); CHECK_F32(gU);
+  TORCH_CHECK(gW.numel() == (int64_t)K * N && gU.numel() == (int64_t)Hd * N, "lstm_wgrad_: grad sizes");
+  if (gb.has_value()) { CHECK_F32(*gb); TORCH_CHECK(gb->numel() == N, "gb size"); }
+  const bool tangent = xd.has_value();
+  if (tangent) {
+    TORCH_CHECK(hds.has_value() && dZd.has_value(), "tangent segment needs xd, hds, dZd");
+    CHECK_GPU(*xd); CHECK_GPU(*hds); CHECK_GPU(*dZd);
+    TORCH_CHECK(xd->sizes() == x.sizes() && hds->sizes() == hs.sizes() && dZd->sizes() == dZ.sizes(), "tangent shapes");
+  }
+  GUARD(x);
+  const int M = B * Tn;
+  Tensor ws = at::empty({(int64_t)hfrep::lstm_wgrad2_workspace_floats(M, K, Hd, N)}, x.options().dtype(at::kFloat));
+  hfrep::launch_lstm_wgrad2(x.data_ptr(), hs.data_ptr(), dZ.data_ptr(), tangent ? xd->data_ptr() : nullptr,
+                            tangent ? hds->data_ptr() : nullptr, tangent ? dZd->data_ptr() : nullptr,
+                            gW.data_ptr<float>(), gU.data_ptr<float>(), gb.has_value() ? gb->data_ptr<float>() : nullptr,
+                            M, K, Hd, N, Tn, ws.data_ptr<float>(), cur_stream(x));
 }
 
 // ------------------------------------------------------------------------------------ elementwise
@@ -353,6 +386,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("linear(Tensor x, Tensor W, Tensor? b, int act) -> Tensor");
   m.def("linear_dgrad(Tensor dz, Tensor W) -> Tensor");
   m.def("linear_wgrad_(Tensor x, Tensor dz, Tensor(a!) gW, Tensor(b!)? gb, int shiftT=0) -> ()");
+  m.def("lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor(a!) gW, Tensor(b!) gU, Tensor(c!)? gb, Tensor? xd=None, Tensor? hds=None, Tensor? dZd=None) -> ()");
   m.def("act_fwd(Tensor x, int act) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor y, int act) -> Tensor");
   m.def("act_tangent_bwd(Tensor dyd, Tensor y, Tensor zd, int act) -> Tensor");
@@ -381,6 +415,7 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("linear", &linear);
   m.impl("linear_dgrad", &linear_dgrad);
   m.impl("linear_wgrad_", &linear_wgrad_);
+  m.impl("lstm_wgrad_", &lstm_wgrad_);
   m.impl("act_fwd", &act_fwd);
   m.impl("act_bwd", &act_bwd);
   m.impl("act_tangent_bwd", &act_tangent_bwd);

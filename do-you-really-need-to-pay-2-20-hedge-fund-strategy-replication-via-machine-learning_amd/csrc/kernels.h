@@ -44,6 +44,13 @@ size_t wgrad_workspace_floats(int M, int K, int N);
 void launch_wgrad(int dt, const void* X, const void* D, float* gW, float* gb, int M, int K, int N, int shiftT,
                   float* ws, hipStream_t s);
 
+// ---- gemm2.hip (bf16) ----
+size_t lstm_wgrad2_workspace_floats(int M, int K, int Hd, int N);
+void launch_lstm_wgrad2(const void* X0, const void* H0, const void* D0, const void* X1, const void* H1, const void* D1,
+                        float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s);
+void launch_linear2(const void* A, const float* W, const float* bias, void* C, int M, int N, int K, int w_trans, int act,
+                    hipStream_t s);
+
 // ---- misc.hip ----
 void launch_act_fwd(int dt, const void* x, void* y, int64_t n, int act, hipStream_t s);
 void launch_act_bwd(int dt, const void* dy, const void* y, void* dx, int64_t n, int act, hipStream_t s);

@@ -139,11 +139,11 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
   const int u = w * 32 + (lane & 31);
   const bool uok = u < H;
   const int uc = uok ? u : H - 1;
-  const int rb = blockIdx.x, row0 = rb * 32;
+  const int nrb = (B + 31) / 32;
 
+  // per-workgroup prologue, amortised over every row block this persistent workgroup owns
   stage_wt(Wt, W, K, G, LX);
   for (int i = threadIdx.x; i < 2 * 32 * LX; i += 256) xb[i] = 0;
-  for (int i = threadIdx.x; i < 2 * 32 * LH; i += 256) hb[i] = 0;
   typename P::frag ub[4][NKH];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -153,6 +153,10 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
   float bq[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) bq[q] = (uok && bias) ? bias[q * H + u] : 0.f;
+
+  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+  const int row0 = rb * 32;
+  for (int i = threadIdx.x; i < 2 * 32 * LH; i += 256) hb[i] = 0;
   float c[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) c[r] = 0.f;
@@ -211,6 +215,8 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
     __syncthreads();
   }
   tile_to_hbm<H>(hb + (Tn & 1) * 32 * LH, LH, hs, row0, B, Tn, Tn - 1, H);
+  __syncthreads();  // LDS is re-initialised for the next row block
+  }
 }
 
 // ==========================================================================================
@@ -234,17 +240,20 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
   const int u = w * 32 + (lane & 31);
   const bool uok = u < H;
   const int uc = uok ? u : H - 1;
-  const int rb = blockIdx.x, row0 = rb * 32;
+  const int nrb = (B + 31) / 32;
 
   stage_wt(Wt, W, K, G, LX);
   for (int i = threadIdx.x; i < 2 * 32 * LX; i += 256) xb[i] = 0;
-  for (int i = threadIdx.x; i < 2 * 32 * LH; i += 256) hb[i] = 0;
   typename P::frag ub[4][NKH];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int ks = 0; ks < NKH; ++ks)
       ub[q][ks] = P::make([&](int k) { return (uok && k < H) ? U[k * G + q * H + u] : 0.f; }, ks, lane);
+
+  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+  const int row0 = rb * 32;
+  for (int i = threadIdx.x; i < 2 * 32 * LH; i += 256) hb[i] = 0;
   float cd[16], cprev[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) { cd[r] = 0.f; cprev[r] = 0.f; }
@@ -324,6 +333,8 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
     __syncthreads();
   }
   tile_to_hbm<H>(hb + (Tn & 1) * 32 * LH, LH, hds, row0, B, Tn, Tn - 1, H);
+  __syncthreads();
+  }
 }
 
 // ==========================================================================================
@@ -343,13 +354,16 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int u = w * 32 + (lane & 31);
   const bool uok = u < H;
-  const int rb = blockIdx.x, row0 = rb * 32;
+  const int nrb = (B + 31) / 32;
 
   typename P::frag ut[NKG];
 #pragma unroll
   for (int ks = 0; ks < NKG; ++ks)
     ut[ks] = P::make([&](int k) { return (uok && k < G) ? U[u * G + k] : 0.f; }, ks, lane);
   for (int i = threadIdx.x; i < 2 * 32 * LG; i += 256) zb[i] = 0;
+
+  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+  const int row0 = rb * 32;
   float dc[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) dc[r] = 0.f;
@@ -430,6 +444,8 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
     __syncthreads();
   }
   tile_to_hbm<H>(zb, LG, dZ, row0, B, Tn, 0, G);
+  __syncthreads();
+  }
 }
 
 // ==========================================================================================
@@ -452,7 +468,7 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int u = w * 32 + (lane & 31);
   const bool uok = u < H;
-  const int rb = blockIdx.x, row0 = rb * 32;
+  const int nrb = (B + 31) / 32;
 
   typename P::frag ut[NKG];
 #pragma unroll
@@ -460,6 +476,9 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
     ut[ks] = P::make([&](int k) { return (uok && k < G) ? U[u * G + k] : 0.f; }, ks, lane);
   for (int i = threadIdx.x; i < 2 * 32 * LG; i += 256) { zb[i] = 0; zdb[i] = 0; }
   for (int i = threadIdx.x; i < 2 * 32 * LH; i += 256) dhb[i] = 0;
+
+  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+  const int row0 = rb * 32;
   float ac[16], acd[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) { ac[r] = 0.f; acd[r] = 0.f; }
@@ -554,6 +573,8 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
   }
   tile_to_hbm<H>(zb, LG, dZ, row0, B, Tn, 0, G);
   tile_to_hbm<H>(zdb, LG, dZd, row0, B, Tn, 0, G);
+  __syncthreads();
+  }
 }
 
 // ==========================================================================================
@@ -585,6 +606,20 @@ static void allow_big_lds(K kernel) {
   }
 }
 
+// persistent grid: one workgroup per CU (the kernels run at one wave per SIMD), each looping over
+// row blocks so the W^T staging and the register-resident U fragments are paid once per CU
+static int persistent_grid(int B) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    HFREP_CHECK_HIP(hipGetDevice(&dev));
+    HFREP_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (cus <= 0) cus = 256;
+  }
+  const int nrb = (B + 31) / 32;
+  return nrb < cus ? nrb : cus;
+}
+
 bool lstm2_supported(int H, int K) { return H == 100 && K >= 1 && K <= 128 && fwd_smem(H, K) <= 160 * 1024; }
 
 // act is a template parameter (0 linear, 1 sigmoid, 2 tanh): the cell-activation switch would
@@ -598,22 +633,22 @@ bool lstm2_supported(int H, int K) { return H == 100 && K >= 1 && K <= 128 && fw
 
 void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float* U, void* hs, void* tape, int B, int Tn,
                       int K, int H, int act, hipStream_t s) {
-  HFREP_ACT_DISPATCH(act, lstm_fwd2_kernel, dim3((B + 31) / 32), dim3(256), fwd_smem(H, K), s, (const bf16_t*)x, W, b,
+  HFREP_ACT_DISPATCH(act, lstm_fwd2_kernel, dim3(persistent_grid(B)), dim3(256), fwd_smem(H, K), s, (const bf16_t*)x, W, b,
                      U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, act)
 }
 void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const void* tape, void* hds, void* ttape, int B,
                        int Tn, int K, int H, int act, hipStream_t s) {
-  HFREP_ACT_DISPATCH(act, lstm_tfwd2_kernel, dim3((B + 31) / 32), dim3(256), fwd_smem(H, K), s, (const bf16_t*)xd, W,
+  HFREP_ACT_DISPATCH(act, lstm_tfwd2_kernel, dim3(persistent_grid(B)), dim3(256), fwd_smem(H, K), s, (const bf16_t*)xd, W,
                      U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K, act)
 }
 void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, int B, int Tn, int H, int act,
                       hipStream_t s) {
-  HFREP_ACT_DISPATCH(act, lstm_bwd2_kernel, dim3((B + 31) / 32), dim3(256), bwd_smem(H), s, (const bf16_t*)dH,
+  HFREP_ACT_DISPATCH(act, lstm_bwd2_kernel, dim3(persistent_grid(B)), dim3(256), bwd_smem(H), s, (const bf16_t*)dH,
                      (const bf16_t*)tape, U, (bf16_t*)dZ, B, Tn, act)
 }
 void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const void* ttape, const float* U, void* dZ,
                        void* dZd, int B, int Tn, int H, int act, hipStream_t s) {
-  HFREP_ACT_DISPATCH(act, lstm_tbwd2_kernel, dim3((B + 31) / 32), dim3(256), tbwd_smem(H), s, (const bf16_t*)dH,
+  HFREP_ACT_DISPATCH(act, lstm_tbwd2_kernel, dim3(persistent_grid(B)), dim3(256), tbwd_smem(H), s, (const bf16_t*)dH,
                      (const bf16_t*)dHd, (const bf16_t*)tape, (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, B,
                      Tn, act)
 }

@@ -210,8 +210,7 @@ class LSTM(Layer):
         U = self.p("recurrent_kernel")
         dZ = Fn.lstm_layer_bwd(dy, ctx["tape"], U, self.act_code)
         if wgrad:
-            Fn.linear_wgrad_(ctx["x"], dZ, self.g("kernel"), self.g("bias"))
-            Fn.linear_wgrad_(ctx["hs"], dZ, self.g("recurrent_kernel"), None, shift_T=ctx["hs"].shape[1])
+            Fn.lstm_wgrad_(ctx["x"], ctx["hs"], dZ, self.g("kernel"), self.g("recurrent_kernel"), self.g("bias"))
         return Fn.linear_dgrad(dZ, self.p("kernel")) if need_dx else None
 
     def etfwd(self, ctx, xd):
@@ -221,10 +220,8 @@ class LSTM(Layer):
     def etbwd(self, ctx, tctx, dy, dyd, need_dx):
         U = self.p("recurrent_kernel")
         dZ, dZd = Fn.lstm_layer_tbwd(dy, dyd, ctx["tape"], tctx["ttape"], U, self.act_code)
-        Fn.linear_wgrad_(ctx["x"], dZ, self.g("kernel"), self.g("bias"))
-        Fn.linear_wgrad_(tctx["xd"], dZd, self.g("kernel"), None)
-        Fn.linear_wgrad_(ctx["hs"], dZ, self.g("recurrent_kernel"), None, shift_T=ctx["hs"].shape[1])
-        Fn.linear_wgrad_(tctx["hds"], dZd, self.g("recurrent_kernel"), None, shift_T=tctx["hds"].shape[1])
+        Fn.lstm_wgrad_(ctx["x"], ctx["hs"], dZ, self.g("kernel"), self.g("recurrent_kernel"), self.g("bias"),
+                       tctx["xd"], tctx["hds"], dZd)
         if not need_dx:
             return None, None
         W = self.p("kernel")

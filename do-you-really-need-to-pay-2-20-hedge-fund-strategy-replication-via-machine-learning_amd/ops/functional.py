@@ -230,6 +230,22 @@ def lstm_layer_tfwd(xd, W, tape, U, act: int):
     return hds, (zds, cds)
 
 
+def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None) -> None:
+    """All weight gradients of one LSTM layer: gW += X^T dZ (+ Xd^T dZd), gU += H_{t-1}^T dZ (+ ...),
+    gb += sum(dZ).  bf16 GPU: ONE fused launch (csrc/gemm2.hip); otherwise per-product calls."""
+    if dZ.dtype == torch.bfloat16 and _nat(dZ):
+        _ops().lstm_wgrad_(x.contiguous(), hs.contiguous(), dZ.contiguous(), gW, gU, gb,
+                           None if xd is None else xd.contiguous(), None if hds is None else hds.contiguous(),
+                           None if dZd is None else dZd.contiguous())
+        return
+    T = hs.shape[1]
+    linear_wgrad_(x, dZ, gW, gb)
+    linear_wgrad_(hs, dZ, gU, None, shift_T=T)
+    if xd is not None:
+        linear_wgrad_(xd, dZd, gW, None)
+        linear_wgrad_(hds, dZd, gU, None, shift_T=T)
+
+
 def lstm_layer_tbwd(dH, dHd, tape, ttape, U, act: int):
     if isinstance(tape, torch.Tensor):
         return tuple(_ops().lstm2_tbwd(None if dH is None else dH.contiguous(), dHd.contiguous(), tape, ttape, U,

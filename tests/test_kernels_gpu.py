@@ -306,3 +306,33 @@ def test_trainer_gradients_bf16_fused(cuda, key):
         a, b = tg.generator.flat.grad.cpu().double(), tc.generator.flat.grad
         cos = (a @ b) / (a.norm() * b.norm())
         assert cos > 0.995, f"generator grad cosine {cos:.4f}"
+
+
+@pytest.mark.parametrize("B,T,K,tangent", [(70, 24, 32, False), (33, 24, 100, True), (200, 12, 35, True), (5, 3, 100, False)])
+def test_lstm_wgrad_fused(cuda, B, T, K, tangent):
+    """One-launch LSTM weight gradients (ds_read_b64_tr_b16 + 16x16x32 MFMA) vs fp64 products."""
+    from hfrep.ops import functional as Fn
+
+    H, N = 100, 400
+    g = torch.Generator().manual_seed(30)
+    bf = lambda *s: torch.randn(*s, generator=g).to(torch.bfloat16)
+    x, hs, dZ = bf(B, T, K), bf(B, T, H), bf(B, T, N)
+    xd, hds, dZd = bf(B, T, K), bf(B, T, H), bf(B, T, N)
+    gW0, gU0, gb0 = torch.randn(K, N, generator=g), torch.randn(H, N, generator=g), torch.randn(N, generator=g)
+    gW, gU, gb = gW0.clone().to(cuda), gU0.clone().to(cuda), gb0.clone().to(cuda)
+    Fn.lstm_wgrad_(x.to(cuda), hs.to(cuda), dZ.to(cuda), gW, gU, gb, *(
+        (xd.to(cuda), hds.to(cuda), dZd.to(cuda)) if tangent else (None, None, None)))
+    d = lambda t: t.double().reshape(-1, t.shape[-1])
+    rW = gW0.double() + d(x).t() @ d(dZ)
+    rU = gU0.double() + d(R.shift_prev(hs.double())).t() @ d(dZ)
+    rb = gb0.double() + d(dZ).sum(0)
+    if tangent:
+        rW += d(xd).t() @ d(dZd)
+        rU += d(R.shift_prev(hds.double())).t() @ d(dZd)
+    sc = lambda a, b: (d(a).abs().t() @ d(b).abs()).max().item() * (2 if tangent else 1)
+    _close(gW, rW, torch.bfloat16, scale=sc(x, dZ))
+    _close(gU, rU, torch.bfloat16, scale=sc(hs, dZ))
+    _close(gb, rb, torch.bfloat16, scale=d(dZ).abs().sum(0).max().item())
+    # tight check against fp32 accumulation of the same bf16 inputs (the kernel's exact math)
+    err = (gW.cpu().double() - rW).abs().max().item()
+    assert err < 1e-3 * sc(x, dZ), err
