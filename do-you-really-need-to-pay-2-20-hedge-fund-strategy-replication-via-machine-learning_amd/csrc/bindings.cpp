@@ -84,7 +84,7 @@ void linear_wgrad_(Tensor x, Tensor dz, Tensor gW, optional<Tensor> gb, int64_t 
 
 // fused LSTM weight gradients (bf16): gW += X^T dZ (+ Xd^T dZd), gU += Hprev^T dZ (+ Hdprev^T dZd), gb += sum dZ
 void lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<Tensor> gb, optional<Tensor> xd,
-                 optional<Tensor> hds, optional<Tensor> dZd) {
+                 optional<Tensor> hds, optional<Tensor> dZd, int64_t impl) {
   CHECK_GPU(x); CHECK_GPU(hs); CHECK_GPU(dZ); same_dt(x, dZ); same_dt(hs, dZ);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16, "lstm_wgrad_: bf16 only");
   TORCH_CHECK(x.dim() == 3 && hs.dim() == 3 && dZ.dim() == 3, "lstm_wgrad_: (B,T,*) tensors");
@@ -101,6 +101,17 @@ void lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<
   }
   GUARD(x);
   const int M = B * Tn;
+  const void* X1 = tangent ? xd->data_ptr() : nullptr;
+  const void* H1 = tangent ? hds->data_ptr() : nullptr;
+  const void* D1 = tangent ? dZd->data_ptr() : nullptr;
+  float* gbp = gb.has_value() ? gb->data_ptr<float>() : nullptr;
+  // impl: 0 = auto (LDS-DMA streaming v3 where supported), 2 = force v2 (tests / A-B)
+  if (impl != 2 && hfrep::lstm_wgrad3_supported(M, K, Hd, N)) {
+    Tensor ws = at::empty({(int64_t)hfrep::lstm_wgrad3_workspace_floats(K, Hd, N)}, x.options().dtype(at::kFloat));
+    if (hfrep::launch_lstm_wgrad3(x.data_ptr(), hs.data_ptr(), dZ.data_ptr(), X1, H1, D1, gW.data_ptr<float>(),
+                                  gU.data_ptr<float>(), gbp, M, K, Hd, N, Tn, ws.data_ptr<float>(), cur_stream(x)))
+      return;
+  }
   Tensor ws = at::empty({(int64_t)hfrep::lstm_wgrad2_workspace_floats(M, K, Hd, N)}, x.options().dtype(at::kFloat));
   hfrep::launch_lstm_wgrad2(x.data_ptr(), hs.data_ptr(), dZ.data_ptr(), tangent ? xd->data_ptr() : nullptr,
                             tangent ? hds->data_ptr() : nullptr, tangent ? dZd->data_ptr() : nullptr,
@@ -386,7 +397,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("linear(Tensor x, Tensor W, Tensor? b, int act) -> Tensor");
   m.def("linear_dgrad(Tensor dz, Tensor W) -> Tensor");
   m.def("linear_wgrad_(Tensor x, Tensor dz, Tensor(a!) gW, Tensor(b!)? gb, int shiftT=0) -> ()");
-  m.def("lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor(a!) gW, Tensor(b!) gU, Tensor(c!)? gb, Tensor? xd=None, Tensor? hds=None, Tensor? dZd=None) -> ()");
+  m.def("lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor(a!) gW, Tensor(b!) gU, Tensor(c!)? gb, Tensor? xd=None, Tensor? hds=None, Tensor? dZd=None, int impl=0) -> ()");
   m.def("act_fwd(Tensor x, int act) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor y, int act) -> Tensor");
   m.def("act_tangent_bwd(Tensor dyd, Tensor y, Tensor zd, int act) -> Tensor");

@@ -180,7 +180,12 @@ void launch_lstm_wgrad2(const void* X0, const void* H0, const void* D0, const vo
   hipLaunchKernelGGL(lstm_wgrad2_kernel, dim3(nti * ntj, splits), dim3(512), 0, s, (const bf16_t*)X0,
                      (const bf16_t*)H0, (const bf16_t*)D0, (const bf16_t*)X1, (const bf16_t*)H1, (const bf16_t*)D1,
                      ws, M, K, Hd, N, Tn, nseg, rps);
-  const int64_t total = (int64_t)Ktot * N;
+  launch_lstm_wgrad2_reduce(ws, gW, gU, gb, splits, K, Hd, N, s);
+}
+
+void launch_lstm_wgrad2_reduce(const float* ws, float* gW, float* gU, float* gb, int splits, int K, int Hd, int N,
+                               hipStream_t s) {
+  const int64_t total = (int64_t)(K + Hd + 1) * N;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 1024);
   hipLaunchKernelGGL(lstm_wgrad2_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, gW, gU, gb, splits, K, Hd, N);
 }

@@ -48,10 +48,20 @@ void launch_wgrad(int dt, const void* X, const void* D, float* gW, float* gb, in
 size_t lstm_wgrad2_workspace_floats(int M, int K, int Hd, int N);
 void launch_lstm_wgrad2(const void* X0, const void* H0, const void* D0, const void* X1, const void* H1, const void* D1,
                         float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s);
+// split-slab reduce shared by wgrad2 / wgrad3: rows 0..K-1 -> gW, K..K+Hd-1 -> gU, K+Hd -> gb (if non-null)
+void launch_lstm_wgrad2_reduce(const float* ws, float* gW, float* gU, float* gb, int splits, int K, int Hd, int N,
+                               hipStream_t s);
 void launch_linear2(const void* A, const float* W, const float* bias, void* C, int M, int N, int K, int w_trans, int act,
                     hipStream_t s);
 
+// ---- wgrad3.hip (bf16 LDS-DMA streaming LSTM wgrad; Hd == 100, K in {32, 100}; false = use wgrad2) ----
+bool lstm_wgrad3_supported(int M, int K, int Hd, int N);
+size_t lstm_wgrad3_workspace_floats(int K, int Hd, int N);
+bool launch_lstm_wgrad3(const void* X0, const void* H0, const void* D0, const void* X1, const void* H1, const void* D1,
+                        float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s);
+
 // ---- misc.hip ----
+int device_cu_count();  // compute units of the current device (cached)
 void launch_act_fwd(int dt, const void* x, void* y, int64_t n, int act, hipStream_t s);
 void launch_act_bwd(int dt, const void* dy, const void* y, void* dx, int64_t n, int act, hipStream_t s);
 void launch_act_tangent_bwd(int dt, const void* dyd, const void* y, const void* zd, void* out, int64_t n, int act,

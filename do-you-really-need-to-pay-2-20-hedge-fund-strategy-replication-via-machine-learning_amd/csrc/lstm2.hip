@@ -609,14 +609,7 @@ static void allow_big_lds(K kernel) {
 // persistent grid: one workgroup per CU (the kernels run at one wave per SIMD), each looping over
 // row blocks so the W^T staging and the register-resident U fragments are paid once per CU
 static int persistent_grid(int B) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    HFREP_CHECK_HIP(hipGetDevice(&dev));
-    HFREP_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    if (cus <= 0) cus = 256;
-  }
-  const int nrb = (B + 31) / 32;
+  const int nrb = (B + 31) / 32, cus = device_cu_count();
   return nrb < cus ? nrb : cus;
 }
 

@@ -282,4 +282,15 @@ void launch_cast(int dt_in, const void* in, int dt_out, void* out, int64_t n, hi
     hipLaunchKernelGGL((cast_kernel<float, float>), dim3(ew_grid(n)), dim3(256), 0, s, (const float*)in, (float*)out, n);
 }
 
+int device_cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    HFREP_CHECK_HIP(hipGetDevice(&dev));
+    HFREP_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
 }  // namespace hfrep

@@ -230,13 +230,15 @@ def lstm_layer_tfwd(xd, W, tape, U, act: int):
     return hds, (zds, cds)
 
 
-def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None) -> None:
+def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None, impl: int = 0) -> None:
     """All weight gradients of one LSTM layer: gW += X^T dZ (+ Xd^T dZd), gU += H_{t-1}^T dZ (+ ...),
-    gb += sum(dZ).  bf16 GPU: ONE fused launch (csrc/gemm2.hip); otherwise per-product calls."""
+    gb += sum(dZ).  bf16 GPU: ONE fused launch (csrc/wgrad3.hip LDS-DMA streaming kernel where the
+    shape is supported, csrc/gemm2.hip otherwise; ``impl=2`` forces the latter); otherwise
+    per-product calls."""
     if dZ.dtype == torch.bfloat16 and _nat(dZ):
         _ops().lstm_wgrad_(x.contiguous(), hs.contiguous(), dZ.contiguous(), gW, gU, gb,
                            None if xd is None else xd.contiguous(), None if hds is None else hds.contiguous(),
-                           None if dZd is None else dZd.contiguous())
+                           None if dZd is None else dZd.contiguous(), int(impl))
         return
     T = hs.shape[1]
     linear_wgrad_(x, dZ, gW, gb)

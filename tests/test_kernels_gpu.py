@@ -308,9 +308,12 @@ def test_trainer_gradients_bf16_fused(cuda, key):
         assert cos > 0.995, f"generator grad cosine {cos:.4f}"
 
 
-@pytest.mark.parametrize("B,T,K,tangent", [(70, 24, 32, False), (33, 24, 100, True), (200, 12, 35, True), (5, 3, 100, False)])
-def test_lstm_wgrad_fused(cuda, B, T, K, tangent):
-    """One-launch LSTM weight gradients (ds_read_b64_tr_b16 + 16x16x32 MFMA) vs fp64 products."""
+@pytest.mark.parametrize("impl", [0, 2])
+@pytest.mark.parametrize("B,T,K,tangent", [(70, 24, 32, False), (33, 24, 100, True), (200, 12, 35, True), (5, 3, 100, False),
+                                           (1000, 24, 32, True), (2051, 24, 100, True), (4096, 24, 100, False)])
+def test_lstm_wgrad_fused(cuda, B, T, K, tangent, impl):
+    """One-launch LSTM weight gradients vs fp64 products: impl 0 = LDS-DMA streaming kernel
+    (wgrad3.hip) where the shape allows it, impl 2 = the tr-read tile kernel (gemm2.hip)."""
     from hfrep.ops import functional as Fn
 
     H, N = 100, 400
@@ -321,7 +324,7 @@ def test_lstm_wgrad_fused(cuda, B, T, K, tangent):
     gW0, gU0, gb0 = torch.randn(K, N, generator=g), torch.randn(H, N, generator=g), torch.randn(N, generator=g)
     gW, gU, gb = gW0.clone().to(cuda), gU0.clone().to(cuda), gb0.clone().to(cuda)
     Fn.lstm_wgrad_(x.to(cuda), hs.to(cuda), dZ.to(cuda), gW, gU, gb, *(
-        (xd.to(cuda), hds.to(cuda), dZd.to(cuda)) if tangent else (None, None, None)))
+        (xd.to(cuda), hds.to(cuda), dZd.to(cuda)) if tangent else (None, None, None)), impl=impl)
     d = lambda t: t.double().reshape(-1, t.shape[-1])
     rW = gW0.double() + d(x).t() @ d(dZ)
     rU = gU0.double() + d(R.shift_prev(hs.double())).t() @ d(dZ)
