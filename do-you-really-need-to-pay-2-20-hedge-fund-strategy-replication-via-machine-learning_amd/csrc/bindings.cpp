@@ -234,16 +234,28 @@ std::tuple<Tensor, Tensor> lstm2_fwd(Tensor x, Tensor W, optional<Tensor> b, Ten
   return {hs, tape};
 }
 
-Tensor lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int64_t act) {
+// W given: also returns dX = dZ W^T (B, T, K) from the same launch; otherwise dX is empty
+static int check_dx_W(const optional<Tensor>& W, int H) {
+  if (!W.has_value()) return 0;
+  CHECK_F32(*W);
+  TORCH_CHECK(W->dim() == 2 && W->size(1) == 4 * H && W->size(0) >= 1 && W->size(0) <= 128,
+              "fused dX: W must be (K <= 128, 4H)");
+  return (int)W->size(0);
+}
+
+std::tuple<Tensor, Tensor> lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int64_t act, optional<Tensor> W) {
   CHECK_GPU(dH); CHECK_GPU(tape); same_dt(dH, tape);
   const int B = dH.size(0), Tn = dH.size(1), H = dH.size(2);
   check_lstm_U(U, H);
   TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstm2_tape_elems(B, Tn), "lstm2_bwd: tape size");
+  const int K = check_dx_W(W, H);
   GUARD(dH);
   Tensor dZ = at::empty({B, Tn, 4 * H}, dH.options());
-  hfrep::launch_lstm2_bwd(dH.data_ptr(), tape.data_ptr(), U.data_ptr<float>(), dZ.data_ptr(), B, Tn, H, (int)act,
+  Tensor dX = at::empty({K ? B : 0, Tn, K}, dH.options());
+  hfrep::launch_lstm2_bwd(dH.data_ptr(), tape.data_ptr(), U.data_ptr<float>(), dZ.data_ptr(),
+                          K ? W->data_ptr<float>() : nullptr, K ? dX.data_ptr() : nullptr, K, B, Tn, H, (int)act,
                           cur_stream(dH));
-  return dZ;
+  return {dZ, dX};
 }
 
 std::tuple<Tensor, Tensor> lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int64_t act) {
@@ -260,17 +272,22 @@ std::tuple<Tensor, Tensor> lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape
   return {hds, ttape};
 }
 
-std::tuple<Tensor, Tensor> lstm2_tbwd(optional<Tensor> dH, Tensor dHd, Tensor tape, Tensor ttape, Tensor U, int64_t act) {
+std::tuple<Tensor, Tensor, Tensor, Tensor> lstm2_tbwd(optional<Tensor> dH, Tensor dHd, Tensor tape, Tensor ttape,
+                                                      Tensor U, int64_t act, optional<Tensor> W) {
   CHECK_GPU(dHd); CHECK_GPU(tape); CHECK_GPU(ttape); same_dt(dHd, tape); same_dt(dHd, ttape);
   if (dH.has_value()) { CHECK_GPU(*dH); same_dt(*dH, dHd); TORCH_CHECK(dH->sizes() == dHd.sizes(), "dH shape"); }
   const int B = dHd.size(0), Tn = dHd.size(1), H = dHd.size(2);
   check_lstm_U(U, H);
   TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstm2_tape_elems(B, Tn) && ttape.numel() == tape.numel(), "tape size");
   GUARD(dHd);
+  const int K = check_dx_W(W, H);
   Tensor dZ = at::empty({B, Tn, 4 * H}, dHd.options()), dZd = at::empty({B, Tn, 4 * H}, dHd.options());
+  Tensor dX = at::empty({K ? B : 0, Tn, K}, dHd.options()), dXd = at::empty({K ? B : 0, Tn, K}, dHd.options());
   hfrep::launch_lstm2_tbwd(ptr_or_null(dH), dHd.data_ptr(), tape.data_ptr(), ttape.data_ptr(), U.data_ptr<float>(),
-                           dZ.data_ptr(), dZd.data_ptr(), B, Tn, H, (int)act, cur_stream(dHd));
-  return {dZ, dZd};
+                           dZ.data_ptr(), dZd.data_ptr(), K ? W->data_ptr<float>() : nullptr,
+                           K ? dX.data_ptr() : nullptr, K ? dXd.data_ptr() : nullptr, K, B, Tn, H, (int)act,
+                           cur_stream(dHd));
+  return {dZ, dZd, dX, dXd};
 }
 
 // ------------------------------------------------------------------------------------ LayerNorm
@@ -406,9 +423,9 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstm_tfwd(Tensor dzx, Tensor gates, Tensor cs, Tensor U, int act) -> (Tensor, Tensor, Tensor)");
   m.def("lstm_tbwd(Tensor? dH, Tensor dHd, Tensor gates, Tensor cs, Tensor zds, Tensor cds, Tensor U, int act) -> (Tensor, Tensor)");
   m.def("lstm2_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
-  m.def("lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int act) -> Tensor");
+  m.def("lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int act, Tensor? W=None) -> (Tensor, Tensor)");
   m.def("lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int act) -> (Tensor, Tensor)");
-  m.def("lstm2_tbwd(Tensor? dH, Tensor dHd, Tensor tape, Tensor ttape, Tensor U, int act) -> (Tensor, Tensor)");
+  m.def("lstm2_tbwd(Tensor? dH, Tensor dHd, Tensor tape, Tensor ttape, Tensor U, int act, Tensor? W=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, Tensor(a!)? ggamma, Tensor(b!)? gbeta) -> Tensor");
   m.def("gp_coef(Tensor g, float weight) -> (Tensor, Tensor)");

@@ -27,10 +27,12 @@ void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float
                       int K, int H, int act, hipStream_t s);
 void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const void* tape, void* hds, void* ttape, int B,
                        int Tn, int K, int H, int act, hipStream_t s);
-void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, int B, int Tn, int H, int act,
-                      hipStream_t s);
+// W / dX non-null: the input gradient dX = dZ W^T (K columns) is produced by the same launch
+void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, const float* W, void* dX, int K,
+                      int B, int Tn, int H, int act, hipStream_t s);
 void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const void* ttape, const float* U, void* dZ,
-                       void* dZd, int B, int Tn, int H, int act, hipStream_t s);
+                       void* dZd, const float* W, void* dX, void* dXd, int K, int B, int Tn, int H, int act,
+                       hipStream_t s);
 
 // ---- gemm.hip ----
 // C[M,N] = act(A[M,K] . op(W) + bias);  op(W) = W (K,N) or W^T when w_trans (W stored (N,K)).

@@ -19,6 +19,10 @@
 #include "mfma.h"
 #include "kernels.h"
 
+#include <cstdlib>
+#include <mutex>
+#include <set>
+
 namespace hfrep {
 
 namespace {
@@ -43,10 +47,16 @@ struct Slot16 {  // 16 bf16 values of one lane, packed
     return (r & 1) ? hi_bf(w) : lo_bf(w);
   }
 };
-__device__ __forceinline__ Slot16 ld_slot(const bf16_t* p) {
+// lanes whose unit is padding (u >= H: 28 of 128 tape columns) neither load nor store: the tape's
+// padded slots are never touched, which trims 22% of the tape traffic
+__device__ __forceinline__ Slot16 ld_slot(bool on, const bf16_t* p) {
   Slot16 s;
-  s.a = reinterpret_cast<const uint4*>(p)[0];
-  s.b = reinterpret_cast<const uint4*>(p)[1];
+  s.a = make_uint4(0, 0, 0, 0);
+  s.b = s.a;
+  if (on) {
+    s.a = reinterpret_cast<const uint4*>(p)[0];
+    s.b = reinterpret_cast<const uint4*>(p)[1];
+  }
   return s;
 }
 __device__ __forceinline__ void st_slot(bf16_t* p, const uint32_t (&v)[8]) {
@@ -66,36 +76,70 @@ __device__ __forceinline__ void stage_wt(bf16_t* Wt, const float* __restrict__ W
   }
 }
 
-// x tile (32 rows x K, time t) -> registers (up to 16 bf16 per thread)
-struct XPref {
-  uint32_t v[8];  // 16 bf16, two per register
+// x tile (32 rows x K, time t) -> registers.  KX > 0 (K % 4 == 0, the model's widths) makes K and
+// every index division a compile-time constant and moves 8-byte chunks (XJ per thread of the tile's
+// 256 threads); KX == 0 is the generic path for any K <= 128 (one element at a time, 16 per thread).
+template <int KX>
+struct XGeo {
+  static constexpr int XJ = KX ? (32 * KX / 4 + 255) / 256 : 4;
+  static_assert(KX % 4 == 0 && XJ <= 4, "x tile");
 };
-__device__ __forceinline__ void x_load(XPref& p, const bf16_t* __restrict__ x, int row0, int B, int Tn, int t, int K) {
+struct XPref {
+  uint2 v[4];
+};
+template <int KX>
+__device__ __forceinline__ void x_load(XPref& p, const bf16_t* __restrict__ x, int row0, int B, int Tn, int t, int K,
+                                       int ltid) {
+  if constexpr (KX == 0) {
+    uint32_t* pv = reinterpret_cast<uint32_t*>(p.v);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int e = threadIdx.x + 256 * j;
-    const int r = e / K, k = e - r * K;
-    const int row = row0 + r;
-    const uint32_t v = (r < 32 && row < B) ? (uint32_t)x[((size_t)row * Tn + t) * K + k] : 0u;
-    if (j & 1) p.v[j >> 1] |= v << 16;
-    else p.v[j >> 1] = v;
+    for (int j = 0; j < 16; ++j) {
+      const int e = ltid + 256 * j;
+      const int r = e / K, k = e - r * K;
+      const int row = row0 + r;
+      const uint32_t v = (r < 32 && row < B) ? (uint32_t)x[((size_t)row * Tn + t) * K + k] : 0u;
+      if (j & 1) pv[j >> 1] |= v << 16;
+      else pv[j >> 1] = v;
+    }
+  } else {
+    constexpr int K4 = KX / 4;
+#pragma unroll
+    for (int j = 0; j < XGeo<KX>::XJ; ++j) {
+      const int e = ltid + 256 * j;
+      const int r = e / K4, c = e - r * K4;
+      const int row = row0 + r;
+      p.v[j] = (r < 32 && row < B) ? *reinterpret_cast<const uint2*>(x + ((size_t)row * Tn + t) * KX + 4 * c)
+                                   : make_uint2(0, 0);
+    }
   }
 }
-__device__ __forceinline__ void x_store_lds(const XPref& p, bf16_t* xb, int K, int LX) {
+template <int KX>
+__device__ __forceinline__ void x_store_lds(const XPref& p, bf16_t* xb, int K, int LX, int ltid) {
+  if constexpr (KX == 0) {
+    const uint32_t* pv = reinterpret_cast<const uint32_t*>(p.v);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int e = threadIdx.x + 256 * j;
-    const int r = e / K, k = e - r * K;
-    if (r < 32) xb[r * LX + k] = (bf16_t)((j & 1) ? (p.v[j >> 1] >> 16) : (p.v[j >> 1] & 0xffffu));
+    for (int j = 0; j < 16; ++j) {
+      const int e = ltid + 256 * j;
+      const int r = e / K, k = e - r * K;
+      if (r < 32) xb[r * LX + k] = (bf16_t)((j & 1) ? (pv[j >> 1] >> 16) : (pv[j >> 1] & 0xffffu));
+    }
+  } else {
+    constexpr int K4 = KX / 4;
+#pragma unroll
+    for (int j = 0; j < XGeo<KX>::XJ; ++j) {
+      const int e = ltid + 256 * j;
+      const int r = e / K4, c = e - r * K4;
+      if (r < 32) *reinterpret_cast<uint2*>(xb + r * LX + 4 * c) = p.v[j];
+    }
   }
 }
 
-// row-major [32 x H] tile <-> HBM (B,T,H) with 8-byte chunks (H % 4 == 0)
-template <int H>
+// row-major [32 x width] tile <-> HBM (B,T,width) with 8-byte chunks (width % 4 == 0), moved by the
+// 256 threads of one row tile (ltid = thread index within the tile)
 __device__ __forceinline__ void tile_to_hbm(const bf16_t* buf, int LD, bf16_t* __restrict__ dst, int row0, int B, int Tn,
-                                            int t, int width) {
+                                            int t, int width, int ltid) {
   const int cpr = width / 4;
-  for (int e = threadIdx.x; e < 32 * cpr; e += 256) {
+  for (int e = ltid; e < 32 * cpr; e += 256) {
     const int r = e / cpr, c = e - r * cpr;
     const int row = row0 + r;
     if (row < B)
@@ -103,11 +147,10 @@ __device__ __forceinline__ void tile_to_hbm(const bf16_t* buf, int LD, bf16_t* _
           *reinterpret_cast<const uint2*>(buf + r * LD + 4 * c);
   }
 }
-template <int H>
 __device__ __forceinline__ void tile_from_hbm(bf16_t* buf, int LD, const bf16_t* __restrict__ src, int row0, int B,
-                                              int Tn, int t, int width) {
+                                              int Tn, int t, int width, int ltid) {
   const int cpr = width / 4;
-  for (int e = threadIdx.x; e < 32 * cpr; e += 256) {
+  for (int e = ltid; e < 32 * cpr; e += 256) {
     const int r = e / cpr, c = e - r * cpr;
     const int row = row0 + r;
     uint2 v = make_uint2(0, 0);
@@ -116,34 +159,56 @@ __device__ __forceinline__ void tile_from_hbm(bf16_t* buf, int LD, const bf16_t*
   }
 }
 
+// dx = dz W^T fused into the backward kernels: wave w owns input columns kc = 32 w + (lane & 31)
+// (K <= 128), W^T fragments live in registers like U^T, and each finished dz tile of step t is
+// multiplied as it is consumed by the recurrence, so the separate dgrad pass that re-read dZ is gone.
+template <int NKG>
+__device__ __forceinline__ void make_wt(typename MF<bf16_t>::frag (&wt)[NKG], const float* __restrict__ W, int K, int G,
+                                        int kc, int lane) {
+#pragma unroll
+  for (int ks = 0; ks < NKG; ++ks)
+    wt[ks] = MF<bf16_t>::make([&](int n) { return (kc < K && n < G) ? W[(size_t)kc * G + n] : 0.f; }, ks, lane);
+}
+__device__ __forceinline__ void store_dx(const f32x16& ax, bf16_t* __restrict__ dX, int row0, int B, int Tn, int t,
+                                         int K, int kc, int lane) {
+  if (kc >= K) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = row0 + acc32_row(r, lane);
+    if (row < B) dX[((size_t)row * Tn + t) * K + kc] = f2bf(ax[r]);
+  }
+}
+
 }  // namespace
 
 // ==========================================================================================
 // forward (+ optional tape):  z_t = x_t W + b + h_{t-1} U
 // ==========================================================================================
-template <int H, int ACT>
-__global__ void __launch_bounds__(256)
+template <int H, int ACT, int KX, int TILES>
+__global__ void __launch_bounds__(256 * TILES)
 lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
-                 const float* __restrict__ U, bf16_t* __restrict__ hs, bf16_t* __restrict__ tape, int B, int Tn, int K,
-                 int act_rt) {
+                 const float* __restrict__ U, bf16_t* __restrict__ hs, bf16_t* __restrict__ tape, int B, int Tn,
+                 int K_rt) {
   constexpr int act = ACT;
-  (void)act_rt;
   using P = MF<bf16_t>;
   constexpr int G = 4 * H, NKH = (H + 15) / 16, LH = NKH * 16 + 8, KPADH = NKH * 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int K = KX ? KX : K_rt;
   const int KP = (K + 15) & ~15, LX = KP + 8, NKX = KP / 16;
+  // TILES row tiles of 32 share the staged W^T; the 4 waves of tile `tile` own its x / h buffers
+  const int tile = threadIdx.x >> 8, ltid = threadIdx.x & 255;
   bf16_t* Wt = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* xb = Wt + G * LX;
+  bf16_t* xb = Wt + G * LX + tile * (2 * 32 * LX + 2 * 32 * LH);
   bf16_t* hb = xb + 2 * 32 * LX;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) & 3;
   const int u = w * 32 + (lane & 31);
   const bool uok = u < H;
   const int uc = uok ? u : H - 1;
-  const int nrb = (B + 31) / 32;
+  const int nrb = (B + 31) / 32, ngrp = (nrb + TILES - 1) / TILES;
 
   // per-workgroup prologue, amortised over every row block this persistent workgroup owns
   stage_wt(Wt, W, K, G, LX);
-  for (int i = threadIdx.x; i < 2 * 32 * LX; i += 256) xb[i] = 0;
+  for (int i = ltid; i < 2 * 32 * LX; i += 256) xb[i] = 0;
   typename P::frag ub[4][NKH];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -154,24 +219,25 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 #pragma unroll
   for (int q = 0; q < 4; ++q) bq[q] = (uok && bias) ? bias[q * H + u] : 0.f;
 
-  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
-  const int row0 = rb * 32;
-  for (int i = threadIdx.x; i < 2 * 32 * LH; i += 256) hb[i] = 0;
+  for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
+  const int rb = grp * TILES + tile, row0 = rb * 32;
+  const bool rbok = rb < nrb;  // a trailing tile past B only joins the barriers
+  for (int i = ltid; i < 2 * 32 * LH; i += 256) hb[i] = 0;
   float c[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) c[r] = 0.f;
   XPref pf;
   __syncthreads();
-  x_load(pf, x, row0, B, Tn, 0, K);
-  x_store_lds(pf, xb, K, LX);
+  x_load<KX>(pf, x, row0, B, Tn, 0, K, ltid);
+  x_store_lds<KX>(pf, xb, K, LX, ltid);
   __syncthreads();
 
   for (int t = 0; t < Tn; ++t) {
     const bf16_t* xcur = xb + (t & 1) * 32 * LX;
     const bf16_t* hcur = hb + (t & 1) * 32 * LH;
     bf16_t* hnext = hb + ((t + 1) & 1) * 32 * LH;
-    if (t > 0) tile_to_hbm<H>(hcur, LH, hs, row0, B, Tn, t - 1, H);
-    if (t + 1 < Tn) x_load(pf, x, row0, B, Tn, t + 1, K);
+    if (t > 0) tile_to_hbm(hcur, LH, hs, row0, B, Tn, t - 1, H, ltid);
+    if (t + 1 < Tn) x_load<KX>(pf, x, row0, B, Tn, t + 1, K, ltid);
     f32x16 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = zero16();
@@ -204,17 +270,17 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
         if (u < KPADH) hnext[rr * LH + u] = f2bf(h);
         put4(pk[0], i, ig); put4(pk[1], i, fg); put4(pk[2], i, gg); put4(pk[3], i, og); put4(pk[4], i, cn);
       }
-      if (tape) {
+      if (tape && rbok && uok) {
         bf16_t* tp = tape + tape_base(rb, t, Tn, w) + lane * 16 + half * 8;
 #pragma unroll
         for (int s = 0; s < TAPE_SLOTS; ++s)
           *reinterpret_cast<uint4*>(tp + s * SLOT_ELEMS) = make_uint4(pk[s][0], pk[s][1], pk[s][2], pk[s][3]);
       }
     }
-    if (t + 1 < Tn) x_store_lds(pf, xb + ((t + 1) & 1) * 32 * LX, K, LX);
+    if (t + 1 < Tn) x_store_lds<KX>(pf, xb + ((t + 1) & 1) * 32 * LX, K, LX, ltid);
     __syncthreads();
   }
-  tile_to_hbm<H>(hb + (Tn & 1) * 32 * LH, LH, hs, row0, B, Tn, Tn - 1, H);
+  tile_to_hbm(hb + (Tn & 1) * 32 * LH, LH, hs, row0, B, Tn, Tn - 1, H, ltid);
   __syncthreads();  // LDS is re-initialised for the next row block
   }
 }
@@ -222,28 +288,29 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 // ==========================================================================================
 // tangent forward at the taped primal point: zdot_t = xdot_t W + hdot_{t-1} U
 // ==========================================================================================
-template <int H, int ACT>
-__global__ void __launch_bounds__(256)
+template <int H, int ACT, int KX, int TILES>
+__global__ void __launch_bounds__(256 * TILES)
 lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, const float* __restrict__ U,
                   const bf16_t* __restrict__ tape, bf16_t* __restrict__ hds, bf16_t* __restrict__ ttape, int B, int Tn,
-                  int K, int act_rt) {
+                  int K_rt) {
   constexpr int act = ACT;
-  (void)act_rt;
   using P = MF<bf16_t>;
   constexpr int G = 4 * H, NKH = (H + 15) / 16, LH = NKH * 16 + 8, KPADH = NKH * 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int K = KX ? KX : K_rt;
   const int KP = (K + 15) & ~15, LX = KP + 8, NKX = KP / 16;
+  const int tile = threadIdx.x >> 8, ltid = threadIdx.x & 255;
   bf16_t* Wt = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* xb = Wt + G * LX;
+  bf16_t* xb = Wt + G * LX + tile * (2 * 32 * LX + 2 * 32 * LH);
   bf16_t* hb = xb + 2 * 32 * LX;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) & 3;
   const int u = w * 32 + (lane & 31);
   const bool uok = u < H;
   const int uc = uok ? u : H - 1;
-  const int nrb = (B + 31) / 32;
+  const int nrb = (B + 31) / 32, ngrp = (nrb + TILES - 1) / TILES;
 
   stage_wt(Wt, W, K, G, LX);
-  for (int i = threadIdx.x; i < 2 * 32 * LX; i += 256) xb[i] = 0;
+  for (int i = ltid; i < 2 * 32 * LX; i += 256) xb[i] = 0;
   typename P::frag ub[4][NKH];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -251,22 +318,24 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
     for (int ks = 0; ks < NKH; ++ks)
       ub[q][ks] = P::make([&](int k) { return (uok && k < H) ? U[k * G + q * H + u] : 0.f; }, ks, lane);
 
-  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
-  const int row0 = rb * 32;
-  for (int i = threadIdx.x; i < 2 * 32 * LH; i += 256) hb[i] = 0;
+  for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
+  const int rb = grp * TILES + tile, row0 = rb * 32;
+  const bool rbok = rb < nrb;
+  const int rbt = rbok ? rb : nrb - 1;  // tape reads of an idle trailing tile stay in bounds
+  for (int i = ltid; i < 2 * 32 * LH; i += 256) hb[i] = 0;
   float cd[16], cprev[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) { cd[r] = 0.f; cprev[r] = 0.f; }
   XPref pf;
   __syncthreads();
-  x_load(pf, xd, row0, B, Tn, 0, K);
-  x_store_lds(pf, xb, K, LX);
+  x_load<KX>(pf, xd, row0, B, Tn, 0, K, ltid);
+  x_store_lds<KX>(pf, xb, K, LX, ltid);
   // primal tape of step 0 (gates + cell)
   Slot16 tg[TAPE_SLOTS];
   {
-    const bf16_t* tp = tape + tape_base(rb, 0, Tn, w) + lane * 16;
+    const bf16_t* tp = tape + tape_base(rbt, 0, Tn, w) + lane * 16;
 #pragma unroll
-    for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = ld_slot(tp + s * SLOT_ELEMS);
+    for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
   }
   __syncthreads();
 
@@ -274,13 +343,13 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
     const bf16_t* xcur = xb + (t & 1) * 32 * LX;
     const bf16_t* hcur = hb + (t & 1) * 32 * LH;
     bf16_t* hnext = hb + ((t + 1) & 1) * 32 * LH;
-    if (t > 0) tile_to_hbm<H>(hcur, LH, hds, row0, B, Tn, t - 1, H);
+    if (t > 0) tile_to_hbm(hcur, LH, hds, row0, B, Tn, t - 1, H, ltid);
     Slot16 tn[TAPE_SLOTS];
     if (t + 1 < Tn) {
-      x_load(pf, xd, row0, B, Tn, t + 1, K);
-      const bf16_t* tp = tape + tape_base(rb, t + 1, Tn, w) + lane * 16;
+      x_load<KX>(pf, xd, row0, B, Tn, t + 1, K, ltid);
+      const bf16_t* tp = tape + tape_base(rbt, t + 1, Tn, w) + lane * 16;
 #pragma unroll
-      for (int s = 0; s < TAPE_SLOTS; ++s) tn[s] = ld_slot(tp + s * SLOT_ELEMS);
+      for (int s = 0; s < TAPE_SLOTS; ++s) tn[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
     }
     f32x16 acc[4];
 #pragma unroll
@@ -321,18 +390,20 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
         put4(pk[4], i, cdn);
       }
       bf16_t* tp = ttape + tape_base(rb, t, Tn, w) + lane * 16 + half * 8;
+      if (rbok && uok) {
 #pragma unroll
-      for (int s = 0; s < TAPE_SLOTS; ++s)
-        *reinterpret_cast<uint4*>(tp + s * SLOT_ELEMS) = make_uint4(pk[s][0], pk[s][1], pk[s][2], pk[s][3]);
+        for (int s = 0; s < TAPE_SLOTS; ++s)
+          *reinterpret_cast<uint4*>(tp + s * SLOT_ELEMS) = make_uint4(pk[s][0], pk[s][1], pk[s][2], pk[s][3]);
+      }
     }
     if (t + 1 < Tn) {
-      x_store_lds(pf, xb + ((t + 1) & 1) * 32 * LX, K, LX);
+      x_store_lds<KX>(pf, xb + ((t + 1) & 1) * 32 * LX, K, LX, ltid);
 #pragma unroll
       for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = tn[s];
     }
     __syncthreads();
   }
-  tile_to_hbm<H>(hb + (Tn & 1) * 32 * LH, LH, hds, row0, B, Tn, Tn - 1, H);
+  tile_to_hbm(hb + (Tn & 1) * 32 * LH, LH, hds, row0, B, Tn, Tn - 1, H, ltid);
   __syncthreads();
   }
 }
@@ -340,43 +411,48 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
 // ==========================================================================================
 // BPTT: dZ (B,T,4H) row-major from dH (B,T,H) and the tape
 // ==========================================================================================
-template <int H, int ACT>
-__global__ void __launch_bounds__(256)
+template <int H, int ACT, int TILES, bool DX>
+__global__ void __launch_bounds__(256 * TILES)
 lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape, const float* __restrict__ U,
-                 bf16_t* __restrict__ dZ, int B, int Tn, int act_rt) {
+                 bf16_t* __restrict__ dZ, const float* __restrict__ W, bf16_t* __restrict__ dX, int B, int Tn, int K) {
   constexpr int act = ACT;
-  (void)act_rt;
   using P = MF<bf16_t>;
   constexpr int G = 4 * H, NKG = (G + 15) / 16, LG = NKG * 16 + 8, NKH = (H + 15) / 16, LH = NKH * 16 + 8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* zb = reinterpret_cast<bf16_t*>(smem);  // [2][32][LG]
-  bf16_t* dhb = zb + 2 * 32 * LG;                 // [2][32][LH]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tile = threadIdx.x >> 8, ltid = threadIdx.x & 255;
+  bf16_t* zb = reinterpret_cast<bf16_t*>(smem) + tile * (2 * 32 * LG + 2 * 32 * LH);  // [2][32][LG]
+  bf16_t* dhb = zb + 2 * 32 * LG;                                                     // [2][32][LH]
+  const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) & 3;
   const int u = w * 32 + (lane & 31);
   const bool uok = u < H;
-  const int nrb = (B + 31) / 32;
+  const int nrb = (B + 31) / 32, ngrp = (nrb + TILES - 1) / TILES;
 
   typename P::frag ut[NKG];
 #pragma unroll
   for (int ks = 0; ks < NKG; ++ks)
     ut[ks] = P::make([&](int k) { return (uok && k < G) ? U[u * G + k] : 0.f; }, ks, lane);
-  for (int i = threadIdx.x; i < 2 * 32 * LG; i += 256) zb[i] = 0;
+  const int kc = w * 32 + (lane & 31);
+  const bool xw = DX && w * 32 < K;  // this wave produces dx columns (wave-uniform)
+  typename P::frag wt[DX ? NKG : 1];
+  if constexpr (DX) make_wt<NKG>(wt, W, K, G, kc, lane);
+  for (int i = ltid; i < 2 * 32 * LG; i += 256) zb[i] = 0;
 
-  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
-  const int row0 = rb * 32;
+  for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
+  const int rb = grp * TILES + tile, row0 = rb * 32;
+  const int rbt = rb < nrb ? rb : nrb - 1;  // tape reads of an idle trailing tile stay in bounds
   float dc[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) dc[r] = 0.f;
   __syncthreads();
-  tile_from_hbm<H>(dhb + ((Tn - 1) & 1) * 32 * LH, LH, dH, row0, B, Tn, Tn - 1, H);
+  tile_from_hbm(dhb + ((Tn - 1) & 1) * 32 * LH, LH, dH, row0, B, Tn, Tn - 1, H, ltid);
   Slot16 tg[4], cc, cp;
   {
-    const bf16_t* tp = tape + tape_base(rb, Tn - 1, Tn, w) + lane * 16;
+    const bf16_t* tp = tape + tape_base(rbt, Tn - 1, Tn, w) + lane * 16;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) tg[s] = ld_slot(tp + s * SLOT_ELEMS);
-    cc = ld_slot(tp + 4 * SLOT_ELEMS);
+    for (int s = 0; s < 4; ++s) tg[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
+    cc = ld_slot(uok, tp + 4 * SLOT_ELEMS);
     cp.a = make_uint4(0, 0, 0, 0); cp.b = cp.a;
-    if (Tn > 1) cp = ld_slot(tape + tape_base(rb, Tn - 2, Tn, w) + lane * 16 + 4 * SLOT_ELEMS);
+    if (Tn > 1) cp = ld_slot(uok, tape + tape_base(rbt, Tn - 2, Tn, w) + lane * 16 + 4 * SLOT_ELEMS);
   }
   __syncthreads();
 
@@ -384,19 +460,19 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
     const bf16_t* zprev = zb + ((t + 1) & 1) * 32 * LG;  // dz_{t+1}
     bf16_t* zcur = zb + (t & 1) * 32 * LG;               // dz_t
     const bf16_t* dhcur = dhb + (t & 1) * 32 * LH;
-    if (t < Tn - 1) tile_to_hbm<H>(zprev, LG, dZ, row0, B, Tn, t + 1, G);
+    if (t < Tn - 1) tile_to_hbm(zprev, LG, dZ, row0, B, Tn, t + 1, G, ltid);
     // prefetch the next (t-1) step: tape gates(t-1), cell(t-2), dH(t-1)
     Slot16 ng[4], ncp;
     uint2 ndh[4];
     if (t > 0) {
-      const bf16_t* tp = tape + tape_base(rb, t - 1, Tn, w) + lane * 16;
+      const bf16_t* tp = tape + tape_base(rbt, t - 1, Tn, w) + lane * 16;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) ng[s] = ld_slot(tp + s * SLOT_ELEMS);
+      for (int s = 0; s < 4; ++s) ng[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
       ncp.a = make_uint4(0, 0, 0, 0); ncp.b = ncp.a;
-      if (t > 1) ncp = ld_slot(tape + tape_base(rb, t - 2, Tn, w) + lane * 16 + 4 * SLOT_ELEMS);
+      if (t > 1) ncp = ld_slot(uok, tape + tape_base(rbt, t - 2, Tn, w) + lane * 16 + 4 * SLOT_ELEMS);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int e = threadIdx.x + 256 * j;
+        const int e = ltid + 256 * j;
         const int r = e / (H / 4), c4 = e - r * (H / 4);
         const int row = row0 + r;
         ndh[j] = make_uint2(0, 0);
@@ -406,8 +482,19 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
     f32x16 acc = zero16();
     if (t < Tn - 1) {
       const bf16_t* arow = zprev + (lane & 31) * LG;
+      if (xw) {
+        f32x16 ax = zero16();
 #pragma unroll
-      for (int ks = 0; ks < NKG; ++ks) acc = P::mma(P::lda(arow, ks, lane), ut[ks], acc);
+        for (int ks = 0; ks < NKG; ++ks) {
+          const typename P::frag a = P::lda(arow, ks, lane);
+          acc = P::mma(a, ut[ks], acc);
+          if constexpr (DX) ax = P::mma(a, wt[ks], ax);
+        }
+        store_dx(ax, dX, row0, B, Tn, t + 1, K, kc, lane);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < NKG; ++ks) acc = P::mma(P::lda(arow, ks, lane), ut[ks], acc);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -432,7 +519,7 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
       bf16_t* dnext = dhb + ((t - 1) & 1) * 32 * LH;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int e = threadIdx.x + 256 * j;
+        const int e = ltid + 256 * j;
         const int r = e / (H / 4), c4 = e - r * (H / 4);
         if (r < 32) *reinterpret_cast<uint2*>(dnext + r * LH + 4 * c4) = ndh[j];
       }
@@ -443,7 +530,16 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
     }
     __syncthreads();
   }
-  tile_to_hbm<H>(zb, LG, dZ, row0, B, Tn, 0, G);
+  tile_to_hbm(zb, LG, dZ, row0, B, Tn, 0, G, ltid);
+  if constexpr (DX) {
+    if (xw) {
+      f32x16 ax = zero16();
+      const bf16_t* arow = zb + (lane & 31) * LG;
+#pragma unroll
+      for (int ks = 0; ks < NKG; ++ks) ax = P::mma(P::lda(arow, ks, lane), wt[ks], ax);
+      store_dx(ax, dX, row0, B, Tn, 0, K, kc, lane);
+    }
+  }
   __syncthreads();
   }
 }
@@ -451,13 +547,15 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
 // ==========================================================================================
 // reverse of the tangent system: (dZ, dZd) from (dH?, dHd), primal tape and tangent tape
 // ==========================================================================================
-template <int H, int ACT>
-__global__ void __launch_bounds__(256)
+template <int H, int ACT, int TILES, bool DX>
+__global__ void __launch_bounds__(256 * TILES)
 lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd, const bf16_t* __restrict__ tape,
                   const bf16_t* __restrict__ ttape, const float* __restrict__ U, bf16_t* __restrict__ dZ,
-                  bf16_t* __restrict__ dZd, int B, int Tn, int act_rt) {
+                  bf16_t* __restrict__ dZd, const float* __restrict__ W, bf16_t* __restrict__ dX,
+                  bf16_t* __restrict__ dXd, int B, int Tn, int K) {
+  static_assert(TILES == 1, "tbwd2: one row tile per workgroup (LDS)");
   constexpr int act = ACT;
-  (void)act_rt;
+  const int ltid = threadIdx.x;
   using P = MF<bf16_t>;
   constexpr int G = 4 * H, NKG = (G + 15) / 16, LG = NKG * 16 + 8, NKH = (H + 15) / 16, LH = NKH * 16 + 8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -474,6 +572,10 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 #pragma unroll
   for (int ks = 0; ks < NKG; ++ks)
     ut[ks] = P::make([&](int k) { return (uok && k < G) ? U[u * G + k] : 0.f; }, ks, lane);
+  const int kc = w * 32 + (lane & 31);
+  const bool xw = DX && w * 32 < K;  // this wave produces dx / dxdot columns (wave-uniform)
+  typename P::frag wt[DX ? NKG : 1];
+  if constexpr (DX) make_wt<NKG>(wt, W, K, G, kc, lane);
   for (int i = threadIdx.x; i < 2 * 32 * LG; i += 256) { zb[i] = 0; zdb[i] = 0; }
   for (int i = threadIdx.x; i < 2 * 32 * LH; i += 256) dhb[i] = 0;
 
@@ -483,21 +585,21 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 #pragma unroll
   for (int r = 0; r < 16; ++r) { ac[r] = 0.f; acd[r] = 0.f; }
   __syncthreads();
-  if (dH) tile_from_hbm<H>(dhb + ((Tn - 1) & 1) * 32 * LH, LH, dH, row0, B, Tn, Tn - 1, H);
-  tile_from_hbm<H>(dhdb + ((Tn - 1) & 1) * 32 * LH, LH, dHd, row0, B, Tn, Tn - 1, H);
+  if (dH) tile_from_hbm(dhb + ((Tn - 1) & 1) * 32 * LH, LH, dH, row0, B, Tn, Tn - 1, H, ltid);
+  tile_from_hbm(dhdb + ((Tn - 1) & 1) * 32 * LH, LH, dHd, row0, B, Tn, Tn - 1, H, ltid);
   Slot16 cc, cdc;  // c_t and cdot_t carried (loaded at the previous iteration as "prev")
   {
     const size_t b = tape_base(rb, Tn - 1, Tn, w) + lane * 16 + 4 * SLOT_ELEMS;
-    cc = ld_slot(tape + b);
-    cdc = ld_slot(ttape + b);
+    cc = ld_slot(uok, tape + b);
+    cdc = ld_slot(uok, ttape + b);
   }
   __syncthreads();
 
   for (int t = Tn - 1; t >= 0; --t) {
     const int cb = t & 1, nb = (t + 1) & 1;
     if (t < Tn - 1) {
-      tile_to_hbm<H>(zb + nb * 32 * LG, LG, dZ, row0, B, Tn, t + 1, G);
-      tile_to_hbm<H>(zdb + nb * 32 * LG, LG, dZd, row0, B, Tn, t + 1, G);
+      tile_to_hbm(zb + nb * 32 * LG, LG, dZ, row0, B, Tn, t + 1, G, ltid);
+      tile_to_hbm(zdb + nb * 32 * LG, LG, dZd, row0, B, Tn, t + 1, G, ltid);
     }
     // this step's tapes
     Slot16 tg[4], zd[4], cp, cdp;
@@ -505,22 +607,38 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
       const bf16_t* tp = tape + tape_base(rb, t, Tn, w) + lane * 16;
       const bf16_t* tq = ttape + tape_base(rb, t, Tn, w) + lane * 16;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) { tg[s] = ld_slot(tp + s * SLOT_ELEMS); zd[s] = ld_slot(tq + s * SLOT_ELEMS); }
+      for (int s = 0; s < 4; ++s) { tg[s] = ld_slot(uok, tp + s * SLOT_ELEMS); zd[s] = ld_slot(uok, tq + s * SLOT_ELEMS); }
       cp.a = make_uint4(0, 0, 0, 0); cp.b = cp.a; cdp = cp;
       if (t > 0) {
         const size_t b = tape_base(rb, t - 1, Tn, w) + lane * 16 + 4 * SLOT_ELEMS;
-        cp = ld_slot(tape + b);
-        cdp = ld_slot(ttape + b);
+        cp = ld_slot(uok, tape + b);
+        cdp = ld_slot(uok, ttape + b);
       }
     }
     f32x16 ah = zero16(), ahd = zero16();
     if (t < Tn - 1) {
       const bf16_t* arow = zb + nb * 32 * LG + (lane & 31) * LG;
       const bf16_t* drow = zdb + nb * 32 * LG + (lane & 31) * LG;
+      if (xw) {
+        f32x16 ax = zero16(), axd = zero16();
 #pragma unroll
-      for (int ks = 0; ks < NKG; ++ks) {
-        ah = P::mma(P::lda(arow, ks, lane), ut[ks], ah);
-        ahd = P::mma(P::lda(drow, ks, lane), ut[ks], ahd);
+        for (int ks = 0; ks < NKG; ++ks) {
+          const typename P::frag a = P::lda(arow, ks, lane), ad = P::lda(drow, ks, lane);
+          ah = P::mma(a, ut[ks], ah);
+          ahd = P::mma(ad, ut[ks], ahd);
+          if constexpr (DX) {
+            ax = P::mma(a, wt[ks], ax);
+            axd = P::mma(ad, wt[ks], axd);
+          }
+        }
+        store_dx(ax, dX, row0, B, Tn, t + 1, K, kc, lane);
+        store_dx(axd, dXd, row0, B, Tn, t + 1, K, kc, lane);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < NKG; ++ks) {
+          ah = P::mma(P::lda(arow, ks, lane), ut[ks], ah);
+          ahd = P::mma(P::lda(drow, ks, lane), ut[ks], ahd);
+        }
       }
     }
     const bf16_t* dh_t = dhb + cb * 32 * LH;
@@ -564,15 +682,29 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
       }
     }
     if (t > 0) {
-      if (dH) tile_from_hbm<H>(dhb + nb * 32 * LH, LH, dH, row0, B, Tn, t - 1, H);
-      tile_from_hbm<H>(dhdb + nb * 32 * LH, LH, dHd, row0, B, Tn, t - 1, H);
+      if (dH) tile_from_hbm(dhb + nb * 32 * LH, LH, dH, row0, B, Tn, t - 1, H, ltid);
+      tile_from_hbm(dhdb + nb * 32 * LH, LH, dHd, row0, B, Tn, t - 1, H, ltid);
       cc = cp;
       cdc = cdp;
     }
     __syncthreads();
   }
-  tile_to_hbm<H>(zb, LG, dZ, row0, B, Tn, 0, G);
-  tile_to_hbm<H>(zdb, LG, dZd, row0, B, Tn, 0, G);
+  tile_to_hbm(zb, LG, dZ, row0, B, Tn, 0, G, ltid);
+  tile_to_hbm(zdb, LG, dZd, row0, B, Tn, 0, G, ltid);
+  if constexpr (DX) {
+    if (xw) {
+      f32x16 ax = zero16(), axd = zero16();
+      const bf16_t* arow = zb + (lane & 31) * LG;
+      const bf16_t* drow = zdb + (lane & 31) * LG;
+#pragma unroll
+      for (int ks = 0; ks < NKG; ++ks) {
+        ax = P::mma(P::lda(arow, ks, lane), wt[ks], ax);
+        axd = P::mma(P::lda(drow, ks, lane), wt[ks], axd);
+      }
+      store_dx(ax, dX, row0, B, Tn, 0, K, kc, lane);
+      store_dx(axd, dXd, row0, B, Tn, 0, K, kc, lane);
+    }
+  }
   __syncthreads();
   }
 }
@@ -582,68 +714,120 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 // ==========================================================================================
 size_t lstm2_tape_elems(int B, int Tn) { return (size_t)((B + 31) / 32) * Tn * NW2 * TAPE_SLOTS * SLOT_ELEMS; }
 
-static size_t fwd_smem(int H, int K) {
+static size_t fwd_smem(int H, int K, int tiles) {
   const int KP = (K + 15) & ~15, LX = KP + 8, LH = ((H + 15) / 16) * 16 + 8;
-  return (size_t)(4 * H * LX + 2 * 32 * LX + 2 * 32 * LH) * 2;
+  return (size_t)(4 * H * LX + tiles * (2 * 32 * LX + 2 * 32 * LH)) * 2;
 }
-static size_t bwd_smem(int H) {
+static size_t bwd_smem(int H, int tiles) {
   const int LG = ((4 * H + 15) / 16) * 16 + 8, LH = ((H + 15) / 16) * 16 + 8;
-  return (size_t)(2 * 32 * LG + 2 * 32 * LH) * 2;
+  return (size_t)tiles * (2 * 32 * LG + 2 * 32 * LH) * 2;
 }
 static size_t tbwd_smem(int H) {
   const int LG = ((4 * H + 15) / 16) * 16 + 8, LH = ((H + 15) / 16) * 16 + 8;
   return (size_t)(4 * 32 * LG + 4 * 32 * LH) * 2;
 }
+constexpr size_t LDS_MAX = 160 * 1024;
 
-// Dynamic LDS above 64 KB needs the per-kernel attribute; set it once per instantiation.
-template <typename K>
-static void allow_big_lds(K kernel) {
-  static bool done = false;
-  if (!done) {
-    HFREP_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    done = true;
-  }
+// Dynamic LDS above 64 KB needs the per-kernel attribute; set it once per kernel.
+static void allow_big_lds(const void* kernel) {
+  static std::mutex mu;
+  static std::set<const void*> done;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.insert(kernel).second)
+    HFREP_CHECK_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX));
 }
 
-// persistent grid: one workgroup per CU (the kernels run at one wave per SIMD), each looping over
-// row blocks so the W^T staging and the register-resident U fragments are paid once per CU
-static int persistent_grid(int B) {
-  const int nrb = (B + 31) / 32, cus = device_cu_count();
-  return nrb < cus ? nrb : cus;
+// persistent grid: one workgroup per CU (the kernels run at one or two waves per SIMD), each looping
+// over groups of `tiles` row blocks so the W^T staging and the register-resident U fragments are
+// paid once per CU
+static int persistent_grid(int B, int tiles) {
+  const int ngrp = ((B + 31) / 32 + tiles - 1) / tiles, cus = device_cu_count();
+  return ngrp < cus ? ngrp : cus;
 }
 
-bool lstm2_supported(int H, int K) { return H == 100 && K >= 1 && K <= 128 && fwd_smem(H, K) <= 160 * 1024; }
+bool lstm2_supported(int H, int K) { return H == 100 && K >= 1 && K <= 128 && fwd_smem(H, K, 1) <= LDS_MAX; }
 
-// act is a template parameter (0 linear, 1 sigmoid, 2 tanh): the cell-activation switch would
-// otherwise cost registers and instructions in the hottest loop
-#define HFREP_ACT_DISPATCH(act, KERNEL, ...)                                 \
-  switch (act) {                                                             \
-    case 0: { auto k = KERNEL<100, 0>; allow_big_lds(k); hipLaunchKernelGGL(k, __VA_ARGS__); break; } \
-    case 1: { auto k = KERNEL<100, 1>; allow_big_lds(k); hipLaunchKernelGGL(k, __VA_ARGS__); break; } \
-    default: { auto k = KERNEL<100, 2>; allow_big_lds(k); hipLaunchKernelGGL(k, __VA_ARGS__); break; } \
+template <typename Kern, typename... Args>
+static void launch(Kern k, int grid, int threads, size_t smem, hipStream_t s, Args... args) {
+  allow_big_lds(reinterpret_cast<const void*>(k));
+  hipLaunchKernelGGL(k, dim3(grid), dim3(threads), smem, s, args...);
+}
+
+// act (0 linear, 1 sigmoid, 2 tanh) and the input width K are template parameters: the cell
+// activation switch and the x-tile index arithmetic would otherwise sit in the hottest loop.
+// K in {32, 100} (the model's widths) get two 32-row tiles per workgroup (8 waves, W^T shared).
+#define HFREP_FWD_LAUNCH(KERNEL, KXV, TL, ...)                                                  \
+  switch (act) {                                                                                 \
+    case 0: launch(KERNEL<100, 0, KXV, TL>, __VA_ARGS__); break;                                 \
+    case 1: launch(KERNEL<100, 1, KXV, TL>, __VA_ARGS__); break;                                 \
+    default: launch(KERNEL<100, 2, KXV, TL>, __VA_ARGS__); break;                                \
   }
+
+// row tiles per workgroup for the fwd / bwd kernels (HFREP_LSTM_TILES=1 or 2, default 2)
+static int lstm_tiles() {
+  static int t = 0;
+  if (!t) {
+    const char* e = getenv("HFREP_LSTM_TILES");
+    t = (e && atoi(e) == 1) ? 1 : 2;
+  }
+  return t;
+}
 
 void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float* U, void* hs, void* tape, int B, int Tn,
                       int K, int H, int act, hipStream_t s) {
-  HFREP_ACT_DISPATCH(act, lstm_fwd2_kernel, dim3(persistent_grid(B)), dim3(256), fwd_smem(H, K), s, (const bf16_t*)x, W, b,
-                     U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, act)
+  const bf16_t* xp = (const bf16_t*)x;
+  if ((K == 32 || K == 100) && lstm_tiles() == 2 && fwd_smem(H, K, 2) <= LDS_MAX) {
+    const int g = persistent_grid(B, 2);
+    const size_t sm = fwd_smem(H, K, 2);
+    if (K == 32) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 32, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
+    else HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 100, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
+  } else {
+    const int g = persistent_grid(B, 1);
+    const size_t sm = fwd_smem(H, K, 1);
+    if (K == 32) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 32, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
+    else if (K == 100) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 100, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
+    else HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 0, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
+  }
 }
 void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const void* tape, void* hds, void* ttape, int B,
                        int Tn, int K, int H, int act, hipStream_t s) {
-  HFREP_ACT_DISPATCH(act, lstm_tfwd2_kernel, dim3(persistent_grid(B)), dim3(256), fwd_smem(H, K), s, (const bf16_t*)xd, W,
-                     U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K, act)
+  const bf16_t* xp = (const bf16_t*)xd;
+  const int g = persistent_grid(B, 1);
+  const size_t sm = fwd_smem(H, K, 1);
+  if (K == 32) HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 32, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
+  else if (K == 100) HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 100, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
+  else HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 0, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
 }
-void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, int B, int Tn, int H, int act,
-                      hipStream_t s) {
-  HFREP_ACT_DISPATCH(act, lstm_bwd2_kernel, dim3(persistent_grid(B)), dim3(256), bwd_smem(H), s, (const bf16_t*)dH,
-                     (const bf16_t*)tape, U, (bf16_t*)dZ, B, Tn, act)
+
+#define HFREP_BWD_LAUNCH(KERNEL, TL, DXV, ...)                                                  \
+  switch (act) {                                                                                 \
+    case 0: launch(KERNEL<100, 0, TL, DXV>, __VA_ARGS__); break;                                 \
+    case 1: launch(KERNEL<100, 1, TL, DXV>, __VA_ARGS__); break;                                 \
+    default: launch(KERNEL<100, 2, TL, DXV>, __VA_ARGS__); break;                                \
+  }
+
+void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, const float* W, void* dX, int K,
+                      int B, int Tn, int H, int act, hipStream_t s) {
+  const bf16_t* dh = (const bf16_t*)dH;
+  const bf16_t* tp = (const bf16_t*)tape;
+  if (dX)  // fused input gradient: U^T and W^T fragments in registers -> one row tile per workgroup
+    HFREP_BWD_LAUNCH(lstm_bwd2_kernel, 1, true, persistent_grid(B, 1), 256, bwd_smem(H, 1), s, dh, tp, U, (bf16_t*)dZ,
+                     W, (bf16_t*)dX, B, Tn, K)
+  else  // (two row tiles per workgroup spill the U^T fragments at 256 VGPRs: measured slower)
+    HFREP_BWD_LAUNCH(lstm_bwd2_kernel, 1, false, persistent_grid(B, 1), 256, bwd_smem(H, 1), s, dh, tp, U, (bf16_t*)dZ,
+                     (const float*)nullptr, (bf16_t*)nullptr, B, Tn, 0)
 }
 void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const void* ttape, const float* U, void* dZ,
-                       void* dZd, int B, int Tn, int H, int act, hipStream_t s) {
-  HFREP_ACT_DISPATCH(act, lstm_tbwd2_kernel, dim3(persistent_grid(B)), dim3(256), tbwd_smem(H), s, (const bf16_t*)dH,
-                     (const bf16_t*)dHd, (const bf16_t*)tape, (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, B,
-                     Tn, act)
+                       void* dZd, const float* W, void* dX, void* dXd, int K, int B, int Tn, int H, int act,
+                       hipStream_t s) {
+  if (dX)
+    HFREP_BWD_LAUNCH(lstm_tbwd2_kernel, 1, true, persistent_grid(B, 1), 256, tbwd_smem(H), s, (const bf16_t*)dH,
+                     (const bf16_t*)dHd, (const bf16_t*)tape, (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, W,
+                     (bf16_t*)dX, (bf16_t*)dXd, B, Tn, K)
+  else
+    HFREP_BWD_LAUNCH(lstm_tbwd2_kernel, 1, false, persistent_grid(B, 1), 256, tbwd_smem(H), s, (const bf16_t*)dH,
+                     (const bf16_t*)dHd, (const bf16_t*)tape, (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd,
+                     (const float*)nullptr, (bf16_t*)nullptr, (bf16_t*)nullptr, B, Tn, 0)
 }
 
 }  // namespace hfrep

@@ -208,10 +208,14 @@ class LSTM(Layer):
 
     def ebwd(self, ctx, dy, need_dx, wgrad=True):
         U = self.p("recurrent_kernel")
-        dZ = Fn.lstm_layer_bwd(dy, ctx["tape"], U, self.act_code)
+        dx = None
+        if need_dx:  # dX = dZ W^T comes out of the BPTT launch itself
+            dZ, dx = Fn.lstm_layer_bwd(dy, ctx["tape"], U, self.act_code, W=self.p("kernel"))
+        else:
+            dZ = Fn.lstm_layer_bwd(dy, ctx["tape"], U, self.act_code)
         if wgrad:
             Fn.lstm_wgrad_(ctx["x"], ctx["hs"], dZ, self.g("kernel"), self.g("recurrent_kernel"), self.g("bias"))
-        return Fn.linear_dgrad(dZ, self.p("kernel")) if need_dx else None
+        return dx
 
     def etfwd(self, ctx, xd):
         hds, ttape = Fn.lstm_layer_tfwd(xd, self.p("kernel"), ctx["tape"], self.p("recurrent_kernel"), self.act_code)
@@ -219,13 +223,15 @@ class LSTM(Layer):
 
     def etbwd(self, ctx, tctx, dy, dyd, need_dx):
         U = self.p("recurrent_kernel")
-        dZ, dZd = Fn.lstm_layer_tbwd(dy, dyd, ctx["tape"], tctx["ttape"], U, self.act_code)
+        dx = dxd = None
+        if need_dx:
+            dZ, dZd, dx, dxd = Fn.lstm_layer_tbwd(dy, dyd, ctx["tape"], tctx["ttape"], U, self.act_code,
+                                                  W=self.p("kernel"))
+        else:
+            dZ, dZd = Fn.lstm_layer_tbwd(dy, dyd, ctx["tape"], tctx["ttape"], U, self.act_code)
         Fn.lstm_wgrad_(ctx["x"], ctx["hs"], dZ, self.g("kernel"), self.g("recurrent_kernel"), self.g("bias"),
                        tctx["xd"], tctx["hds"], dZd)
-        if not need_dx:
-            return None, None
-        W = self.p("kernel")
-        return Fn.linear_dgrad(dZ, W), Fn.linear_dgrad(dZd, W)
+        return dx, dxd
 
 
 class LayerNormalization(Layer):

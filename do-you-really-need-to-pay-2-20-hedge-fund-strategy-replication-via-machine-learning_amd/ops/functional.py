@@ -212,12 +212,15 @@ def lstm_layer_fwd(x, W, b, U, act: int, save: bool):
     return hs, ((gates, cs) if save else None)
 
 
-def lstm_layer_bwd(dH, tape, U, act: int):
-    """dZ = dL/d(x W + b + h U) for every step."""
+def lstm_layer_bwd(dH, tape, U, act: int, W=None):
+    """dZ = dL/d(x W + b + h U) for every step; with ``W`` also the input gradient dX = dZ W^T,
+    returned as ``(dZ, dX)`` (the v2 kernel produces it in the same launch, csrc/lstm2.hip)."""
     if isinstance(tape, torch.Tensor):
-        return _ops().lstm2_bwd(dH.contiguous(), tape, U, int(act))
+        dZ, dX = _ops().lstm2_bwd(dH.contiguous(), tape, U, int(act), W)
+        return dZ if W is None else (dZ, dX)
     gates, cs = tape
-    return lstm_seq_bwd(dH, gates, cs, U, act)
+    dZ = lstm_seq_bwd(dH, gates, cs, U, act)
+    return dZ if W is None else (dZ, linear_dgrad(dZ, W))
 
 
 def lstm_layer_tfwd(xd, W, tape, U, act: int):
@@ -248,12 +251,15 @@ def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None, impl: int = 
         linear_wgrad_(hds, dZd, gU, None, shift_T=T)
 
 
-def lstm_layer_tbwd(dH, dHd, tape, ttape, U, act: int):
+def lstm_layer_tbwd(dH, dHd, tape, ttape, U, act: int, W=None):
+    """(dZ, dZd) of the reverse-over-tangent pass; with ``W`` also (dX, dXd) = (dZ W^T, dZd W^T)."""
     if isinstance(tape, torch.Tensor):
-        return tuple(_ops().lstm2_tbwd(None if dH is None else dH.contiguous(), dHd.contiguous(), tape, ttape, U,
-                                       int(act)))
+        dZ, dZd, dX, dXd = _ops().lstm2_tbwd(None if dH is None else dH.contiguous(), dHd.contiguous(), tape, ttape,
+                                             U, int(act), W)
+        return (dZ, dZd) if W is None else (dZ, dZd, dX, dXd)
     gates, cs = tape
     zds, cds = ttape
     if dH is None:
         dH = torch.zeros_like(dHd)
-    return lstm_seq_tbwd(dH, dHd, gates, cs, zds, cds, U, act)
+    dZ, dZd = lstm_seq_tbwd(dH, dHd, gates, cs, zds, cds, U, act)
+    return (dZ, dZd) if W is None else (dZ, dZd, linear_dgrad(dZ, W), linear_dgrad(dZd, W))

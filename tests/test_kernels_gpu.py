@@ -261,7 +261,12 @@ def test_lstm2_fused_layer(cuda, act, B, T, K):
     _close(hs, rh, torch.bfloat16)
     dH = torch.randn(B, T, H, generator=g).to(torch.bfloat16)
     dZ = Fn.lstm_layer_bwd(dH.to(cuda), tape, U.to(cuda), act)
-    _close(dZ, R.lstm_seq_bwd(dH.double(), rg, rc, U.double(), act), torch.bfloat16)
+    rdz = R.lstm_seq_bwd(dH.double(), rg, rc, U.double(), act)
+    _close(dZ, rdz, torch.bfloat16)
+    # fused input gradient: dX = dZ W^T from the same launch (K <= 128)
+    dZ1, dX = Fn.lstm_layer_bwd(dH.to(cuda), tape, U.to(cuda), act, W=W.to(cuda))
+    assert torch.equal(dZ1, dZ)
+    _close(dX, rdz @ W.double().t(), torch.bfloat16, scale=(rdz.abs() @ W.double().abs().t()).max().item())
     xd = (torch.randn(B, T, K, generator=g) * 0.3).to(torch.bfloat16)
     hds, ttape = Fn.lstm_layer_tfwd(xd.to(cuda), W.to(cuda), tape, U.to(cuda), act)
     th, tz, tc = R.lstm_seq_tfwd(xd.double() @ W.double(), rg, rc, U.double(), act)
@@ -273,6 +278,12 @@ def test_lstm2_fused_layer(cuda, act, B, T, K):
                                   dHd.double(), rg, rc, tz, tc, U.double(), act)
         _close(dZ2, rz, torch.bfloat16)
         _close(dZd2, rzd, torch.bfloat16)
+        dZ3, dZd3, dX3, dXd3 = Fn.lstm_layer_tbwd(dH.to(cuda) if with_dh else None, dHd.to(cuda), tape, ttape,
+                                                  U.to(cuda), act, W=W.to(cuda))
+        assert torch.equal(dZ3, dZ2) and torch.equal(dZd3, dZd2)
+        Wd = W.double()
+        _close(dX3, rz @ Wd.t(), torch.bfloat16, scale=(rz.abs() @ Wd.abs().t()).max().item())
+        _close(dXd3, rzd @ Wd.t(), torch.bfloat16, scale=(rzd.abs() @ Wd.abs().t()).max().item())
 
 
 @pytest.mark.parametrize("key", [("lstm", "wgan_gp"), ("lstm", "wgan")])
