@@ -62,6 +62,15 @@ size_t lstm_wgrad3_workspace_floats(int K, int Hd, int N);
 bool launch_lstm_wgrad3(const void* X0, const void* H0, const void* D0, const void* X1, const void* H1, const void* D1,
                         float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s);
 
+// ---- skinny.hip (bf16, N <= 4 output columns, K % 8 == 0: the Flatten -> Dense(1) critic head) ----
+bool skinny_supported(int K, int N);
+void launch_skinny_fwd(const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
+                       hipStream_t s);
+size_t skinny_wgrad_workspace_floats(int M, int K, int N);
+void launch_skinny_wgrad(const void* x, const void* d, float* gW, float* gb, int M, int K, int N, float* ws,
+                         hipStream_t s);
+void launch_skinny_dgrad(const void* d, const float* W, void* dx, int M, int K, int N, hipStream_t s);
+
 // ---- misc.hip ----
 int device_cu_count();  // compute units of the current device (cached)
 void launch_act_fwd(int dt, const void* x, void* y, int64_t n, int act, hipStream_t s);
@@ -72,7 +81,9 @@ void launch_layernorm_fwd(int dt, const void* x, const float* gamma, const float
                           float* rstd, int64_t rows, int D, float eps, hipStream_t s);
 void launch_layernorm_bwd(int dt, const void* dy, const void* xhat, const float* rstd, const float* gamma,
                           void* dx, float* ggamma, float* gbeta, int64_t rows, int D, hipStream_t s);
-void launch_gp_coef(int dt, const void* g, void* v, float* pen, int B, int64_t D, float weight, hipStream_t s);
+// v = dGP/dg per row, pen += sum_b (1 - |g_b|)^2 / B  (rowpen: B floats of workspace)
+void launch_gp_coef(int dt, const void* g, void* v, float* pen, float* rowpen, int B, int64_t D, float weight,
+                    hipStream_t s);
 void launch_interpolate(int dt, const void* real, const void* fake, const float* alpha, void* out, int B,
                         int64_t D, hipStream_t s);
 void launch_philox_fill(int dt, void* out, int64_t n, uint64_t seed, int64_t* ctr, int dist, hipStream_t s);

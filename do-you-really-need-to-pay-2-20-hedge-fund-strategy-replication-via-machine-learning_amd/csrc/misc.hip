@@ -141,7 +141,9 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict_
 
 void launch_layernorm_fwd(int dt, const void* x, const float* gamma, const float* beta, void* y, void* xhat,
                           float* rstd, int64_t rows, int D, float eps, hipStream_t s) {
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 8192));
+  // one row per wave and no grid-stride loop: a wave's row is a dependent load -> reduce -> store
+  // chain, so latency is hidden by having every row in flight at once, not by looping
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 1 << 30));
   if (dt == DT_BF16)
     hipLaunchKernelGGL(layernorm_fwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, gamma, beta,
                        (bf16_t*)y, (bf16_t*)xhat, rstd, rows, D, eps);
@@ -162,26 +164,42 @@ void launch_layernorm_bwd(int dt, const void* dy, const void* xhat, const float*
 }
 
 // ------------------------------------------------------------------ gradient penalty coefficient
+// One wave per sample row: the per-row penalty term goes to its own slot and a single-workgroup
+// reduce sums them (a per-row atomicAdd on one address serialised 16k adds: 212 us at B = 16384).
 template <typename T>
-__global__ void __launch_bounds__(256) gp_coef_kernel(const T* __restrict__ g, T* __restrict__ v, float* __restrict__ pen,
-                                                      int B, int64_t D, float weight) {
-  __shared__ float red[4];
-  const int b = blockIdx.x;
+__global__ void __launch_bounds__(256) gp_coef_kernel(const T* __restrict__ g, T* __restrict__ v,
+                                                      float* __restrict__ rowpen, int B, int64_t D, float weight) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
   const T* gr = g + (int64_t)b * D;
   float s = 0.f;
-  for (int64_t j = threadIdx.x; j < D; j += 256) { const float x = ld_f(gr + j); s += x * x; }
-  const float nrm = sqrtf(block_sum<4>(s, red));
+  for (int64_t j = lane; j < D; j += 64) { const float x = ld_f(gr + j); s += x * x; }
+  const float nrm = sqrtf(wave_sum(s));
   const float one_m = 1.f - nrm;
   const float scale = -(2.f * weight / B) * one_m / fmaxf(nrm, 1e-30f);
-  for (int64_t j = threadIdx.x; j < D; j += 256) st_f(v + (int64_t)b * D + j, ld_f(gr + j) * scale);
-  if (threadIdx.x == 0) atomicAdd(pen, one_m * one_m / B);
+  for (int64_t j = lane; j < D; j += 64) st_f(v + (int64_t)b * D + j, ld_f(gr + j) * scale);
+  if (lane == 0) rowpen[b] = one_m * one_m / B;
 }
 
-void launch_gp_coef(int dt, const void* g, void* v, float* pen, int B, int64_t D, float weight, hipStream_t s) {
+__global__ void __launch_bounds__(1024) sum_into_kernel(const float* __restrict__ x, int n, float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 1024) s += x[i];
+  s = block_sum<16>(s, red);
+  if (threadIdx.x == 0) out[0] += s;
+}
+
+void launch_gp_coef(int dt, const void* g, void* v, float* pen, float* rowpen, int B, int64_t D, float weight,
+                    hipStream_t s) {
+  const int grid = (B + 3) / 4;
   if (dt == DT_BF16)
-    hipLaunchKernelGGL(gp_coef_kernel<bf16_t>, dim3(B), dim3(256), 0, s, (const bf16_t*)g, (bf16_t*)v, pen, B, D, weight);
+    hipLaunchKernelGGL(gp_coef_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)g, (bf16_t*)v, rowpen, B, D,
+                       weight);
   else
-    hipLaunchKernelGGL(gp_coef_kernel<float>, dim3(B), dim3(256), 0, s, (const float*)g, (float*)v, pen, B, D, weight);
+    hipLaunchKernelGGL(gp_coef_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)g, (float*)v, rowpen, B, D,
+                       weight);
+  hipLaunchKernelGGL(sum_into_kernel, dim3(1), dim3(1024), 0, s, rowpen, B, pen);
 }
 
 // ------------------------------------------------------------------ interpolation

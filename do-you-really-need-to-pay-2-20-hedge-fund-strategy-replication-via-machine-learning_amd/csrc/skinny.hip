@@ -1,0 +1,229 @@
+// Skinny GEMMs (bf16 activations, N <= 4 output columns, K % 8 == 0): the critic head
+// Flatten(T*H) -> Dense(1) of every WGAN family (reference GAN/MTSS_WGAN_GP.py build_critic).
+//
+// All three products of a Dense(1) layer are HBM-streaming with O(1) arithmetic per byte, so the
+// MFMA tile kernels (gemm.hip / gemm2.hip) - which stage a 128-wide W tile for one useful column
+// and launch one workgroup per 128 rows - ran them at 0.2-0.6 TB/s.  Here every op is a flat stream
+// of 16-byte accesses with enough rows in flight per wave to cover HBM latency:
+//
+//   skinny_fwd   y[m,n]   = act(sum_k x[m,k] W[k,n] + b[n])   wave per row group, W in LDS,
+//                                                            lanes stride the row, shuffle-reduce
+//   skinny_wgrad gW[k,n] += sum_m x[m,k] d[m,n]  (+ gb)      thread per 8-column chunk, split-M
+//                                                            slabs + one reduce launch (deterministic)
+//   skinny_dgrad dx[m,k]  = sum_n d[m,n] W[k,n]              one 16-byte output chunk per thread
+#include "common.h"
+#include "kernels.h"
+
+namespace hfrep {
+
+namespace {
+
+__device__ __forceinline__ float lo_bf(uint32_t v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
+__device__ __forceinline__ void unpack8(const uint4& v, float (&f)[8]) {
+  f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+  f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+constexpr int SK_ROWS = 4;  // rows per wave in flight (forward)
+
+}  // namespace
+
+template <int N>
+__global__ void __launch_bounds__(256) skinny_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W,
+                                                         const float* __restrict__ b, bf16_t* __restrict__ y, int M,
+                                                         int K, int act) {
+  extern __shared__ float wsh[];  // [K][N]
+  for (int i = threadIdx.x; i < K * N; i += 256) wsh[i] = W[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int KC = K / 8;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t m0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * SK_ROWS; m0 < M; m0 += nw * SK_ROWS) {
+    float acc[SK_ROWS][N];
+#pragma unroll
+    for (int r = 0; r < SK_ROWS; ++r)
+#pragma unroll
+      for (int n = 0; n < N; ++n) acc[r][n] = 0.f;
+    for (int c = lane; c < KC; c += 64) {
+      uint4 v[SK_ROWS];
+#pragma unroll
+      for (int r = 0; r < SK_ROWS; ++r)
+        v[r] = (m0 + r < M) ? *reinterpret_cast<const uint4*>(x + (m0 + r) * K + 8 * c) : make_uint4(0, 0, 0, 0);
+      float w[8][N];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int n = 0; n < N; ++n) w[j][n] = wsh[(8 * c + j) * N + n];
+#pragma unroll
+      for (int r = 0; r < SK_ROWS; ++r) {
+        float f[8];
+        unpack8(v[r], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int n = 0; n < N; ++n) acc[r][n] = fmaf(f[j], w[j][n], acc[r][n]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < SK_ROWS; ++r)
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        const float s = wave_sum(acc[r][n]);
+        if (lane == 0 && m0 + r < M) y[(m0 + r) * N + n] = f2bf(act_f(act, s + (b ? b[n] : 0.f)));
+      }
+  }
+}
+
+template <int N>
+__global__ void __launch_bounds__(1024) skinny_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ d,
+                                                            float* __restrict__ slab, int M, int K, int rps) {
+  const int c = threadIdx.x, KC = K / 8;
+  const int z = blockIdx.x;
+  const int mb = z * rps, me = min(M, mb + rps);
+  float acc[8][N], bacc[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    bacc[n] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j][n] = 0.f;
+  }
+  const bool own = c < KC;
+  int m = mb;
+  for (; m + 4 <= me; m += 4) {  // four rows in flight
+    uint4 v[4];
+    float dv[4][N];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = own ? *reinterpret_cast<const uint4*>(x + (int64_t)(m + r) * K + 8 * c) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int n = 0; n < N; ++n) dv[r][n] = bf2f(d[(int64_t)(m + r) * N + n]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float f[8];
+      unpack8(v[r], f);
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        bacc[n] += dv[r][n];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j][n] = fmaf(f[j], dv[r][n], acc[j][n]);
+      }
+    }
+  }
+  for (; m < me; ++m) {
+    const uint4 v = own ? *reinterpret_cast<const uint4*>(x + (int64_t)m * K + 8 * c) : make_uint4(0, 0, 0, 0);
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const float dv = bf2f(d[(int64_t)m * N + n]);
+      bacc[n] += dv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j][n] = fmaf(f[j], dv, acc[j][n]);
+    }
+  }
+  float* out = slab + (size_t)z * (K + 1) * N;
+  if (own) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int n = 0; n < N; ++n) out[(8 * c + j) * N + n] = acc[j][n];
+  }
+  if (c == 0) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) out[K * N + n] = bacc[n];
+  }
+}
+
+// sum the split slabs: 64 consecutive elements per workgroup, the 4 waves split the slabs
+__global__ void __launch_bounds__(256) skinny_reduce_kernel(const float* __restrict__ slab, float* __restrict__ gW,
+                                                            float* __restrict__ gb, int splits, int KN, int N) {
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  const int total = KN + N;
+  float s = 0.f;
+  if (e < total)
+    for (int z = wv; z < splits; z += 4) s += slab[(size_t)z * total + e];
+  part[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && e < total) {
+    const float t = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    if (e < KN) gW[e] += t;
+    else if (gb) gb[e - KN] += t;
+  }
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) skinny_dgrad_kernel(const bf16_t* __restrict__ d, const float* __restrict__ W,
+                                                           bf16_t* __restrict__ dx, int M, int K) {
+  const int KC = K / 8;
+  const int64_t total = (int64_t)M * KC;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+    const int64_t m = q / KC;
+    const int c = (int)(q - m * KC);
+    float dv[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) dv[n] = bf2f(d[m * N + n]);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int n = 0; n < N; ++n) s = fmaf(dv[n], W[(8 * c + j) * N + n], s);
+      o[j] = s;
+    }
+    *reinterpret_cast<uint4*>(dx + m * K + 8 * c) = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]),
+                                                                pack2(o[4], o[5]), pack2(o[6], o[7]));
+  }
+}
+
+// ------------------------------------------------------------------------------------ host
+bool skinny_supported(int K, int N) {
+  return N >= 1 && N <= 4 && K % 8 == 0 && K >= 8 && K / 8 <= 1024 && K * N <= 16384;  // W in <= 64 KB LDS
+}
+
+#define HFREP_SKINNY_N(N, KERNEL, ...)                                     \
+  switch (N) {                                                             \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;             \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;             \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break;             \
+    default: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;            \
+  }
+
+void launch_skinny_fwd(const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
+                       hipStream_t s) {
+  if (M <= 0) return;
+  const int64_t groups = ((int64_t)M + 4 * SK_ROWS - 1) / (4 * SK_ROWS);
+  const int grid = (int)std::min<int64_t>(groups, (int64_t)device_cu_count() * 8);
+  HFREP_SKINNY_N(N, skinny_fwd_kernel, dim3(grid), dim3(256), (size_t)K * N * sizeof(float), s, (const bf16_t*)x, W, b,
+                 (bf16_t*)y, M, K, act)
+}
+
+size_t skinny_wgrad_workspace_floats(int M, int K, int N) {
+  const int splits = std::max(1, std::min(512, (M + 63) / 64));
+  return (size_t)splits * (K + 1) * N;
+}
+
+void launch_skinny_wgrad(const void* x, const void* d, float* gW, float* gb, int M, int K, int N, float* ws,
+                         hipStream_t s) {
+  if (M <= 0) return;
+  const int splits = std::max(1, std::min(512, (M + 63) / 64));
+  const int rps = (M + splits - 1) / splits;
+  const int threads = ((K / 8 + 63) / 64) * 64;
+  HFREP_SKINNY_N(N, skinny_wgrad_kernel, dim3(splits), dim3(threads), 0, s, (const bf16_t*)x, (const bf16_t*)d, ws, M, K,
+                 rps)
+  const int total = (K + 1) * N;
+  hipLaunchKernelGGL(skinny_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, s, ws, gW, gb, splits, K * N, N);
+}
+
+void launch_skinny_dgrad(const void* d, const float* W, void* dx, int M, int K, int N, hipStream_t s) {
+  if (M <= 0) return;
+  const int64_t total = (int64_t)M * (K / 8);
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, (int64_t)device_cu_count() * 16);
+  HFREP_SKINNY_N(N, skinny_dgrad_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)d, W, (bf16_t*)dx, M, K)
+}
+
+}  // namespace hfrep

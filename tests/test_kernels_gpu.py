@@ -350,3 +350,43 @@ def test_lstm_wgrad_fused(cuda, B, T, K, tangent, impl):
     # tight check against fp32 accumulation of the same bf16 inputs (the kernel's exact math)
     err = (gW.cpu().double() - rW).abs().max().item()
     assert err < 1e-3 * sc(x, dZ), err
+
+
+@pytest.mark.parametrize("M,K,N", [(37, 2400, 1), (1000, 2400, 1), (513, 64, 3), (70, 8, 4), (4099, 800, 2)])
+def test_skinny_dense_ops(cuda, M, K, N):
+    """Flatten -> Dense(N <= 4) head kernels (csrc/skinny.hip): forward, input grad, weight+bias grad
+    vs fp64 products of the same bf16 inputs."""
+    from hfrep.ops import functional as Fn
+
+    g = torch.Generator().manual_seed(40)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    W = torch.randn(K, N, generator=g) * K ** -0.5
+    b = torch.randn(N, generator=g)
+    y = Fn.linear(x.to(cuda), W.to(cuda), b.to(cuda), 0)
+    ry = x.double() @ W.double() + b.double()
+    _close(y, ry, torch.bfloat16, scale=(x.double().abs() @ W.double().abs()).max().item())
+    d = torch.randn(M, N, generator=g).to(torch.bfloat16)
+    dx = Fn.linear_dgrad(d.to(cuda), W.to(cuda))
+    _close(dx, d.double() @ W.double().t(), torch.bfloat16)
+    gW0, gb0 = torch.randn(K, N, generator=g), torch.randn(N, generator=g)
+    gW, gb = gW0.clone().to(cuda), gb0.clone().to(cuda)
+    Fn.linear_wgrad_(x.to(cuda), d.to(cuda), gW, gb)
+    rW = gW0.double() + x.double().t() @ d.double()
+    rb = gb0.double() + d.double().sum(0)
+    assert (gW.cpu().double() - rW).abs().max().item() < 1e-3 * max(1.0, (x.double().abs().t() @ d.double().abs()).max().item())
+    assert (gb.cpu().double() - rb).abs().max().item() < 1e-3 * max(1.0, d.double().abs().sum(0).max().item())
+
+
+@pytest.mark.parametrize("B,D", [(7, 768), (16384, 768), (33, 100)])
+def test_gp_coef_many_rows(cuda, B, D):
+    from hfrep.ops import functional as Fn
+
+    g = torch.Generator().manual_seed(41)
+    x = (torch.randn(B, D, generator=g) * 0.05).to(torch.bfloat16)
+    pen, v = Fn.gp_coef(x.to(cuda), 10.0)
+    xd = x.double()
+    nrm = xd.norm(dim=1)
+    rpen = ((1 - nrm) ** 2).mean()
+    rv = -(2 * 10.0 / B) * ((1 - nrm) / nrm)[:, None] * xd
+    assert abs(pen.item() - rpen.item()) < 1e-3 * max(1.0, rpen.item())
+    _close(v, rv, torch.bfloat16)
