@@ -20,12 +20,14 @@ typedef uint16_t bf16_t;
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
-// round-to-nearest-even; NaN stays NaN (quiet bit forced)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+// round-to-nearest-even through the gfx950 conversion instruction (v_cvt_pk_bf16_f32: one VALU op
+// per PAIR of values, NaN stays NaN); the integer-rounding form it replaces cost ~8 VALU per value
+typedef __bf16 hw_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+// two values -> packed bf16 pair (lo in bits 0..15)
+__device__ __forceinline__ uint32_t pk2bf(float lo, float hi) {
+  const hw_bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 template <typename T> struct Cvt;
@@ -46,13 +48,16 @@ template <typename T> __device__ __forceinline__ void st_f(T* p, float v) { *p =
 // ---------------------------------------------------------------------------
 enum Act : int { ACT_LINEAR = 0, ACT_SIGMOID = 1, ACT_TANH = 2, ACT_LRELU = 3, ACT_RELU = 4 };
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// The LSTM cell evaluates 3 sigmoids + 2 tanh per unit per step; with IEEE division (a ~10
+// instruction div_scale/div_fmas/div_fixup sequence each) these were ~2.4k VALU instructions per
+// step per wave, the single largest cost of the recurrent kernels.  v_exp_f32 + v_rcp_f32 (1 ulp
+// each) is 4-5 instructions per activation and far below bf16 storage precision.
+__device__ __forceinline__ float rcpf_(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float sigmoidf_(float x) { return rcpf_(1.0f + __expf(-x)); }
 __device__ __forceinline__ float tanhf_(float x) {
-  // tanh via exp: accurate to ~1 ulp of fp32 over the useful range, saturates cleanly
-  float ax = fabsf(x);
-  float e = __expf(-2.0f * ax);
-  float t = (1.0f - e) / (1.0f + e);
-  return copysignf(t, x);
+  // tanh(|x|) = (1 - e) / (1 + e), e = exp(-2|x|) in (0, 1]: no overflow, saturates cleanly
+  const float e = __expf(-2.0f * fabsf(x));
+  return copysignf((1.0f - e) * rcpf_(1.0f + e), x);
 }
 
 __device__ __forceinline__ float act_f(int act, float x) {

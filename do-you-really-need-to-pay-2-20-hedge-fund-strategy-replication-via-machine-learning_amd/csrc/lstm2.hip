@@ -35,7 +35,7 @@ __device__ __forceinline__ size_t tape_base(int rb, int t, int Tn, int w) {
   return (((size_t)rb * Tn + t) * NW2 + w) * TAPE_SLOTS * SLOT_ELEMS;
 }
 
-__device__ __forceinline__ uint32_t pk2(float lo, float hi) { return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16); }
+__device__ __forceinline__ uint32_t pk2(float lo, float hi) { return pk2bf(lo, hi); }
 __device__ __forceinline__ float lo_bf(uint32_t v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ float hi_bf(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
 
@@ -188,7 +188,7 @@ template <int H, int ACT, int KX, int TILES>
 __global__ void __launch_bounds__(256 * TILES)
 lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
                  const float* __restrict__ U, bf16_t* __restrict__ hs, bf16_t* __restrict__ tape, int B, int Tn,
-                 int K_rt) {
+                 int K_rt, int dbg) {
   constexpr int act = ACT;
   using P = MF<bf16_t>;
   constexpr int G = 4 * H, NKH = (H + 15) / 16, LH = NKH * 16 + 8, KPADH = NKH * 16;
@@ -236,12 +236,13 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
     const bf16_t* xcur = xb + (t & 1) * 32 * LX;
     const bf16_t* hcur = hb + (t & 1) * 32 * LH;
     bf16_t* hnext = hb + ((t + 1) & 1) * 32 * LH;
-    if (t > 0) tile_to_hbm(hcur, LH, hs, row0, B, Tn, t - 1, H, ltid);
-    if (t + 1 < Tn) x_load<KX>(pf, x, row0, B, Tn, t + 1, K, ltid);
+    if (t > 0 && !(dbg & 2)) tile_to_hbm(hcur, LH, hs, row0, B, Tn, t - 1, H, ltid);
+    if (t + 1 < Tn && !(dbg & 4)) x_load<KX>(pf, x, row0, B, Tn, t + 1, K, ltid);
     f32x16 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = zero16();
     const bf16_t* xrow = xcur + (lane & 31) * LX;
+    if (!(dbg & 8)) {
     for (int kx = 0; kx < NKX; ++kx) {
       const typename P::frag a = P::lda(xrow, kx, lane);
 #pragma unroll
@@ -253,6 +254,7 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
       const typename P::frag a = P::lda(hrow, ks, lane);
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc[q] = P::mma(a, ub[q][ks], acc[q]);
+    }
     }
 #pragma unroll
     for (int half = 0; half < 2; ++half) {  // two halves of 8 rows: 20 packing registers, not 40
@@ -267,10 +269,10 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
         float h = og * act_f(act, cn);
         if (!uok) { cn = 0.f; h = 0.f; }
         c[r] = cn;
-        if (u < KPADH) hnext[rr * LH + u] = f2bf(h);
+        if (u < KPADH && !(dbg & 16)) hnext[rr * LH + u] = f2bf(h);
         put4(pk[0], i, ig); put4(pk[1], i, fg); put4(pk[2], i, gg); put4(pk[3], i, og); put4(pk[4], i, cn);
       }
-      if (tape && rbok && uok) {
+      if (tape && rbok && uok && !(dbg & 1)) {
         bf16_t* tp = tape + tape_base(rb, t, Tn, w) + lane * 16 + half * 8;
 #pragma unroll
         for (int s = 0; s < TAPE_SLOTS; ++s)
@@ -278,7 +280,7 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
       }
     }
     if (t + 1 < Tn) x_store_lds<KX>(pf, xb + ((t + 1) & 1) * 32 * LX, K, LX, ltid);
-    __syncthreads();
+    if (!(dbg & 32)) __syncthreads();
   }
   tile_to_hbm(hb + (Tn & 1) * 32 * LH, LH, hs, row0, B, Tn, Tn - 1, H, ltid);
   __syncthreads();  // LDS is re-initialised for the next row block
@@ -764,6 +766,17 @@ static void launch(Kern k, int grid, int threads, size_t smem, hipStream_t s, Ar
   }
 
 // row tiles per workgroup for the fwd / bwd kernels (HFREP_LSTM_TILES=1 or 2, default 2)
+// timing-only ablation mask for the forward kernel (HFREP_LSTM_DBG; 0 in every real run):
+// 1 no tape store, 2 no h store, 4 no x load, 8 no MFMA, 16 no h LDS write, 32 no step barrier
+static int lstm_dbg() {
+  static int d = -1;
+  if (d < 0) {
+    const char* e = getenv("HFREP_LSTM_DBG");
+    d = e ? atoi(e) : 0;
+  }
+  return d;
+}
+
 static int lstm_tiles() {
   static int t = 0;
   if (!t) {
@@ -779,14 +792,14 @@ void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float
   if ((K == 32 || K == 100) && lstm_tiles() == 2 && fwd_smem(H, K, 2) <= LDS_MAX) {
     const int g = persistent_grid(B, 2);
     const size_t sm = fwd_smem(H, K, 2);
-    if (K == 32) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 32, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
-    else HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 100, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
+    if (K == 32) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 32, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
+    else HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 100, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
   } else {
     const int g = persistent_grid(B, 1);
     const size_t sm = fwd_smem(H, K, 1);
-    if (K == 32) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 32, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
-    else if (K == 100) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 100, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
-    else HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 0, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
+    if (K == 32) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 32, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
+    else if (K == 100) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 100, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
+    else HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 0, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
   }
 }
 void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const void* tape, void* hds, void* ttape, int B,

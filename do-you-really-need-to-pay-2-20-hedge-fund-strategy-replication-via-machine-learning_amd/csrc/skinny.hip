@@ -24,7 +24,7 @@ __device__ __forceinline__ void unpack8(const uint4& v, float (&f)[8]) {
   f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
   f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
 }
-__device__ __forceinline__ uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+__device__ __forceinline__ uint32_t pack2(float a, float b) { return pk2bf(a, b); }
 
 constexpr int SK_ROWS = 4;  // rows per wave in flight (forward)
 
