@@ -328,8 +328,12 @@ Tensor layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, optiona
   if (gbeta.has_value()) { CHECK_F32(*gbeta); gbp = gbeta->data_ptr<float>(); }
   GUARD(dy);
   Tensor dx = at::empty_like(dy);
+  const int64_t rows = dy.numel() / D;
+  Tensor ws = at::empty({(gg || gbp) ? (int64_t)hfrep::layernorm_bwd_splits(rows) * 2 * D : 0},
+                        dy.options().dtype(at::kFloat));
   hfrep::launch_layernorm_bwd(dt_of(dy), dy.data_ptr(), xhat.data_ptr(), rstd.data_ptr<float>(),
-                              gamma.data_ptr<float>(), dx.data_ptr(), gg, gbp, dy.numel() / D, D, cur_stream(dy));
+                              gamma.data_ptr<float>(), dx.data_ptr(), gg, gbp, (gg || gbp) ? ws.data_ptr<float>() : nullptr,
+                              rows, D, cur_stream(dy));
   return dx;
 }
 

@@ -70,6 +70,8 @@ size_t skinny_wgrad_workspace_floats(int M, int K, int N);
 void launch_skinny_wgrad(const void* x, const void* d, float* gW, float* gb, int M, int K, int N, float* ws,
                          hipStream_t s);
 void launch_skinny_dgrad(const void* d, const float* W, void* dx, int M, int K, int N, hipStream_t s);
+// a[0..na) += sum_z slab[z][0..na), b[0..nb) += sum_z slab[z][na..na+nb)  (fixed order; a/b may be null)
+void launch_split_reduce(const float* slab, float* a, float* b, int splits, int na, int nb, hipStream_t s);
 
 // ---- misc.hip ----
 int device_cu_count();  // compute units of the current device (cached)
@@ -79,8 +81,11 @@ void launch_act_tangent_bwd(int dt, const void* dyd, const void* y, const void* 
                             hipStream_t s);
 void launch_layernorm_fwd(int dt, const void* x, const float* gamma, const float* beta, void* y, void* xhat,
                           float* rstd, int64_t rows, int D, float eps, hipStream_t s);
+// ggamma/gbeta (either may be null) += column sums via per-workgroup slabs in ws
+// (layernorm_bwd_splits(rows) * 2 * D floats) and a fixed-order reduce: deterministic
+int layernorm_bwd_splits(int64_t rows);
 void launch_layernorm_bwd(int dt, const void* dy, const void* xhat, const float* rstd, const float* gamma,
-                          void* dx, float* ggamma, float* gbeta, int64_t rows, int D, hipStream_t s);
+                          void* dx, float* ggamma, float* gbeta, float* ws, int64_t rows, int D, hipStream_t s);
 // v = dGP/dg per row, pen += sum_b (1 - |g_b|)^2 / B  (rowpen: B floats of workspace)
 void launch_gp_coef(int dt, const void* g, void* v, float* pen, float* rowpen, int B, int64_t D, float weight,
                     hipStream_t s);

@@ -86,8 +86,8 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const T* __restrict_
 template <typename T>
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ xhat,
                                                             const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                                            T* __restrict__ dx, float* __restrict__ ggamma,
-                                                            float* __restrict__ gbeta, int64_t rows, int D) {
+                                                            T* __restrict__ dx, float* __restrict__ slab,
+                                                            int64_t rows, int D) {
   constexpr int MAXJ = 4;  // D <= 256
   __shared__ float red_g[4 * MAXJ * 64];
   __shared__ float red_b[4 * MAXJ * 64];
@@ -121,8 +121,9 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict_
       if (j < D) st_f(dx + row * D + j, rs * (gv[q] - mg - xv[q] * mgx));
     }
   }
-  if (ggamma == nullptr) return;
-  // reduce the 4 waves' partials through LDS, then one atomic per column per workgroup
+  if (slab == nullptr) return;
+  // reduce the 4 waves' partials through LDS, then one slab row per workgroup (summed in a fixed
+  // order by launch_split_reduce: bitwise run-to-run determinism, no float atomics)
 #pragma unroll
   for (int q = 0; q < MAXJ; ++q) {
     red_g[(wid * MAXJ + q) * 64 + lane] = pg[q];
@@ -134,8 +135,8 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict_
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) { a += red_g[(w * MAXJ + q) * 64 + l]; b += red_b[(w * MAXJ + q) * 64 + l]; }
-    atomicAdd(ggamma + j, a);
-    atomicAdd(gbeta + j, b);
+    slab[(size_t)blockIdx.x * 2 * D + j] = a;
+    slab[(size_t)blockIdx.x * 2 * D + D + j] = b;
   }
 }
 
@@ -152,15 +153,19 @@ void launch_layernorm_fwd(int dt, const void* x, const float* gamma, const float
                        (float*)y, (float*)xhat, rstd, rows, D, eps);
 }
 
+int layernorm_bwd_splits(int64_t rows) { return (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 2048)); }
+
 void launch_layernorm_bwd(int dt, const void* dy, const void* xhat, const float* rstd, const float* gamma, void* dx,
-                          float* ggamma, float* gbeta, int64_t rows, int D, hipStream_t s) {
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 2048));
+                          float* ggamma, float* gbeta, float* ws, int64_t rows, int D, hipStream_t s) {
+  const int grid = layernorm_bwd_splits(rows);
+  float* slab = (ggamma || gbeta) ? ws : nullptr;
   if (dt == DT_BF16)
     hipLaunchKernelGGL(layernorm_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)dy,
-                       (const bf16_t*)xhat, rstd, gamma, (bf16_t*)dx, ggamma, gbeta, rows, D);
+                       (const bf16_t*)xhat, rstd, gamma, (bf16_t*)dx, slab, rows, D);
   else
     hipLaunchKernelGGL(layernorm_bwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)dy, (const float*)xhat,
-                       rstd, gamma, (float*)dx, ggamma, gbeta, rows, D);
+                       rstd, gamma, (float*)dx, slab, rows, D);
+  if (slab) launch_split_reduce(slab, ggamma, gbeta, grid, D, D, s);
 }
 
 // ------------------------------------------------------------------ gradient penalty coefficient

@@ -137,7 +137,8 @@ __global__ void __launch_bounds__(1024) skinny_wgrad_kernel(const bf16_t* __rest
   }
 }
 
-// sum the split slabs: 64 consecutive elements per workgroup, the 4 waves split the slabs
+// sum the split slabs: 64 consecutive elements per workgroup, the 4 waves split the slabs (fixed
+// order: deterministic).  Elements [0, KN) accumulate into gW, [KN, KN + N) into gb (if non-null).
 __global__ void __launch_bounds__(256) skinny_reduce_kernel(const float* __restrict__ slab, float* __restrict__ gW,
                                                             float* __restrict__ gb, int splits, int KN, int N) {
   __shared__ float part[4][64];
@@ -151,8 +152,11 @@ __global__ void __launch_bounds__(256) skinny_reduce_kernel(const float* __restr
   __syncthreads();
   if (wv == 0 && e < total) {
     const float t = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
-    if (e < KN) gW[e] += t;
-    else if (gb) gb[e - KN] += t;
+    if (e < KN) {
+      if (gW) gW[e] += t;
+    } else if (gb) {
+      gb[e - KN] += t;
+    }
   }
 }
 
@@ -217,6 +221,11 @@ void launch_skinny_wgrad(const void* x, const void* d, float* gW, float* gb, int
                  rps)
   const int total = (K + 1) * N;
   hipLaunchKernelGGL(skinny_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, s, ws, gW, gb, splits, K * N, N);
+}
+
+void launch_split_reduce(const float* slab, float* a, float* b, int splits, int na, int nb, hipStream_t s) {
+  const int total = na + nb;
+  hipLaunchKernelGGL(skinny_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, s, slab, a, b, splits, na, nb);
 }
 
 void launch_skinny_dgrad(const void* d, const float* W, void* dx, int M, int K, int N, hipStream_t s) {

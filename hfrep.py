@@ -22,3 +22,8 @@ _spec = importlib.util.spec_from_file_location(
 _mod = importlib.util.module_from_spec(_spec)
 sys.modules["hfrep"] = _mod
 _spec.loader.exec_module(_mod)
+
+if __name__ == "__main__":  # python -m hfrep <command> ... / python hfrep.py <command> ...
+    from hfrep.cli import main
+
+    sys.exit(main())
