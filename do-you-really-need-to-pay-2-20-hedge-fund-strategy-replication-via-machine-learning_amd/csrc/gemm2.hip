@@ -158,8 +158,10 @@ lstm_wgrad2_reduce_kernel(const float* __restrict__ slab, float* __restrict__ gW
 }
 
 static int wgrad2_splits(int M, int N) {
+  // enough workgroups to occupy the chip even at the reference batch (M = 32 x 48 rows): one split
+  // per 128 rows (4 chunks per workgroup), at most ~1024 workgroups in total
   const int ntj = (N + WG_J - 1) / WG_J;
-  int splits = (M + 4095) / 4096;
+  int splits = (M + 127) / 128;
   splits = std::max(1, std::min(splits, std::max(1, 1024 / ntj)));
   return splits;
 }

@@ -81,8 +81,9 @@ __device__ __forceinline__ void stage_wt(bf16_t* Wt, const float* __restrict__ W
 // 256 threads); KX == 0 is the generic path for any K <= 128 (one element at a time, 16 per thread).
 template <int KX>
 struct XGeo {
-  static constexpr int XJ = KX ? (32 * KX / 4 + 255) / 256 : 4;
-  static_assert(KX % 4 == 0 && XJ <= 4, "x tile");
+  static constexpr bool VEC = KX > 0 && KX % 4 == 0;  // 8-byte chunks; else one element at a time
+  static constexpr int XJ = VEC ? (32 * KX / 4 + 255) / 256 : 4;
+  static_assert(XJ <= 4, "x tile");
 };
 struct XPref {
   uint2 v[4];
@@ -90,7 +91,8 @@ struct XPref {
 template <int KX>
 __device__ __forceinline__ void x_load(XPref& p, const bf16_t* __restrict__ x, int row0, int B, int Tn, int t, int K,
                                        int ltid) {
-  if constexpr (KX == 0) {
+  if constexpr (!XGeo<KX>::VEC) {
+    if constexpr (KX > 0) K = KX;
     uint32_t* pv = reinterpret_cast<uint32_t*>(p.v);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -115,7 +117,8 @@ __device__ __forceinline__ void x_load(XPref& p, const bf16_t* __restrict__ x, i
 }
 template <int KX>
 __device__ __forceinline__ void x_store_lds(const XPref& p, bf16_t* xb, int K, int LX, int ltid) {
-  if constexpr (KX == 0) {
+  if constexpr (!XGeo<KX>::VEC) {
+    if constexpr (KX > 0) K = KX;
     const uint32_t* pv = reinterpret_cast<const uint32_t*>(p.v);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -794,6 +797,11 @@ void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float
     const size_t sm = fwd_smem(H, K, 2);
     if (K == 32) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 32, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
     else HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 100, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
+  } else if ((K == 35 || K == 36) && lstm_tiles() == 2) {  // reference (F=35) / production (F=36) panels
+    const int g = persistent_grid(B, 2);
+    const size_t sm = fwd_smem(H, K, 2);
+    if (K == 35) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 35, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
+    else HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 36, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
   } else {
     const int g = persistent_grid(B, 1);
     const size_t sm = fwd_smem(H, K, 1);
@@ -808,6 +816,8 @@ void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const voi
   const int g = persistent_grid(B, 1);
   const size_t sm = fwd_smem(H, K, 1);
   if (K == 32) HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 32, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
+  else if (K == 35) HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 35, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
+  else if (K == 36) HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 36, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
   else if (K == 100) HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 100, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
   else HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 0, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
 }
