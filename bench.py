@@ -32,7 +32,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch-per-gpu", type=int, default=16384)
+    # per-GPU batch sized for HBM (≈87 GB of 288 GB): throughput 2.21 M (32k) -> 2.35 M (65k) ->
+    # 2.42 M (131k) -> 2.48 M seq/s (262k) on one MI355X (profiles/r01_batch_sweep)
+    ap.add_argument("--batch-per-gpu", type=int, default=262144)
     ap.add_argument("--window", type=int, default=24)
     ap.add_argument("--features", type=int, default=32)
     ap.add_argument("--dtype", default="bfloat16")
@@ -91,7 +93,7 @@ def main():
     if rank == 0:
         finite = all(np.isfinite(v) for k, v in losses.items() if k != "iteration")
         rec = {
-            "metric": "seq/sec/node MTSS-WGAN-GP train (24x32 windows)",
+            "metric": "seq/sec/node MTSS-WGAN-GP train (24x32 windows) at 1/2/4/8 GPUs; W-dist parity",
             "value": round(value, 2),
             "unit": "seq/s",
             "n_gpus": world,
@@ -114,6 +116,9 @@ def main():
                 "windows_per_step": per_rank * world,
             },
             "losses_finite": bool(finite),
+            # the W-dist half of the metric is a training-quality run, not a throughput step:
+            # `python -m hfrep parity` (fp32 vs bf16, B=32 vs 4096) -> profiles/r01_parity
+            "w_dist_parity": "profiles/r01_parity/README.md",
             "peak_mem_gb_rank0": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
         }
         print(json.dumps(rec))
