@@ -246,7 +246,19 @@ def cmd_replicate(a) -> int:
         ae = AE(x_tr, y_tr, x_te, y_te, a.latent)
         ae.train(verbose=0, plot=False)
         res["ae"] = {"latent": a.latent, "IS_r2": float(ae.model_IS_r2()), "OOS_r2": float(np.mean(ae.model_OOS_r2()))}
-    print(json.dumps(res, indent=1))
+    if a.method == "ae-sweep":
+        from .finance.experiment import generated_augmentation, latent_sweep
+
+        lo, _, hi = a.latents.partition("-")
+        latents = range(int(lo), int(hi or lo) + 1)
+        xe = ye = None
+        if a.augment:
+            xe, ye = generated_augmentation(np.load(a.augment, allow_pickle=False), c)
+        sw = latent_sweep(c, latents=latents, window=a.window, x_extra=xe, y_extra=ye, verbose=True)
+        res["ae_sweep"] = {"metrics": sw.metrics.to_dict(orient="index"),
+                           "sharpe_post": sw.sharpe_post.to_dict(orient="index"),
+                           "best": sw.best.to_dict(orient="index")}
+    print(json.dumps(res, indent=1, default=float))
     return 0
 
 
@@ -288,7 +300,9 @@ def main(argv=None) -> int:
     c.add_argument("--raw", required=True)
     c.add_argument("--out", required=True)
     r = sub.add_parser("replicate", help="hedge-fund clone benchmarks")
-    r.add_argument("--method", default="all", choices=["linear", "ae", "all"])
+    r.add_argument("--method", default="all", choices=["linear", "ae", "all", "ae-sweep"])
+    r.add_argument("--latents", default="1-21", help="ae-sweep latent sizes, e.g. 1-21")
+    r.add_argument("--augment", default=None, help="ae-sweep: generated windows .npy (F=36) to add to training")
     r.add_argument("--window", type=int, default=24)
     r.add_argument("--latent", type=int, default=12)
     sub.add_parser("bench", help="flagship throughput benchmark (bench.py flags)")

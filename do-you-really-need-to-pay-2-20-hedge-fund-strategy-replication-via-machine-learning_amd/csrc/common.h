@@ -88,6 +88,13 @@ __device__ __forceinline__ float act_d2y(int act, float y) {
   }
 }
 
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup-scope release fence
+// + s_barrier, and the fence waits for every outstanding global STORE (vmcnt(0)): in the
+// recurrent kernels that exposed the full write latency of each step's tape / h stores at every
+// step barrier (70% of wave cycles parked in lstm_fwd2).  Here only LDS traffic is drained; global
+// stores retire in the background and nothing in the kernel reads them back.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // ---------------------------------------------------------------------------
 // wave / block reductions (wave64)
 // ---------------------------------------------------------------------------

@@ -70,9 +70,11 @@ __device__ __forceinline__ void put4(uint32_t (&v)[4], int i, float x) {
 
 // stage W^T (K x G fp32, row-major) into LDS as bf16 [G][LX], zero-padded in k
 __device__ __forceinline__ void stage_wt(bf16_t* Wt, const float* __restrict__ W, int K, int G, int LX) {
+#pragma unroll 4
   for (int e = threadIdx.x; e < G * LX; e += blockDim.x) {
     const int k = e / G, n = e % G;  // consecutive threads read consecutive n (coalesced)
-    if (k < LX) Wt[n * LX + k] = f2bf(k < K ? W[(size_t)k * G + n] : 0.f);
+    const float v = W[(size_t)min(k, K - 1) * G + n];  // in-bounds load, then select: no per-element branch
+    Wt[n * LX + k] = f2bf(k < K ? v : 0.f);
   }
 }
 
@@ -170,7 +172,10 @@ __device__ __forceinline__ void make_wt(typename MF<bf16_t>::frag (&wt)[NKG], co
                                         int kc, int lane) {
 #pragma unroll
   for (int ks = 0; ks < NKG; ++ks)
-    wt[ks] = MF<bf16_t>::make([&](int n) { return (kc < K && n < G) ? W[(size_t)kc * G + n] : 0.f; }, ks, lane);
+    wt[ks] = MF<bf16_t>::make([&](int n) {
+      const float v = W[(size_t)min(kc, K - 1) * G + min(n, G - 1)];
+      return (kc < K && n < G) ? v : 0.f;
+    }, ks, lane);
 }
 __device__ __forceinline__ void store_dx(const f32x16& ax, bf16_t* __restrict__ dX, int row0, int B, int Tn, int t,
                                          int K, int kc, int lane) {
@@ -214,10 +219,15 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
   for (int i = ltid; i < 2 * 32 * LX; i += 256) xb[i] = 0;
   typename P::frag ub[4][NKH];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 4; ++q) {
 #pragma unroll
     for (int ks = 0; ks < NKH; ++ks)
-      ub[q][ks] = P::make([&](int k) { return (uok && k < H) ? U[k * G + q * H + u] : 0.f; }, ks, lane);
+      ub[q][ks] = P::make([&](int k) {
+        const float v = U[min(k, H - 1) * G + q * H + uc];
+        return (uok && k < H) ? v : 0.f;
+      }, ks, lane);
+    __builtin_amdgcn_sched_barrier(0);  // one gate's loads in flight at a time: bounded prologue live range
+  }
   float bq[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) bq[q] = (uok && bias) ? bias[q * H + u] : 0.f;
@@ -283,7 +293,7 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
       }
     }
     if (t + 1 < Tn) x_store_lds<KX>(pf, xb + ((t + 1) & 1) * 32 * LX, K, LX, ltid);
-    if (!(dbg & 32)) __syncthreads();
+    if (!(dbg & 32)) lds_barrier();  // step hand-off: LDS only, stores stay in flight
   }
   tile_to_hbm(hb + (Tn & 1) * 32 * LH, LH, hs, row0, B, Tn, Tn - 1, H, ltid);
   __syncthreads();  // LDS is re-initialised for the next row block
@@ -318,10 +328,15 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
   for (int i = ltid; i < 2 * 32 * LX; i += 256) xb[i] = 0;
   typename P::frag ub[4][NKH];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 4; ++q) {
 #pragma unroll
     for (int ks = 0; ks < NKH; ++ks)
-      ub[q][ks] = P::make([&](int k) { return (uok && k < H) ? U[k * G + q * H + u] : 0.f; }, ks, lane);
+      ub[q][ks] = P::make([&](int k) {
+        const float v = U[min(k, H - 1) * G + q * H + uc];
+        return (uok && k < H) ? v : 0.f;
+      }, ks, lane);
+    __builtin_amdgcn_sched_barrier(0);  // one gate's loads in flight at a time: bounded prologue live range
+  }
 
   for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
   const int rb = grp * TILES + tile, row0 = rb * 32;
@@ -406,7 +421,7 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
 #pragma unroll
       for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = tn[s];
     }
-    __syncthreads();
+    lds_barrier();  // step hand-off: LDS only, stores stay in flight
   }
   tile_to_hbm(hb + (Tn & 1) * 32 * LH, LH, hds, row0, B, Tn, Tn - 1, H, ltid);
   __syncthreads();
@@ -435,7 +450,10 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
   typename P::frag ut[NKG];
 #pragma unroll
   for (int ks = 0; ks < NKG; ++ks)
-    ut[ks] = P::make([&](int k) { return (uok && k < G) ? U[u * G + k] : 0.f; }, ks, lane);
+    ut[ks] = P::make([&](int k) {
+      const float v = U[(uok ? u : H - 1) * G + min(k, G - 1)];
+      return (uok && k < G) ? v : 0.f;
+    }, ks, lane);
   const int kc = w * 32 + (lane & 31);
   const bool xw = DX && w * 32 < K;  // this wave produces dx columns (wave-uniform)
   typename P::frag wt[DX ? NKG : 1];
@@ -533,7 +551,7 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
       cc = cp;
       cp = ncp;
     }
-    __syncthreads();
+    lds_barrier();  // step hand-off: LDS only, stores stay in flight
   }
   tile_to_hbm(zb, LG, dZ, row0, B, Tn, 0, G, ltid);
   if constexpr (DX) {
@@ -576,7 +594,10 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
   typename P::frag ut[NKG];
 #pragma unroll
   for (int ks = 0; ks < NKG; ++ks)
-    ut[ks] = P::make([&](int k) { return (uok && k < G) ? U[u * G + k] : 0.f; }, ks, lane);
+    ut[ks] = P::make([&](int k) {
+      const float v = U[(uok ? u : H - 1) * G + min(k, G - 1)];
+      return (uok && k < G) ? v : 0.f;
+    }, ks, lane);
   const int kc = w * 32 + (lane & 31);
   const bool xw = DX && w * 32 < K;  // this wave produces dx / dxdot columns (wave-uniform)
   typename P::frag wt[DX ? NKG : 1];
@@ -692,7 +713,7 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
       cc = cp;
       cdc = cdp;
     }
-    __syncthreads();
+    lds_barrier();  // step hand-off: LDS only, stores stay in flight
   }
   tile_to_hbm(zb, LG, dZ, row0, B, Tn, 0, G, ltid);
   tile_to_hbm(zdb, LG, dZd, row0, B, Tn, 0, G, ltid);

@@ -21,21 +21,33 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running test")
 
 
-@pytest.fixture(scope="session")
-def data_root():
+def _first_root_with(sub):
     from hfrep.data.io import data_root as _dr
 
-    r = _dr()
-    if r is None or not os.path.isdir(os.path.join(r, "data")):
+    for r in (os.environ.get("HFREP_DATA_ROOT"), "/root/reference", _dr()):
+        if r and os.path.isdir(os.path.join(r, sub)):
+            return r
+    return None
+
+
+@pytest.fixture(scope="session")
+def data_root():
+    """A root with the RAW reference data (data/) and cleaned_data/."""
+    r = _first_root_with("data")
+    if r is None or not os.path.isdir(os.path.join(r, "cleaned_data")):
         pytest.skip("reference dataset not available")
     return r
 
 
 @pytest.fixture(scope="session")
-def cleaned(data_root):
+def cleaned():
+    """The cleaned panel only (cleaned_data/: also staged under assets/ for GPU runs)."""
+    r = _first_root_with("cleaned_data")
+    if r is None:
+        pytest.skip("cleaned reference data not available")
     from hfrep.data.io import load_cleaned
 
-    return load_cleaned(data_root)
+    return load_cleaned(r)
 
 
 @pytest.fixture

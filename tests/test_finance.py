@@ -111,3 +111,25 @@ def test_res_sort():
     b = pd.DataFrame({"Annualized_Sharpe": [0.5, 0.2]}, index=["x", "y"])
     best, idx = A.res_sort([a, b])
     assert idx == [1, 0] and list(best.index) == ["x latent 2", "y latent 1"]
+
+
+def test_latent_sweep_and_augmentation(cleaned):
+    """Notebook experiment driver (P31/P32): AE per latent size -> metrics, clone Sharpes, turnover,
+    best latent per strategy; generated windows -> extra training rows in return units."""
+    from hfrep.finance.experiment import generated_augmentation, latent_sweep
+
+    res = latent_sweep(cleaned, latents=[1, 3])
+    assert list(res.metrics.index) == [1, 3]
+    assert (res.metrics["IS_r2"] <= 1).all() and np.isfinite(res.metrics.to_numpy()).all()
+    assert res.sharpe_post.shape == (2, cleaned["hfd"].shape[1])
+    assert np.isfinite(res.sharpe_post.to_numpy()).all() and (res.turnover.to_numpy() >= 0).all()
+    assert set(res.best["latent"]) <= {1, 3} and len(res.best) == cleaned["hfd"].shape[1]
+
+    gen = np.random.RandomState(0).rand(4, 10, 36).astype(np.float32)
+    x, y = generated_augmentation(gen, cleaned)
+    assert x.shape == (40, 22) and y.shape == (40, 13)
+    panel = cleaned["factor_etf_data"].join(cleaned["hfd"]).join(cleaned["rf"]).to_numpy()
+    lo, hi = panel.min(0), panel.max(0)
+    assert (x >= lo[:22] - 1e-9).all() and (x <= hi[:22] + 1e-9).all()
+    aug = latent_sweep(cleaned, latents=[2], x_extra=x, y_extra=y)
+    assert np.isfinite(aug.metrics.to_numpy()).all()
