@@ -148,8 +148,16 @@ lstm_wgrad2_reduce_kernel(const float* __restrict__ slab, float* __restrict__ gW
   const int Ktot = K + Hd + 1;
   const int64_t total = (int64_t)Ktot * N;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += slab[(size_t)z * total + e];
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // 4 independent chains: loads stay in flight
+    int z = 0;
+    for (; z + 3 < splits; z += 4) {
+      s0 += slab[(size_t)z * total + e];
+      s1 += slab[(size_t)(z + 1) * total + e];
+      s2 += slab[(size_t)(z + 2) * total + e];
+      s3 += slab[(size_t)(z + 3) * total + e];
+    }
+    for (; z < splits; ++z) s0 += slab[(size_t)z * total + e];
+    const float s = (s0 + s1) + (s2 + s3);
     const int i = (int)(e / N), j = (int)(e % N);
     if (i < K) gW[(size_t)i * N + j] += s;
     else if (i < K + Hd) gU[(size_t)(i - K) * N + j] += s;

@@ -137,21 +137,32 @@ __global__ void __launch_bounds__(1024) skinny_wgrad_kernel(const bf16_t* __rest
   }
 }
 
-// sum the split slabs: 64 consecutive elements per workgroup, the 4 waves split the slabs (fixed
+// sum the split slabs: 64 consecutive elements per workgroup, 16 waves split the slabs (fixed
 // order: deterministic).  Elements [0, KN) accumulate into gW, [KN, KN + N) into gb (if non-null).
-__global__ void __launch_bounds__(256) skinny_reduce_kernel(const float* __restrict__ slab, float* __restrict__ gW,
-                                                            float* __restrict__ gb, int splits, int KN, int N) {
-  __shared__ float part[4][64];
+__global__ void __launch_bounds__(1024) skinny_reduce_kernel(const float* __restrict__ slab, float* __restrict__ gW,
+                                                             float* __restrict__ gb, int splits, int KN, int N) {
+  // 16 waves split the slabs (4 independent partial sums each, so loads overlap), fixed order
+  __shared__ float part[16][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + lane;
   const int total = KN + N;
-  float s = 0.f;
-  if (e < total)
-    for (int z = wv; z < splits; z += 4) s += slab[(size_t)z * total + e];
-  part[wv][lane] = s;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (e < total) {
+    int z = wv;
+    for (; z + 48 < splits; z += 64) {
+      s0 += slab[(size_t)z * total + e];
+      s1 += slab[(size_t)(z + 16) * total + e];
+      s2 += slab[(size_t)(z + 32) * total + e];
+      s3 += slab[(size_t)(z + 48) * total + e];
+    }
+    for (; z < splits; z += 16) s0 += slab[(size_t)z * total + e];
+  }
+  part[wv][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (wv == 0 && e < total) {
-    const float t = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += part[w][lane];
     if (e < KN) {
       if (gW) gW[e] += t;
     } else if (gb) {
@@ -220,12 +231,12 @@ void launch_skinny_wgrad(const void* x, const void* d, float* gW, float* gb, int
   HFREP_SKINNY_N(N, skinny_wgrad_kernel, dim3(splits), dim3(threads), 0, s, (const bf16_t*)x, (const bf16_t*)d, ws, M, K,
                  rps)
   const int total = (K + 1) * N;
-  hipLaunchKernelGGL(skinny_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, s, ws, gW, gb, splits, K * N, N);
+  hipLaunchKernelGGL(skinny_reduce_kernel, dim3((total + 63) / 64), dim3(1024), 0, s, ws, gW, gb, splits, K * N, N);
 }
 
 void launch_split_reduce(const float* slab, float* a, float* b, int splits, int na, int nb, hipStream_t s) {
   const int total = na + nb;
-  hipLaunchKernelGGL(skinny_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, s, slab, a, b, splits, na, nb);
+  hipLaunchKernelGGL(skinny_reduce_kernel, dim3((total + 63) / 64), dim3(1024), 0, s, slab, a, b, splits, na, nb);
 }
 
 void launch_skinny_dgrad(const void* d, const float* W, void* dx, int M, int K, int N, hipStream_t s) {
