@@ -139,6 +139,28 @@ __device__ __forceinline__ void x_store_lds(const XPref& p, bf16_t* xb, int K, i
   }
 }
 
+// [32 x W] bf16 tile in LDS (row stride LD) -> HBM (B,T,W) in 16-byte chunks; W % 8 == 0 and
+// LD % 8 == 0 (16-byte aligned rows on both sides).  16 threads per row, two rows per pass of the
+// tile's 256 threads: each thread walks one row with pointer increments (no per-chunk division),
+// and 16 consecutive threads write 256 contiguous bytes of a row.
+template <int W>
+__device__ __forceinline__ void tile16_to_hbm(const bf16_t* buf, int LD, bf16_t* __restrict__ dst, int row0, int B,
+                                              int Tn, int t, int ltid) {
+  static_assert(W % 8 == 0, "16-byte chunks");
+  constexpr int CPR = W / 8;
+  const int c0 = ltid & 15;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int r = (ltid >> 4) + 16 * pass, row = row0 + r;
+    if (row >= B) continue;
+    const bf16_t* s = buf + r * LD + 8 * c0;
+    bf16_t* d = dst + ((size_t)row * Tn + t) * W + 8 * c0;
+#pragma unroll
+    for (int c = c0; c < CPR; c += 16, s += 128, d += 128)
+      *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+  }
+}
+
 // row-major [32 x width] tile <-> HBM (B,T,width) with 8-byte chunks (width % 4 == 0), moved by the
 // 256 threads of one row tile (ltid = thread index within the tile)
 __device__ __forceinline__ void tile_to_hbm(const bf16_t* buf, int LD, bf16_t* __restrict__ dst, int row0, int B, int Tn,
@@ -434,7 +456,8 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
 template <int H, int ACT, int TILES, bool DX>
 __global__ void __launch_bounds__(256 * TILES)
 lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape, const float* __restrict__ U,
-                 bf16_t* __restrict__ dZ, const float* __restrict__ W, bf16_t* __restrict__ dX, int B, int Tn, int K) {
+                 bf16_t* __restrict__ dZ, const float* __restrict__ W, bf16_t* __restrict__ dX, int B, int Tn, int K,
+                 int dbg) {
   constexpr int act = ACT;
   using P = MF<bf16_t>;
   constexpr int G = 4 * H, NKG = (G + 15) / 16, LG = NKG * 16 + 8, NKH = (H + 15) / 16, LH = NKH * 16 + 8;
@@ -483,11 +506,11 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
     const bf16_t* zprev = zb + ((t + 1) & 1) * 32 * LG;  // dz_{t+1}
     bf16_t* zcur = zb + (t & 1) * 32 * LG;               // dz_t
     const bf16_t* dhcur = dhb + (t & 1) * 32 * LH;
-    if (t < Tn - 1) tile_to_hbm(zprev, LG, dZ, row0, B, Tn, t + 1, G, ltid);
+    if (t < Tn - 1 && !(dbg & 1)) tile16_to_hbm<G>(zprev, LG, dZ, row0, B, Tn, t + 1, ltid);
     // prefetch the next (t-1) step: tape gates(t-1), cell(t-2), dH(t-1)
     Slot16 ng[4], ncp;
     uint2 ndh[4];
-    if (t > 0) {
+    if (t > 0 && !(dbg & 2)) {
       const bf16_t* tp = tape + tape_base(rbt, t - 1, Tn, w) + lane * 16;
 #pragma unroll
       for (int s = 0; s < 4; ++s) ng[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
@@ -503,7 +526,7 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
       }
     }
     f32x16 acc = zero16();
-    if (t < Tn - 1) {
+    if (t < Tn - 1 && !(dbg & 4)) {
       const bf16_t* arow = zprev + (lane & 31) * LG;
       if (xw) {
         f32x16 ax = zero16();
@@ -533,12 +556,12 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
       float z1 = dct * cpv * fg * (1.f - fg);
       float z2 = dct * ig * act_dy(act, gg);
       float z3 = dov * og * (1.f - og);
-      if (uok) {
+      if (uok && !(dbg & 8)) {
         bf16_t* zr = zcur + rr * LG + u;
         zr[0] = f2bf(z0); zr[H] = f2bf(z1); zr[2 * H] = f2bf(z2); zr[3 * H] = f2bf(z3);
       }
     }
-    if (t > 0) {
+    if (t > 0 && !(dbg & 2)) {
       bf16_t* dnext = dhb + ((t - 1) & 1) * 32 * LH;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -551,9 +574,9 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
       cc = cp;
       cp = ncp;
     }
-    lds_barrier();  // step hand-off: LDS only, stores stay in flight
+    if (!(dbg & 32)) lds_barrier();  // step hand-off: LDS only, stores stay in flight
   }
-  tile_to_hbm(zb, LG, dZ, row0, B, Tn, 0, G, ltid);
+  tile16_to_hbm<G>(zb, LG, dZ, row0, B, Tn, 0, ltid);
   if constexpr (DX) {
     if (xw) {
       f32x16 ax = zero16();
@@ -624,8 +647,13 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
   for (int t = Tn - 1; t >= 0; --t) {
     const int cb = t & 1, nb = (t + 1) & 1;
     if (t < Tn - 1) {
-      tile_to_hbm(zb + nb * 32 * LG, LG, dZ, row0, B, Tn, t + 1, G, ltid);
-      tile_to_hbm(zdb + nb * 32 * LG, LG, dZd, row0, B, Tn, t + 1, G, ltid);
+      if constexpr (DX) {  // (the 16-byte copy perturbs this variant's register allocation into spills)
+        tile_to_hbm(zb + nb * 32 * LG, LG, dZ, row0, B, Tn, t + 1, G, ltid);
+        tile_to_hbm(zdb + nb * 32 * LG, LG, dZd, row0, B, Tn, t + 1, G, ltid);
+      } else {
+        tile16_to_hbm<G>(zb + nb * 32 * LG, LG, dZ, row0, B, Tn, t + 1, ltid);
+        tile16_to_hbm<G>(zdb + nb * 32 * LG, LG, dZd, row0, B, Tn, t + 1, ltid);
+      }
     }
     // this step's tapes
     Slot16 tg[4], zd[4], cp, cdp;
@@ -715,8 +743,8 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
     }
     lds_barrier();  // step hand-off: LDS only, stores stay in flight
   }
-  tile_to_hbm(zb, LG, dZ, row0, B, Tn, 0, G, ltid);
-  tile_to_hbm(zdb, LG, dZd, row0, B, Tn, 0, G, ltid);
+  tile16_to_hbm<G>(zb, LG, dZ, row0, B, Tn, 0, ltid);
+  tile16_to_hbm<G>(zdb, LG, dZd, row0, B, Tn, 0, ltid);
   if constexpr (DX) {
     if (xw) {
       f32x16 ax = zero16(), axd = zero16();
@@ -856,10 +884,10 @@ void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ
   const bf16_t* tp = (const bf16_t*)tape;
   if (dX)  // fused input gradient: U^T and W^T fragments in registers -> one row tile per workgroup
     HFREP_BWD_LAUNCH(lstm_bwd2_kernel, 1, true, persistent_grid(B, 1), 256, bwd_smem(H, 1), s, dh, tp, U, (bf16_t*)dZ,
-                     W, (bf16_t*)dX, B, Tn, K)
+                     W, (bf16_t*)dX, B, Tn, K, lstm_dbg())
   else  // (two row tiles per workgroup spill the U^T fragments at 256 VGPRs: measured slower)
     HFREP_BWD_LAUNCH(lstm_bwd2_kernel, 1, false, persistent_grid(B, 1), 256, bwd_smem(H, 1), s, dh, tp, U, (bf16_t*)dZ,
-                     (const float*)nullptr, (bf16_t*)nullptr, B, Tn, 0)
+                     (const float*)nullptr, (bf16_t*)nullptr, B, Tn, 0, lstm_dbg())
 }
 void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const void* ttape, const float* U, void* dZ,
                        void* dZd, const float* W, void* dX, void* dXd, int K, int B, int Tn, int H, int act,
