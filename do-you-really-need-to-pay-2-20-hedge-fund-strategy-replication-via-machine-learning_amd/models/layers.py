@@ -503,10 +503,13 @@ class Sequential(torch.nn.Module):
     def predict(self, x):
         return self.efwd(x, save=False)[0]
 
-    def ebwd(self, tape, dy, need_dx: bool = False, wgrad: bool = True):
+    def ebwd(self, tape, dy, need_dx: bool = False, wgrad: bool = True, hook=None):
+        """Reverse pass; ``hook(i)`` runs after layer i (its gradients are then final)."""
         for i in range(len(self.layers) - 1, -1, -1):
             need = need_dx or i > 0
             dy = self.layers[i].ebwd(tape[i], dy, need, wgrad)
+            if hook is not None:
+                hook(i)
         return dy
 
     def etfwd(self, tape, xd):
@@ -516,8 +519,36 @@ class Sequential(torch.nn.Module):
             ttape.append(tctx)
         return xd, ttape
 
-    def etbwd(self, tape, ttape, dy, dyd, need_dx: bool = False):
+    def etbwd(self, tape, ttape, dy, dyd, need_dx: bool = False, hook=None):
         for i in range(len(self.layers) - 1, -1, -1):
             need = need_dx or i > 0
             dy, dyd = self.layers[i].etbwd(tape[i], ttape[i], dy, dyd, need)
+            if hook is not None:
+                hook(i)
         return dy, dyd
+
+    def grad_buckets(self, n: int = 2) -> list[tuple[int, int, int]]:
+        """Split the flat gradient buffer at layer boundaries into <= n buckets of similar size.
+
+        Returns ``[(first_layer, start, end)]`` in reverse-pass completion order (the bucket of
+        the LAST layers first): bucket b is final as soon as the reverse pass has processed its
+        ``first_layer``, so its all-reduce can overlap the backward of the earlier layers.
+        """
+        starts = []
+        for li, l in enumerate(self.layers):
+            if l.specs:
+                starts.append((li, min(s.offset for s in l.specs)))
+        if not starts:
+            return []
+        total = self.numel_padded
+        cuts = [starts[0]]
+        for k in range(1, max(n, 1)):  # the layer boundary closest to k/n of the buffer
+            goal = total * k / n
+            li, off = min(starts[1:] or starts, key=lambda c: abs(c[1] - goal))
+            if off > cuts[-1][1]:
+                cuts.append((li, off))
+        out = []
+        for j, (li, off) in enumerate(cuts):
+            end = cuts[j + 1][1] if j + 1 < len(cuts) else total
+            out.append((li, off, end))
+        return out[::-1]

@@ -50,9 +50,10 @@ def init_distributed(backend: str | None = None, timeout_s: float = 600.0):
 class GradSync:
     """Averages flat gradient buckets across ranks (one collective per model per step)."""
 
-    def __init__(self, group, world: int):
-        self.group, self.world = group, world
+    def __init__(self, group, world: int, buckets: int = 2):
+        self.group, self.world, self.buckets = group, world, buckets
         self.backend = dist.get_backend(group) if group is not None else None
+        self._pending = []
 
     def all_reduce_(self, flat_grad: torch.Tensor) -> None:
         if self.world <= 1:
@@ -62,6 +63,34 @@ class GradSync:
         else:
             dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.group)
             flat_grad.div_(self.world)
+
+    # ---- bucketed, overlapped reduction -------------------------------------------------------
+    def start_(self, grad_slice: torch.Tensor):
+        """Launch the average of one gradient bucket without blocking the compute stream.
+
+        ProcessGroupNCCL orders the collective after the work already queued on the current
+        stream and runs it on its own stream, so the backward of the remaining (earlier) layers
+        keeps running while this bucket is reduced over xGMI; :meth:`finish_` makes the compute
+        stream wait for all launched buckets before the optimizer reads the gradients.
+        """
+        if self.world <= 1:
+            return
+        if self.backend == "nccl":
+            self._pending.append(dist.all_reduce(grad_slice, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
+        else:
+            self._pending.append((dist.all_reduce(grad_slice, op=dist.ReduceOp.SUM, group=self.group,
+                                                  async_op=True), grad_slice))
+
+    def finish_(self) -> int:
+        n = len(self._pending)
+        for w in self._pending:
+            if isinstance(w, tuple):
+                w[0].wait()
+                w[1].div_(self.world)
+            else:
+                w.wait()
+        self._pending = []
+        return n
 
     def broadcast_params(self, models, src: int = 0) -> None:
         if self.world <= 1:

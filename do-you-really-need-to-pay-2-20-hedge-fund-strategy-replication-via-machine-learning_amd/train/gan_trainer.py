@@ -110,9 +110,25 @@ class GANTrainer:
         noise = self.rng.normal((B, self.cfg.window, self.cfg.features), dtype=self.dtype)
         return real, noise
 
+    def _hook(self, model):
+        """Reverse-pass hook that launches each gradient bucket's all-reduce as soon as it is
+        final (None when single-process): the reduction of the last layers overlaps the backward
+        of the first ones."""
+        if self.grad_sync is None or self.grad_sync.buckets <= 1:
+            return None
+        plan = {li: (a, b) for li, a, b in model.grad_buckets(self.grad_sync.buckets)}
+        g = model.flat.grad
+
+        def hook(i):
+            if i in plan:
+                a, b = plan[i]
+                self.grad_sync.start_(g[a:b])
+        return hook
+
     def _sync(self, model):
         if self.grad_sync is not None:
-            self.grad_sync.all_reduce_(model.flat.grad)
+            if self.grad_sync.finish_() == 0:  # no overlapped buckets were launched
+                self.grad_sync.all_reduce_(model.flat.grad)
 
     def _apply(self, model, clip=0.0):
         self._sync(model)
@@ -129,7 +145,7 @@ class GANTrainer:
         loss = -(label * torch.log(o + R.KERAS_EPS) + (1 - label) * torch.log(1 - o + R.KERAS_EPS)).mean()
         inside = ((pf > R.KERAS_EPS) & (pf < 1 - R.KERAS_EPS)).to(pf.dtype)
         dp = -(label / (o + R.KERAS_EPS) - (1 - label) / (1 - o + R.KERAS_EPS)) * inside / n
-        C.ebwd(tape, dp.to(p.dtype))
+        C.ebwd(tape, dp.to(p.dtype), hook=self._hook(C))
         self._apply(C)
         return loss
 
@@ -138,7 +154,7 @@ class GANTrainer:
         s, tape = C.efwd(x, save=True)
         loss = label * s.to(self._acc).mean()
         ds = torch.full_like(s, label / s.numel())
-        C.ebwd(tape, ds)
+        C.ebwd(tape, ds, hook=self._hook(C))
         self._apply(C, clip=clip)
         return loss
 
@@ -167,7 +183,7 @@ class GANTrainer:
         g = C.ebwd(tape_h, torch.ones_like(sh), need_dx=True, wgrad=False)
         pen, v = Fn.gp_coef(g, self.gp_weight)
         sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
-        C.etbwd(tape_h, ttape, None, torch.ones_like(sd))
+        C.etbwd(tape_h, ttape, None, torch.ones_like(sd), hook=self._hook(C))
         sf = s.to(self._acc)
         w_real = -sf[:B].mean()
         w_fake = sf[B:].mean()
@@ -195,7 +211,7 @@ class GANTrainer:
             loss = -s.to(self._acc).mean()
             ds = torch.full_like(s, -1.0 / s.numel())
         dfake = C.ebwd(tc, ds, need_dx=True, wgrad=False)
-        G.ebwd(tg, dfake)
+        G.ebwd(tg, dfake, hook=self._hook(G))
         return loss
 
     # ---- one reference "epoch" (= iteration) ----------------------------------------------------

@@ -1,7 +1,8 @@
 """Data-parallel correctness on CPU (gloo, world_size 2) — SURVEY §4 item 3.
 
-* bucketed DP gradients (one flat all-reduce per model) equal the single-process gradient of the
-  concatenated global batch (fp64), for the GP critic and the generator;
+* bucketed DP gradients (two buckets per model, each all-reduce launched from the reverse pass as
+  soon as its layers are final) equal the single-process gradient of the concatenated global
+  batch (fp64), for the GP critic and the generator;
 * a DP training run keeps every rank's parameters bit-identical (same averaged update everywhere).
 The same code path runs over RCCL on GPUs (backend 'nccl'); only the backend differs.
 """
@@ -44,10 +45,10 @@ def _worker(rank, world, port, q):
         sl = slice(r * (B // w), (r + 1) * (B // w))
         with torch.no_grad():
             fake = tr.generator.predict(noise)
-            tr.critic_gp_grads(real[sl], fake[sl], alpha[sl])
-            tr.grad_sync.all_reduce_(tr.critic.flat.grad)
+            tr.critic_gp_grads(real[sl], fake[sl], alpha[sl])  # launches its bucket all-reduces
+            tr._sync(tr.critic)                                # ... and waits for them
             tr.generator_grads(noise[sl])
-            tr.grad_sync.all_reduce_(tr.generator.flat.grad)
+            tr._sync(tr.generator)
         out = {"critic": tr.critic.flat.grad.clone(), "gen": tr.generator.flat.grad.clone()}
         tr.critic.zero_grad(); tr.generator.zero_grad()
         tr.train(3, verbose=False)
