@@ -337,6 +337,27 @@ Tensor layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, optiona
   return dx;
 }
 
+// ------------------------------------------------------------------------------------ conv1d (causal)
+Tensor im2col_causal(Tensor x, int64_t k, int64_t dil) {
+  CHECK_GPU(x);
+  TORCH_CHECK(x.dim() == 3 && k >= 1 && dil >= 1, "im2col_causal: (B,T,C), k, dil");
+  GUARD(x);
+  const int B = x.size(0), Tn = x.size(1), C = x.size(2);
+  Tensor cols = at::empty({B, Tn, k * C}, x.options());
+  hfrep::launch_im2col_causal(dt_of(x), x.data_ptr(), cols.data_ptr(), B, Tn, C, (int)k, (int)dil, cur_stream(x));
+  return cols;
+}
+Tensor col2im_causal(Tensor dcols, int64_t k, int64_t dil, int64_t C) {
+  CHECK_GPU(dcols);
+  TORCH_CHECK(dcols.dim() == 3 && dcols.size(2) == k * C, "col2im_causal: (B,T,k*C)");
+  GUARD(dcols);
+  const int B = dcols.size(0), Tn = dcols.size(1);
+  Tensor dx = at::empty({B, Tn, C}, dcols.options());
+  hfrep::launch_col2im_causal(dt_of(dcols), dcols.data_ptr(), dx.data_ptr(), B, Tn, (int)C, (int)k, (int)dil,
+                              cur_stream(dcols));
+  return dx;
+}
+
 // ------------------------------------------------------------------------------------ WGAN-GP helpers
 std::tuple<Tensor, Tensor> gp_coef(Tensor g, double weight) {
   CHECK_GPU(g); GUARD(g);
@@ -446,6 +467,8 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, Tensor(a!)? ggamma, Tensor(b!)? gbeta) -> Tensor");
   m.def("gp_coef(Tensor g, float weight) -> (Tensor, Tensor)");
+  m.def("im2col_causal(Tensor x, int k, int dil) -> Tensor");
+  m.def("col2im_causal(Tensor dcols, int k, int dil, int C) -> Tensor");
   m.def("interpolate(Tensor real, Tensor fake, Tensor alpha) -> Tensor");
   m.def("philox_fill_(Tensor(a!) out, int seed, Tensor(b!) ctr, int dist) -> ()");
   m.def("sample_windows(Tensor data, int batch, int seed, Tensor(a!) ctr, ScalarType out_dtype) -> Tensor");
@@ -475,6 +498,8 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("layernorm_bwd_", &layernorm_bwd_);
   m.impl("gp_coef", &gp_coef);
+  m.impl("im2col_causal", &im2col_causal);
+  m.impl("col2im_causal", &col2im_causal);
   m.impl("interpolate", &interpolate);
   m.impl("philox_fill_", &philox_fill_);
   m.impl("sample_windows", &sample_windows);

@@ -75,6 +75,8 @@ void launch_split_reduce(const float* slab, float* a, float* b, int splits, int 
 
 // ---- misc.hip ----
 int device_cu_count();  // compute units of the current device (cached)
+void launch_im2col_causal(int dt, const void* x, void* cols, int B, int Tn, int C, int k, int dil, hipStream_t s);
+void launch_col2im_causal(int dt, const void* dcols, void* dx, int B, int Tn, int C, int k, int dil, hipStream_t s);
 void launch_act_fwd(int dt, const void* x, void* y, int64_t n, int act, hipStream_t s);
 void launch_act_bwd(int dt, const void* dy, const void* y, void* dx, int64_t n, int act, hipStream_t s);
 void launch_act_tangent_bwd(int dt, const void* dyd, const void* y, const void* zd, void* out, int64_t n, int act,

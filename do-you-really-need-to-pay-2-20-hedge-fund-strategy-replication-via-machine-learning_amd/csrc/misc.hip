@@ -305,6 +305,58 @@ void launch_cast(int dt_in, const void* in, int dt_out, void* out, int64_t n, hi
     hipLaunchKernelGGL((cast_kernel<float, float>), dim3(ew_grid(n)), dim3(256), 0, s, (const float*)in, (float*)out, n);
 }
 
+// ------------------------------------------------------------------ causal dilated conv1d (im2col)
+// cols[b, t, j*C + c] = x[b, t - (k-1-j)*dil, c] (0 before the start): the Conv1D layer is then a
+// Dense GEMM over (k*C) columns (models/layers.py Conv1D); col2im is the matching GATHER (no
+// atomics): dx[b, t, c] = sum_j dcols[b, t + (k-1-j)*dil, j*C + c].
+template <typename T>
+__global__ void __launch_bounds__(256) im2col_causal_kernel(const T* __restrict__ x, T* __restrict__ cols, int B, int Tn,
+                                                            int C, int k, int dil) {
+  const int64_t n = (int64_t)B * Tn * k * C;
+  const int KC = k * C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t bt = i / KC;
+    const int jc = (int)(i - bt * KC), j = jc / C, c = jc - j * C;
+    const int t = (int)(bt % Tn);
+    const int src = t - (k - 1 - j) * dil;
+    cols[i] = src >= 0 ? x[(bt - t + src) * C + c] : Cvt<T>::from_f(0.f);
+  }
+}
+template <typename T>
+__global__ void __launch_bounds__(256) col2im_causal_kernel(const T* __restrict__ dcols, T* __restrict__ dx, int B,
+                                                            int Tn, int C, int k, int dil) {
+  const int64_t n = (int64_t)B * Tn * C;
+  const int KC = k * C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t bt = i / C;
+    const int c = (int)(i - bt * C), t = (int)(bt % Tn);
+    float s = 0.f;
+    for (int j = 0; j < k; ++j) {
+      const int dst = t + (k - 1 - j) * dil;
+      if (dst < Tn) s += ld_f(dcols + (bt - t + dst) * KC + j * C + c);
+    }
+    st_f(dx + i, s);
+  }
+}
+void launch_im2col_causal(int dt, const void* x, void* cols, int B, int Tn, int C, int k, int dil, hipStream_t s) {
+  const int64_t n = (int64_t)B * Tn * k * C;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(im2col_causal_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, s, (const bf16_t*)x,
+                       (bf16_t*)cols, B, Tn, C, k, dil);
+  else
+    hipLaunchKernelGGL(im2col_causal_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, s, (const float*)x, (float*)cols,
+                       B, Tn, C, k, dil);
+}
+void launch_col2im_causal(int dt, const void* dcols, void* dx, int B, int Tn, int C, int k, int dil, hipStream_t s) {
+  const int64_t n = (int64_t)B * Tn * C;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(col2im_causal_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, s, (const bf16_t*)dcols,
+                       (bf16_t*)dx, B, Tn, C, k, dil);
+  else
+    hipLaunchKernelGGL(col2im_causal_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, s, (const float*)dcols,
+                       (float*)dx, B, Tn, C, k, dil);
+}
+
 int device_cu_count() {
   static int cus = 0;
   if (!cus) {

@@ -158,6 +158,8 @@ def layer_norm_bwd_(dy, xhat, rstd, gamma, ggamma, gbeta):
 # ---------------------------------------------------------------------------------------
 def im2col_causal(x: torch.Tensor, k: int, dil: int) -> torch.Tensor:
     """(B, T, C) -> (B, T, k*C) with column block j holding x[t - (k-1-j)*dil] (zero padded)."""
+    if _nat(x):
+        return _ops().im2col_causal(x.contiguous(), int(k), int(dil))
     B, T, C = x.shape
     pad = (k - 1) * dil
     xp = torch.nn.functional.pad(x, (0, 0, pad, 0))
@@ -166,6 +168,9 @@ def im2col_causal(x: torch.Tensor, k: int, dil: int) -> torch.Tensor:
 
 
 def col2im_causal(dcols: torch.Tensor, k: int, dil: int, C: int) -> torch.Tensor:
+    """Adjoint of :func:`im2col_causal` (a gather on the GPU: no atomics)."""
+    if _nat(dcols):
+        return _ops().col2im_causal(dcols.contiguous(), int(k), int(dil), int(C))
     B, T, _ = dcols.shape
     pad = (k - 1) * dil
     dxp = dcols.new_zeros(B, T + pad, C)

@@ -390,3 +390,37 @@ def test_gp_coef_many_rows(cuda, B, D):
     rv = -(2 * 10.0 / B) * ((1 - nrm) / nrm)[:, None] * xd
     assert abs(pen.item() - rpen.item()) < 1e-3 * max(1.0, rpen.item())
     _close(v, rv, torch.bfloat16)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,T,C,k,dil", [(3, 24, 32, 3, 1), (5, 17, 100, 3, 2), (2, 5, 7, 4, 3)])
+def test_conv1d_im2col_col2im(cuda, dt, B, T, C, k, dil):
+    """Native causal im2col / col2im (csrc/misc.hip) vs the PyTorch formulation; col2im is the
+    adjoint of im2col: <im2col(x), y> == <x, col2im(y)>."""
+    from hfrep.ops import functional as Fn
+
+    g = torch.Generator().manual_seed(50)
+    x = torch.randn(B, T, C, generator=g).to(dt)
+    y = torch.randn(B, T, k * C, generator=g).to(dt)
+    cols = Fn.im2col_causal(x.to(cuda), k, dil).cpu()
+    ref = Fn.im2col_causal(x, k, dil)
+    assert torch.equal(cols, ref)
+    dx = Fn.col2im_causal(y.to(cuda), k, dil, C).cpu()
+    rdx = Fn.col2im_causal(y.double(), k, dil, C)
+    _close(dx, rdx, dt, scale=k * y.double().abs().max().item())
+    lhs = (ref.double() * y.double()).sum()
+    rhs = (x.double() * rdx).sum()
+    assert abs(lhs - rhs) < 1e-6 * max(1.0, abs(lhs.item()))
+
+
+def test_conv_critic_trains_native(cuda):
+    """conv WGAN-GP variant (K14): a bf16 training iteration on the GPU runs and stays finite."""
+    from hfrep.train.gan_trainer import GANConfig, GANTrainer
+
+    ds = np.random.RandomState(0).rand(256, 24, 32).astype(np.float32)
+    tr = GANTrainer(GANConfig(arch="conv", loss="wgan_gp", window=24, features=32, batch_size=128, dtype="bfloat16"),
+                    ds, device=cuda)
+    for _ in range(2):
+        tr.train_step()
+    rec = tr.losses()
+    assert all(np.isfinite(v) for k, v in rec.items() if k != "iteration")
