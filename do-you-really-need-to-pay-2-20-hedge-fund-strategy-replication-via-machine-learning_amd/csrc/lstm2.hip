@@ -9,8 +9,9 @@
 //    prefetched one step ahead into registers and written to a double-buffered LDS tile, so the
 //    HBM latency hides under the previous step's MFMA + gate math.  zx never exists in HBM;
 //  * tapes (gate activations + cell state for BPTT; tangent pre-activations + cell tangent for the
-//    GP's reverse pass) are stored in a BLOCKED layout [rowblock][t][wave][slot][lane][16] that
-//    matches the accumulator layout: each lane moves its 16 values with two 16-byte accesses;
+//    GP's reverse pass) are stored in a BLOCKED layout [rowblock][t][wave][slot][half][lane][8]
+//    that matches the accumulator layout: each lane moves its 16 values with two 16-byte accesses
+//    and every wave-level access covers 1 KiB of contiguous memory;
 //  * row-major activations (h, dH, dZ) go through the LDS tile that the recurrence needs anyway
 //    and are streamed to/from HBM with coalesced 8-byte accesses by the whole workgroup.
 //
@@ -30,6 +31,10 @@ namespace {
 constexpr int NW2 = 4;       // waves per workgroup: 4 x 32 units covers H <= 128
 constexpr int TAPE_SLOTS = 5;  // 4 gates (or 4 tangent pre-activations) + cell (or cell tangent)
 constexpr int SLOT_ELEMS = 64 * 16;
+// a slot is [half][lane][8]: lane l's 16 values are two 16-byte pieces 1 KiB apart, so every
+// wave-level 16-byte store / load of a tape slot covers one contiguous 1 KiB (whole cache lines;
+// the [lane][16] form left 16-byte holes in every line and cost ~1/3 of lstm_fwd2's time)
+constexpr int SLOT_HALF = 64 * 8;
 
 __device__ __forceinline__ size_t tape_base(int rb, int t, int Tn, int w) {
   return (((size_t)rb * Tn + t) * NW2 + w) * TAPE_SLOTS * SLOT_ELEMS;
@@ -54,14 +59,10 @@ __device__ __forceinline__ Slot16 ld_slot(bool on, const bf16_t* p) {
   s.a = make_uint4(0, 0, 0, 0);
   s.b = s.a;
   if (on) {
-    s.a = reinterpret_cast<const uint4*>(p)[0];
-    s.b = reinterpret_cast<const uint4*>(p)[1];
+    s.a = *reinterpret_cast<const uint4*>(p);
+    s.b = *reinterpret_cast<const uint4*>(p + SLOT_HALF);
   }
   return s;
-}
-__device__ __forceinline__ void st_slot(bf16_t* p, const uint32_t (&v)[8]) {
-  reinterpret_cast<uint4*>(p)[0] = make_uint4(v[0], v[1], v[2], v[3]);
-  reinterpret_cast<uint4*>(p)[1] = make_uint4(v[4], v[5], v[6], v[7]);
 }
 __device__ __forceinline__ void put4(uint32_t (&v)[4], int i, float x) {
   if (i & 1) v[i >> 1] |= ((uint32_t)f2bf(x) << 16);
@@ -308,7 +309,7 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
         put4(pk[0], i, ig); put4(pk[1], i, fg); put4(pk[2], i, gg); put4(pk[3], i, og); put4(pk[4], i, cn);
       }
       if (tape && rbok && uok && !(dbg & 1)) {
-        bf16_t* tp = tape + tape_base(rb, t, Tn, w) + lane * 16 + half * 8;
+        bf16_t* tp = tape + tape_base(rb, t, Tn, w) + lane * 8 + half * SLOT_HALF;
 #pragma unroll
         for (int s = 0; s < TAPE_SLOTS; ++s)
           *reinterpret_cast<uint4*>(tp + s * SLOT_ELEMS) = make_uint4(pk[s][0], pk[s][1], pk[s][2], pk[s][3]);
@@ -375,7 +376,7 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
   // primal tape of step 0 (gates + cell)
   Slot16 tg[TAPE_SLOTS];
   {
-    const bf16_t* tp = tape + tape_base(rbt, 0, Tn, w) + lane * 16;
+    const bf16_t* tp = tape + tape_base(rbt, 0, Tn, w) + lane * 8;
 #pragma unroll
     for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
   }
@@ -389,7 +390,7 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
     Slot16 tn[TAPE_SLOTS];
     if (t + 1 < Tn) {
       x_load<KX>(pf, xd, row0, B, Tn, t + 1, K, ltid);
-      const bf16_t* tp = tape + tape_base(rbt, t + 1, Tn, w) + lane * 16;
+      const bf16_t* tp = tape + tape_base(rbt, t + 1, Tn, w) + lane * 8;
 #pragma unroll
       for (int s = 0; s < TAPE_SLOTS; ++s) tn[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
     }
@@ -431,7 +432,7 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
         put4(pk[0], i, acc[0][r]); put4(pk[1], i, acc[1][r]); put4(pk[2], i, acc[2][r]); put4(pk[3], i, acc[3][r]);
         put4(pk[4], i, cdn);
       }
-      bf16_t* tp = ttape + tape_base(rb, t, Tn, w) + lane * 16 + half * 8;
+      bf16_t* tp = ttape + tape_base(rb, t, Tn, w) + lane * 8 + half * SLOT_HALF;
       if (rbok && uok) {
 #pragma unroll
         for (int s = 0; s < TAPE_SLOTS; ++s)
@@ -493,12 +494,12 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
   tile_from_hbm(dhb + ((Tn - 1) & 1) * 32 * LH, LH, dH, row0, B, Tn, Tn - 1, H, ltid);
   Slot16 tg[4], cc, cp;
   {
-    const bf16_t* tp = tape + tape_base(rbt, Tn - 1, Tn, w) + lane * 16;
+    const bf16_t* tp = tape + tape_base(rbt, Tn - 1, Tn, w) + lane * 8;
 #pragma unroll
     for (int s = 0; s < 4; ++s) tg[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
     cc = ld_slot(uok, tp + 4 * SLOT_ELEMS);
     cp.a = make_uint4(0, 0, 0, 0); cp.b = cp.a;
-    if (Tn > 1) cp = ld_slot(uok, tape + tape_base(rbt, Tn - 2, Tn, w) + lane * 16 + 4 * SLOT_ELEMS);
+    if (Tn > 1) cp = ld_slot(uok, tape + tape_base(rbt, Tn - 2, Tn, w) + lane * 8 + 4 * SLOT_ELEMS);
   }
   __syncthreads();
 
@@ -511,11 +512,11 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
     Slot16 ng[4], ncp;
     uint2 ndh[4];
     if (t > 0 && !(dbg & 2)) {
-      const bf16_t* tp = tape + tape_base(rbt, t - 1, Tn, w) + lane * 16;
+      const bf16_t* tp = tape + tape_base(rbt, t - 1, Tn, w) + lane * 8;
 #pragma unroll
       for (int s = 0; s < 4; ++s) ng[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
       ncp.a = make_uint4(0, 0, 0, 0); ncp.b = ncp.a;
-      if (t > 1) ncp = ld_slot(uok, tape + tape_base(rbt, t - 2, Tn, w) + lane * 16 + 4 * SLOT_ELEMS);
+      if (t > 1) ncp = ld_slot(uok, tape + tape_base(rbt, t - 2, Tn, w) + lane * 8 + 4 * SLOT_ELEMS);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int e = ltid + 256 * j;
@@ -638,7 +639,7 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
   tile_from_hbm(dhdb + ((Tn - 1) & 1) * 32 * LH, LH, dHd, row0, B, Tn, Tn - 1, H, ltid);
   Slot16 cc, cdc;  // c_t and cdot_t carried (loaded at the previous iteration as "prev")
   {
-    const size_t b = tape_base(rb, Tn - 1, Tn, w) + lane * 16 + 4 * SLOT_ELEMS;
+    const size_t b = tape_base(rb, Tn - 1, Tn, w) + lane * 8 + 4 * SLOT_ELEMS;
     cc = ld_slot(uok, tape + b);
     cdc = ld_slot(uok, ttape + b);
   }
@@ -658,13 +659,13 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
     // this step's tapes
     Slot16 tg[4], zd[4], cp, cdp;
     {
-      const bf16_t* tp = tape + tape_base(rb, t, Tn, w) + lane * 16;
-      const bf16_t* tq = ttape + tape_base(rb, t, Tn, w) + lane * 16;
+      const bf16_t* tp = tape + tape_base(rb, t, Tn, w) + lane * 8;
+      const bf16_t* tq = ttape + tape_base(rb, t, Tn, w) + lane * 8;
 #pragma unroll
       for (int s = 0; s < 4; ++s) { tg[s] = ld_slot(uok, tp + s * SLOT_ELEMS); zd[s] = ld_slot(uok, tq + s * SLOT_ELEMS); }
       cp.a = make_uint4(0, 0, 0, 0); cp.b = cp.a; cdp = cp;
       if (t > 0) {
-        const size_t b = tape_base(rb, t - 1, Tn, w) + lane * 16 + 4 * SLOT_ELEMS;
+        const size_t b = tape_base(rb, t - 1, Tn, w) + lane * 8 + 4 * SLOT_ELEMS;
         cp = ld_slot(uok, tape + b);
         cdp = ld_slot(uok, ttape + b);
       }
