@@ -255,16 +255,18 @@ static int check_dx_W(const optional<Tensor>& W, int H) {
   return (int)W->size(0);
 }
 
-std::tuple<Tensor, Tensor> lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int64_t act, optional<Tensor> W) {
+std::tuple<Tensor, Tensor> lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int64_t act, optional<Tensor> W,
+                                     bool need_dz) {
   CHECK_GPU(dH); CHECK_GPU(tape); same_dt(dH, tape);
   const int B = dH.size(0), Tn = dH.size(1), H = dH.size(2);
   check_lstm_U(U, H);
   TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstm2_tape_elems(B, Tn), "lstm2_bwd: tape size");
   const int K = check_dx_W(W, H);
   GUARD(dH);
-  Tensor dZ = at::empty({B, Tn, 4 * H}, dH.options());
+  TORCH_CHECK(need_dz || K, "lstm2_bwd: nothing to compute (need_dz=False without W)");
+  Tensor dZ = at::empty({need_dz ? B : 0, Tn, 4 * H}, dH.options());
   Tensor dX = at::empty({K ? B : 0, Tn, K}, dH.options());
-  hfrep::launch_lstm2_bwd(dH.data_ptr(), tape.data_ptr(), U.data_ptr<float>(), dZ.data_ptr(),
+  hfrep::launch_lstm2_bwd(dH.data_ptr(), tape.data_ptr(), U.data_ptr<float>(), need_dz ? dZ.data_ptr() : nullptr,
                           K ? W->data_ptr<float>() : nullptr, K ? dX.data_ptr() : nullptr, K, B, Tn, H, (int)act,
                           cur_stream(dH));
   return {dZ, dX};
@@ -461,7 +463,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstm_tfwd(Tensor dzx, Tensor gates, Tensor cs, Tensor U, int act) -> (Tensor, Tensor, Tensor)");
   m.def("lstm_tbwd(Tensor? dH, Tensor dHd, Tensor gates, Tensor cs, Tensor zds, Tensor cds, Tensor U, int act) -> (Tensor, Tensor)");
   m.def("lstm2_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
-  m.def("lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int act, Tensor? W=None) -> (Tensor, Tensor)");
+  m.def("lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int act, Tensor? W=None, bool need_dz=True) -> (Tensor, Tensor)");
   m.def("lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int act) -> (Tensor, Tensor)");
   m.def("lstm2_tbwd(Tensor? dH, Tensor dHd, Tensor tape, Tensor ttape, Tensor U, int act, Tensor? W=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps) -> (Tensor, Tensor, Tensor)");

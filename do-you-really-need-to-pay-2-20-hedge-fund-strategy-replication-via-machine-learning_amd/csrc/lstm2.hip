@@ -507,7 +507,8 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
     const bf16_t* zprev = zb + ((t + 1) & 1) * 32 * LG;  // dz_{t+1}
     bf16_t* zcur = zb + (t & 1) * 32 * LG;               // dz_t
     const bf16_t* dhcur = dhb + (t & 1) * 32 * LH;
-    if (t < Tn - 1 && !(dbg & 1)) tile16_to_hbm<G>(zprev, LG, dZ, row0, B, Tn, t + 1, ltid);
+    // dZ == nullptr: the caller needs only dX (gradient-penalty input gradient, generator step)
+    if (t < Tn - 1 && dZ && !(dbg & 1)) tile16_to_hbm<G>(zprev, LG, dZ, row0, B, Tn, t + 1, ltid);
     // prefetch the next (t-1) step: tape gates(t-1), cell(t-2), dH(t-1)
     Slot16 ng[4], ncp;
     uint2 ndh[4];
@@ -577,7 +578,7 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
     }
     if (!(dbg & 32)) lds_barrier();  // step hand-off: LDS only, stores stay in flight
   }
-  tile16_to_hbm<G>(zb, LG, dZ, row0, B, Tn, 0, ltid);
+  if (dZ) tile16_to_hbm<G>(zb, LG, dZ, row0, B, Tn, 0, ltid);
   if constexpr (DX) {
     if (xw) {
       f32x16 ax = zero16();

@@ -209,8 +209,8 @@ class LSTM(Layer):
     def ebwd(self, ctx, dy, need_dx, wgrad=True):
         U = self.p("recurrent_kernel")
         dx = None
-        if need_dx:  # dX = dZ W^T comes out of the BPTT launch itself
-            dZ, dx = Fn.lstm_layer_bwd(dy, ctx["tape"], U, self.act_code, W=self.p("kernel"))
+        if need_dx:  # dX = dZ W^T comes out of the BPTT launch itself; dZ is only kept for wgrad
+            dZ, dx = Fn.lstm_layer_bwd(dy, ctx["tape"], U, self.act_code, W=self.p("kernel"), need_dz=wgrad)
         else:
             dZ = Fn.lstm_layer_bwd(dy, ctx["tape"], U, self.act_code)
         if wgrad:

@@ -217,11 +217,15 @@ def lstm_layer_fwd(x, W, b, U, act: int, save: bool):
     return hs, ((gates, cs) if save else None)
 
 
-def lstm_layer_bwd(dH, tape, U, act: int, W=None):
+def lstm_layer_bwd(dH, tape, U, act: int, W=None, need_dz: bool = True):
     """dZ = dL/d(x W + b + h U) for every step; with ``W`` also the input gradient dX = dZ W^T,
-    returned as ``(dZ, dX)`` (the v2 kernel produces it in the same launch, csrc/lstm2.hip)."""
+    returned as ``(dZ, dX)`` (the v2 kernel produces it in the same launch, csrc/lstm2.hip).
+    ``need_dz=False`` (only dX wanted, e.g. the gradient penalty's dD/dx) lets the v2 kernel skip
+    writing dZ to HBM; the returned dZ is then None."""
     if isinstance(tape, torch.Tensor):
-        dZ, dX = _ops().lstm2_bwd(dH.contiguous(), tape, U, int(act), W)
+        dZ, dX = _ops().lstm2_bwd(dH.contiguous(), tape, U, int(act), W, bool(need_dz or W is None))
+        if W is not None and not need_dz:
+            dZ = None
         return dZ if W is None else (dZ, dX)
     gates, cs = tape
     dZ = lstm_seq_bwd(dH, gates, cs, U, act)

@@ -424,3 +424,20 @@ def test_conv_critic_trains_native(cuda):
         tr.train_step()
     rec = tr.losses()
     assert all(np.isfinite(v) for k, v in rec.items() if k != "iteration")
+
+
+def test_lstm2_bwd_dx_only(cuda):
+    """need_dz=False (gradient-penalty input gradient): same dX, no dZ written."""
+    from hfrep.ops import functional as Fn
+
+    B, T, K, H = 40, 12, 32, 100
+    g = torch.Generator().manual_seed(60)
+    x = (torch.randn(B, T, K, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    W = (torch.randn(K, 4 * H, generator=g) * K ** -0.5).to(cuda)
+    U = (torch.randn(H, 4 * H, generator=g) * H ** -0.5).to(cuda)
+    b = torch.zeros(4 * H, device=cuda)
+    _, tape = Fn.lstm_layer_fwd(x, W, b, U, 2, True)
+    dH = torch.randn(B, T, H, generator=g).to(torch.bfloat16).to(cuda)
+    dZ, dX = Fn.lstm_layer_bwd(dH, tape, U, 2, W=W)
+    dZ2, dX2 = Fn.lstm_layer_bwd(dH, tape, U, 2, W=W, need_dz=False)
+    assert dZ2 is None and torch.equal(dX, dX2)
