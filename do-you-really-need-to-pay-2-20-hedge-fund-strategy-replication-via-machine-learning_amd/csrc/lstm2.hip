@@ -215,7 +215,20 @@ __device__ __forceinline__ void store_dx(const f32x16& ax, bf16_t* __restrict__ 
 // ==========================================================================================
 // forward (+ optional tape):  z_t = x_t W + b + h_{t-1} U
 // ==========================================================================================
-template <int H, int ACT, int KX, int TILES>
+// diagnostic phase timers (HFREP_LSTM_DBG & 64 -> an ST=true instantiation of the forward
+// kernel): s_memtime deltas per phase summed per wave, read back by lstm2_read_stamps().  Only
+// the diagnostic build executes them; its absolute time is not a benchmark.
+__device__ unsigned long long g_lstm_stamps[4096 * 8];
+#define HFREP_STAMP(i)                                     \
+  if constexpr (ST) {                                      \
+    __builtin_amdgcn_sched_barrier(0);                     \
+    const uint64_t _t = __builtin_amdgcn_s_memtime();      \
+    __builtin_amdgcn_sched_barrier(0);                     \
+    st_acc[i] += _t - st_last;                             \
+    st_last = _t;                                          \
+  }
+
+template <int H, int ACT, int KX, int TILES, bool ST = false>
 __global__ void __launch_bounds__(256 * TILES)
 lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
                  const float* __restrict__ U, bf16_t* __restrict__ hs, bf16_t* __restrict__ tape, int B, int Tn,
@@ -254,6 +267,8 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
   float bq[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) bq[q] = (uok && bias) ? bias[q * H + u] : 0.f;
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+  if constexpr (ST) st_last = __builtin_amdgcn_s_memtime();
 
   for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
   const int rb = grp * TILES + tile, row0 = rb * 32;
@@ -272,8 +287,11 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
     const bf16_t* xcur = xb + (t & 1) * 32 * LX;
     const bf16_t* hcur = hb + (t & 1) * 32 * LH;
     bf16_t* hnext = hb + ((t + 1) & 1) * 32 * LH;
+    HFREP_STAMP(7)
     if (t > 0 && !(dbg & 2)) tile_to_hbm(hcur, LH, hs, row0, B, Tn, t - 1, H, ltid);
+    HFREP_STAMP(0)
     if (t + 1 < Tn && !(dbg & 4)) x_load<KX>(pf, x, row0, B, Tn, t + 1, K, ltid);
+    HFREP_STAMP(1)
     f32x16 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = zero16();
@@ -284,6 +302,7 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc[q] = P::mma(a, P::lda(Wt + (q * H + uc) * LX, kx, lane), acc[q]);
     }
+    HFREP_STAMP(2)
     const bf16_t* hrow = hcur + (lane & 31) * LH;
 #pragma unroll
     for (int ks = 0; ks < NKH; ++ks) {
@@ -292,6 +311,7 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
       for (int q = 0; q < 4; ++q) acc[q] = P::mma(a, ub[q][ks], acc[q]);
     }
     }
+    HFREP_STAMP(3)
 #pragma unroll
     for (int half = 0; half < 2; ++half) {  // two halves of 8 rows: 20 packing registers, not 40
       uint32_t pk[TAPE_SLOTS][4];
@@ -315,11 +335,21 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
           *reinterpret_cast<uint4*>(tp + s * SLOT_ELEMS) = make_uint4(pk[s][0], pk[s][1], pk[s][2], pk[s][3]);
       }
     }
+    HFREP_STAMP(4)
     if (t + 1 < Tn) x_store_lds<KX>(pf, xb + ((t + 1) & 1) * 32 * LX, K, LX, ltid);
+    HFREP_STAMP(5)
     if (!(dbg & 32)) lds_barrier();  // step hand-off: LDS only, stores stay in flight
+    HFREP_STAMP(6)
   }
   tile_to_hbm(hb + (Tn & 1) * 32 * LH, LH, hs, row0, B, Tn, Tn - 1, H, ltid);
   __syncthreads();  // LDS is re-initialised for the next row block
+  }
+  if constexpr (ST) {
+    if (lane == 0) {
+      const int slot = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+      if (slot < 4096)
+        for (int i = 0; i < 8; ++i) g_lstm_stamps[slot * 8 + i] = st_acc[i];
+    }
   }
 }
 
@@ -843,6 +873,11 @@ static int lstm_tiles() {
 void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float* U, void* hs, void* tape, int B, int Tn,
                       int K, int H, int act, hipStream_t s) {
   const bf16_t* xp = (const bf16_t*)x;
+  if (K == 100 && (lstm_dbg() & 64) && act == 2) {  // diagnostic phase-timer build
+    launch(lstm_fwd2_kernel<100, 2, 100, 2, true>, persistent_grid(B, 2), 512, fwd_smem(H, K, 2), s, xp, W, b, U,
+           (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg() & ~64);
+    return;
+  }
   if ((K == 32 || K == 100) && lstm_tiles() == 2 && fwd_smem(H, K, 2) <= LDS_MAX) {
     const int g = persistent_grid(B, 2);
     const size_t sm = fwd_smem(H, K, 2);
@@ -902,6 +937,11 @@ void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const 
     HFREP_BWD_LAUNCH(lstm_tbwd2_kernel, 1, false, persistent_grid(B, 1), 256, tbwd_smem(H), s, (const bf16_t*)dH,
                      (const bf16_t*)dHd, (const bf16_t*)tape, (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd,
                      (const float*)nullptr, (bf16_t*)nullptr, (bf16_t*)nullptr, B, Tn, 0)
+}
+
+void lstm2_read_stamps(uint64_t* out, int n) {
+  HFREP_CHECK_HIP(hipDeviceSynchronize());
+  HFREP_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstm_stamps), (size_t)n * sizeof(uint64_t)));
 }
 
 }  // namespace hfrep
