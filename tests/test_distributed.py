@@ -62,8 +62,8 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-def test_dp_gloo_matches_single_process():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_gloo_matches_single_process(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -96,6 +96,7 @@ def test_dp_gloo_matches_single_process():
         tr.generator_grads(noise)
     np.testing.assert_allclose(res[0]["critic"], tr.critic.flat.grad.numpy(), rtol=1e-10, atol=1e-13)
     np.testing.assert_allclose(res[0]["gen"], tr.generator.flat.grad.numpy(), rtol=1e-10, atol=1e-13)
-    np.testing.assert_array_equal(res[0]["critic"], res[1]["critic"])
-    # after DP training every rank holds identical parameters
-    np.testing.assert_array_equal(res[0]["params"], res[1]["params"])
+    for r in range(1, world):
+        np.testing.assert_array_equal(res[0]["critic"], res[r]["critic"])
+        # after DP training every rank holds identical parameters
+        np.testing.assert_array_equal(res[0]["params"], res[r]["params"])
