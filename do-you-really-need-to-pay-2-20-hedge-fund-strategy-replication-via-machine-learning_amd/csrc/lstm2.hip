@@ -39,6 +39,45 @@ constexpr int SLOT_HALF = 64 * 8;
 __device__ __forceinline__ size_t tape_base(int rb, int t, int Tn, int w) {
   return (((size_t)rb * Tn + t) * NW2 + w) * TAPE_SLOTS * SLOT_ELEMS;
 }
+// element offset of (t, wave w) inside one row block's tape region
+__device__ __forceinline__ int tape_off(int t, int w) { return (t * NW2 + w) * TAPE_SLOTS * SLOT_ELEMS; }
+
+// ---------------------------------------------------------------------------------------------
+// Buffer descriptors.  Every global access of the step loops goes through a buffer resource
+// (SRD) that covers one 32-row tile (or one row block's tape region) and nothing else: rows past
+// B, padded unit lanes, idle trailing tiles and the out-of-range neighbours of the first / last
+// step get an offset beyond num_records, so the hardware range check turns their loads into
+// zeros and drops their stores.  Each thread therefore issues the SAME memory instructions in
+// every step, without exec-masked branches, and that matters on CDNA4: vmcnt retires loads and
+// stores together in issue order, and a wait the compiler computes across a branch that may skip
+// some stores must assume the shortest path, i.e. wait for stores it never needed (the waits in
+// the v2 step loops were vmcnt(0) behind the step's own tile stores; profiles/r01_vmcnt).
+// The range check looks at voffset only (soffset is added to the base address unchecked): the row
+// of an access always lives in voffset, and soffset carries only step / wave / slot offsets that
+// are in range whenever the voffset part is.  Per-lane parts in voffset, uniform parts in soffset
+// also keeps the loop-invariant address registers to one or two per access group.
+// ---------------------------------------------------------------------------------------------
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int kOOB = 0x7fff0000;  // byte offset past every descriptor's num_records
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+// rows [row0, min(row0 + 32, B)) of a row-major (B, Tn, W) bf16 tensor; a null base or a tile
+// past B gets zero records
+__device__ __forceinline__ rsrc_t tile_rsrc(const bf16_t* base, int row0, int B, int Tn, int W) {
+  row0 = __builtin_amdgcn_readfirstlane(row0);
+  const int nr = base ? max(0, min(32, B - row0)) : 0;
+  return make_rsrc(base + (nr ? (size_t)row0 * Tn * W : 0), nr * Tn * W * 2);
+}
+// one row block's tape region ([t][wave][slot][half][lane][8])
+__device__ __forceinline__ rsrc_t tape_rsrc(const bf16_t* tape, int rb, int nrb, int Tn) {
+  rb = __builtin_amdgcn_readfirstlane(rb);
+  const bool on = tape && rb < nrb;
+  return make_rsrc(tape + (on ? tape_base(rb, 0, Tn, 0) : 0), on ? Tn * NW2 * TAPE_SLOTS * SLOT_ELEMS * 2 : 0);
+}
 
 __device__ __forceinline__ uint32_t pk2(float lo, float hi) { return pk2bf(lo, hi); }
 __device__ __forceinline__ float lo_bf(uint32_t v) { return __uint_as_float(v << 16); }
@@ -52,17 +91,22 @@ struct Slot16 {  // 16 bf16 values of one lane, packed
     return (r & 1) ? hi_bf(w) : lo_bf(w);
   }
 };
-// lanes whose unit is padding (u >= H: 28 of 128 tape columns) neither load nor store: the tape's
-// padded slots are never touched, which trims 22% of the tape traffic
-__device__ __forceinline__ Slot16 ld_slot(bool on, const bf16_t* p) {
+// lanes whose unit is padding (u >= H: 28 of 128 tape columns) neither load nor store (their
+// offsets are out of range): the tape's padded slots are never touched, which trims 22% of the
+// tape traffic.  `off` is this lane's element offset of the slot's first half.
+__device__ __forceinline__ Slot16 ld_slot(rsrc_t rs, bool on, int lane_off, int uoff) {
   Slot16 s;
-  s.a = make_uint4(0, 0, 0, 0);
-  s.b = s.a;
-  if (on) {
-    s.a = *reinterpret_cast<const uint4*>(p);
-    s.b = *reinterpret_cast<const uint4*>(p + SLOT_HALF);
-  }
+  const int v = on ? lane_off * 2 : kOOB;
+  s.a = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, v, uoff * 2, 0));
+  s.b = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, v, (uoff + SLOT_HALF) * 2, 0));
   return s;
+}
+// 16-byte STORES keep soffset = 0: a buffer store of more than 8 bytes whose data VGPRs a VALU
+// instruction overwrites right after it needs one wait state, and the compiler's hazard model
+// omits it when soffset is a register (measured on gfx950: the 4th tape slot came back corrupt)
+__device__ __forceinline__ void st_slot(rsrc_t rs, bool on, int lane_off, int uoff, const uint32_t (&v)[4]) {
+  const v4i d = {(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
+  __builtin_amdgcn_raw_buffer_store_b128(d, rs, on ? (lane_off + uoff) * 2 : kOOB, 0, 0);
 }
 __device__ __forceinline__ void put4(uint32_t (&v)[4], int i, float x) {
   if (i & 1) v[i >> 1] |= ((uint32_t)f2bf(x) << 16);
@@ -91,9 +135,10 @@ struct XGeo {
 struct XPref {
   uint2 v[4];
 };
+// x tile of step t through the tile descriptor `rx` (rows past B read 0); `on` == false (a step
+// outside [0, Tn)) issues the same loads out of range
 template <int KX>
-__device__ __forceinline__ void x_load(XPref& p, const bf16_t* __restrict__ x, int row0, int B, int Tn, int t, int K,
-                                       int ltid) {
+__device__ __forceinline__ void x_load(XPref& p, rsrc_t rx, int Tn, int t, bool on, int K, int ltid) {
   if constexpr (!XGeo<KX>::VEC) {
     if constexpr (KX > 0) K = KX;
     uint32_t* pv = reinterpret_cast<uint32_t*>(p.v);
@@ -101,8 +146,8 @@ __device__ __forceinline__ void x_load(XPref& p, const bf16_t* __restrict__ x, i
     for (int j = 0; j < 16; ++j) {
       const int e = ltid + 256 * j;
       const int r = e / K, k = e - r * K;
-      const int row = row0 + r;
-      const uint32_t v = (r < 32 && row < B) ? (uint32_t)x[((size_t)row * Tn + t) * K + k] : 0u;
+      const int off = (on && r < 32) ? (r * Tn * K + k) * 2 : kOOB;  // step t in soffset
+      const uint32_t v = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rx, off, t * K * 2, 0);
       if (j & 1) pv[j >> 1] |= v << 16;
       else pv[j >> 1] = v;
     }
@@ -112,9 +157,8 @@ __device__ __forceinline__ void x_load(XPref& p, const bf16_t* __restrict__ x, i
     for (int j = 0; j < XGeo<KX>::XJ; ++j) {
       const int e = ltid + 256 * j;
       const int r = e / K4, c = e - r * K4;
-      const int row = row0 + r;
-      p.v[j] = (r < 32 && row < B) ? *reinterpret_cast<const uint2*>(x + ((size_t)row * Tn + t) * KX + 4 * c)
-                                   : make_uint2(0, 0);
+      const int off = (on && r < 32) ? (r * Tn * KX + 4 * c) * 2 : kOOB;  // step t in soffset
+      p.v[j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rx, off, t * KX * 2, 0));
     }
   }
 }
@@ -140,50 +184,65 @@ __device__ __forceinline__ void x_store_lds(const XPref& p, bf16_t* xb, int K, i
   }
 }
 
-// [32 x W] bf16 tile in LDS (row stride LD) -> HBM (B,T,W) in 16-byte chunks; W % 8 == 0 and
-// LD % 8 == 0 (16-byte aligned rows on both sides).  16 threads per row, two rows per pass of the
-// tile's 256 threads: each thread walks one row with pointer increments (no per-chunk division),
-// and 16 consecutive threads write 256 contiguous bytes of a row.
+// [32 x W] bf16 tile in LDS (row stride LD) -> step t of the tile descriptor `rd` in 16-byte
+// chunks; W % 8 == 0 and LD % 8 == 0.  16 threads per row, two rows per pass of the tile's 256
+// threads, 16 consecutive threads write 256 contiguous bytes of a row.  Every thread issues
+// 2 * ceil(W / 128) stores; chunks past the row end (and `on` == false) go out of range.
 template <int W>
-__device__ __forceinline__ void tile16_to_hbm(const bf16_t* buf, int LD, bf16_t* __restrict__ dst, int row0, int B,
-                                              int Tn, int t, int ltid) {
+__device__ __forceinline__ void tile16_store(const bf16_t* buf, int LD, rsrc_t rd, int Tn, int t, bool on, int ltid) {
   static_assert(W % 8 == 0, "16-byte chunks");
-  constexpr int CPR = W / 8;
+  constexpr int CPR = W / 8, NK = (CPR + 15) / 16;
   const int c0 = ltid & 15;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
-    const int r = (ltid >> 4) + 16 * pass, row = row0 + r;
-    if (row >= B) continue;
-    const bf16_t* s = buf + r * LD + 8 * c0;
-    bf16_t* d = dst + ((size_t)row * Tn + t) * W + 8 * c0;
+    const int r = (ltid >> 4) + 16 * pass;
+    const int row_off = (r * Tn * W + 8 * c0) * 2;  // row in voffset (range-checked), step + chunk uniform
 #pragma unroll
-    for (int c = c0; c < CPR; c += 16, s += 128, d += 128)
-      *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+    for (int k = 0; k < NK; ++k) {
+      const int c = c0 + 16 * k;
+      const bool ok = c < CPR;
+      const v4i v = *reinterpret_cast<const v4i*>(buf + r * LD + 8 * (ok ? c : CPR - 1));
+      // (16-byte store: soffset 0, see st_slot)
+      __builtin_amdgcn_raw_buffer_store_b128(v, rd, (on && ok) ? row_off + (t * W + 128 * k) * 2 : kOOB, 0, 0);
+    }
   }
 }
 
-// row-major [32 x width] tile <-> HBM (B,T,width) with 8-byte chunks (width % 4 == 0), moved by the
-// 256 threads of one row tile (ltid = thread index within the tile)
-__device__ __forceinline__ void tile_to_hbm(const bf16_t* buf, int LD, bf16_t* __restrict__ dst, int row0, int B, int Tn,
-                                            int t, int width, int ltid) {
-  const int cpr = width / 4;
-  for (int e = ltid; e < 32 * cpr; e += 256) {
-    const int r = e / cpr, c = e - r * cpr;
-    const int row = row0 + r;
-    if (row < B)
-      *reinterpret_cast<uint2*>(dst + ((size_t)row * Tn + t) * width + 4 * c) =
-          *reinterpret_cast<const uint2*>(buf + r * LD + 4 * c);
+// row-major [32 x W] tile <-> step t of a tile descriptor in 8-byte chunks (W % 4 == 0), moved by
+// the 256 threads of one row tile (ltid = thread index within the tile); a fixed NJ chunks per
+// thread, the ones past the tile out of range
+template <int W>
+struct Tile8 {
+  static constexpr int CPR = W / 4, NJ = (32 * CPR + 255) / 256;
+  static_assert(W % 4 == 0, "8-byte chunks");
+  v2i v[NJ];
+  __device__ __forceinline__ void load(rsrc_t rs, int Tn, int t, bool on, int ltid) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int e = ltid + 256 * j;
+      const int r = e / CPR, c = e - r * CPR;
+      v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, (on && r < 32) ? (r * Tn * W + 4 * c) * 2 : kOOB, t * W * 2, 0);
+    }
   }
-}
-__device__ __forceinline__ void tile_from_hbm(bf16_t* buf, int LD, const bf16_t* __restrict__ src, int row0, int B,
-                                              int Tn, int t, int width, int ltid) {
-  const int cpr = width / 4;
-  for (int e = ltid; e < 32 * cpr; e += 256) {
-    const int r = e / cpr, c = e - r * cpr;
-    const int row = row0 + r;
-    uint2 v = make_uint2(0, 0);
-    if (row < B) v = *reinterpret_cast<const uint2*>(src + ((size_t)row * Tn + t) * width + 4 * c);
-    *reinterpret_cast<uint2*>(buf + r * LD + 4 * c) = v;
+  __device__ __forceinline__ void to_lds(bf16_t* buf, int LD, int ltid) const {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int e = ltid + 256 * j;
+      const int r = e / CPR, c = e - r * CPR;
+      if (r < 32) *reinterpret_cast<v2i*>(buf + r * LD + 4 * c) = v[j];
+    }
+  }
+};
+template <int W>
+__device__ __forceinline__ void tile8_store(const bf16_t* buf, int LD, rsrc_t rd, int Tn, int t, bool on, int ltid) {
+  constexpr int CPR = W / 4, NJ = (32 * CPR + 255) / 256;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int e = ltid + 256 * j;
+    const int r = e / CPR, c = e - r * CPR;
+    const bool ok = r < 32;
+    const v2i v = *reinterpret_cast<const v2i*>(buf + (ok ? r : 31) * LD + 4 * c);
+    __builtin_amdgcn_raw_buffer_store_b64(v, rd, (on && ok) ? (r * Tn * W + 4 * c) * 2 : kOOB, t * W * 2, 0);
   }
 }
 
@@ -200,14 +259,17 @@ __device__ __forceinline__ void make_wt(typename MF<bf16_t>::frag (&wt)[NKG], co
       return (kc < K && n < G) ? v : 0.f;
     }, ks, lane);
 }
-__device__ __forceinline__ void store_dx(const f32x16& ax, bf16_t* __restrict__ dX, int row0, int B, int Tn, int t,
-                                         int K, int kc, int lane) {
-  if (kc >= K) return;
+// 16 two-byte stores per lane, always issued (rows >= nr, columns >= K and `on` == false out of
+// range).  The range check covers voffset only (soffset is added to the base), so each row's
+// validity is decided in voffset: lane part of the row + column there, register-dependent row
+// part + step in soffset.
+__device__ __forceinline__ void store_dx(const f32x16& ax, rsrc_t rd, int Tn, int t, bool on, int nr, int K, int kc,
+                                         int lane) {
+  const int off = (on && kc < K) ? (4 * (lane >> 5) * Tn * K + kc) * 2 : kOOB;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = row0 + acc32_row(r, lane);
-    if (row < B) dX[((size_t)row * Tn + t) * K + kc] = f2bf(ax[r]);
-  }
+  for (int r = 0; r < 16; ++r)
+    __builtin_amdgcn_raw_buffer_store_b16(f2bf(ax[r]), rd, acc32_row(r, lane) < nr ? off : kOOB,
+                                          (((r & 3) + 8 * (r >> 2)) * Tn * K + t * K) * 2, 0);
 }
 
 }  // namespace
@@ -245,6 +307,7 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
   bf16_t* xb = Wt + G * LX + tile * (2 * 32 * LX + 2 * 32 * LH);
   bf16_t* hb = xb + 2 * 32 * LX;
   const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) & 3;
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index as a scalar (uniform offsets)
   const int u = w * 32 + (lane & 31);
   const bool uok = u < H;
   const int uc = uok ? u : H - 1;
@@ -270,16 +333,18 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
   uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
   if constexpr (ST) st_last = __builtin_amdgcn_s_memtime();
 
+  (void)dbg;
   for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
-  const int rb = grp * TILES + tile, row0 = rb * 32;
-  const bool rbok = rb < nrb;  // a trailing tile past B only joins the barriers
+  const int rb = grp * TILES + tile, row0 = rb * 32;  // a trailing tile past B only joins the barriers
+  const rsrc_t rx = tile_rsrc(x, row0, B, Tn, K), rh = tile_rsrc(hs, row0, B, Tn, H);
+  const rsrc_t rt = tape_rsrc(tape, rb, nrb, Tn);  // zero records: no tape / idle tile
   for (int i = ltid; i < 2 * 32 * LH; i += 256) hb[i] = 0;
   float c[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) c[r] = 0.f;
   XPref pf;
   __syncthreads();
-  x_load<KX>(pf, x, row0, B, Tn, 0, K, ltid);
+  x_load<KX>(pf, rx, Tn, 0, true, K, ltid);
   x_store_lds<KX>(pf, xb, K, LX, ltid);
   __syncthreads();
 
@@ -288,15 +353,15 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
     const bf16_t* hcur = hb + (t & 1) * 32 * LH;
     bf16_t* hnext = hb + ((t + 1) & 1) * 32 * LH;
     HFREP_STAMP(7)
-    if (t > 0 && !(dbg & 2)) tile_to_hbm(hcur, LH, hs, row0, B, Tn, t - 1, H, ltid);
+    // loads before stores: the x wait at the end of the step then covers only older traffic
+    x_load<KX>(pf, rx, Tn, t + 1, t + 1 < Tn, K, ltid);
     HFREP_STAMP(0)
-    if (t + 1 < Tn && !(dbg & 4)) x_load<KX>(pf, x, row0, B, Tn, t + 1, K, ltid);
+    tile8_store<H>(hcur, LH, rh, Tn, t - 1, t > 0, ltid);
     HFREP_STAMP(1)
     f32x16 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = zero16();
     const bf16_t* xrow = xcur + (lane & 31) * LX;
-    if (!(dbg & 8)) {
     for (int kx = 0; kx < NKX; ++kx) {
       const typename P::frag a = P::lda(xrow, kx, lane);
 #pragma unroll
@@ -309,7 +374,6 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
       const typename P::frag a = P::lda(hrow, ks, lane);
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc[q] = P::mma(a, ub[q][ks], acc[q]);
-    }
     }
     HFREP_STAMP(3)
 #pragma unroll
@@ -325,23 +389,20 @@ lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
         float h = og * act_f(act, cn);
         if (!uok) { cn = 0.f; h = 0.f; }
         c[r] = cn;
-        if (u < KPADH && !(dbg & 16)) hnext[rr * LH + u] = f2bf(h);
+        if (u < KPADH) hnext[rr * LH + u] = f2bf(h);
         put4(pk[0], i, ig); put4(pk[1], i, fg); put4(pk[2], i, gg); put4(pk[3], i, og); put4(pk[4], i, cn);
       }
-      if (tape && rbok && uok && !(dbg & 1)) {
-        bf16_t* tp = tape + tape_base(rb, t, Tn, w) + lane * 8 + half * SLOT_HALF;
+      const int to = tape_off(t, wu) + half * SLOT_HALF;
 #pragma unroll
-        for (int s = 0; s < TAPE_SLOTS; ++s)
-          *reinterpret_cast<uint4*>(tp + s * SLOT_ELEMS) = make_uint4(pk[s][0], pk[s][1], pk[s][2], pk[s][3]);
-      }
+      for (int s = 0; s < TAPE_SLOTS; ++s) st_slot(rt, uok, lane * 8, to + s * SLOT_ELEMS, pk[s]);
     }
     HFREP_STAMP(4)
     if (t + 1 < Tn) x_store_lds<KX>(pf, xb + ((t + 1) & 1) * 32 * LX, K, LX, ltid);
     HFREP_STAMP(5)
-    if (!(dbg & 32)) lds_barrier();  // step hand-off: LDS only, stores stay in flight
+    lds_barrier();  // step hand-off: LDS only, stores stay in flight
     HFREP_STAMP(6)
   }
-  tile_to_hbm(hb + (Tn & 1) * 32 * LH, LH, hs, row0, B, Tn, Tn - 1, H, ltid);
+  tile8_store<H>(hb + (Tn & 1) * 32 * LH, LH, rh, Tn, Tn - 1, true, ltid);
   __syncthreads();  // LDS is re-initialised for the next row block
   }
   if constexpr (ST) {
@@ -372,6 +433,7 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
   bf16_t* xb = Wt + G * LX + tile * (2 * 32 * LX + 2 * 32 * LH);
   bf16_t* hb = xb + 2 * 32 * LX;
   const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) & 3;
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index as a scalar (uniform offsets)
   const int u = w * 32 + (lane & 31);
   const bool uok = u < H;
   const int uc = uok ? u : H - 1;
@@ -393,37 +455,33 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
 
   for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
   const int rb = grp * TILES + tile, row0 = rb * 32;
-  const bool rbok = rb < nrb;
-  const int rbt = rbok ? rb : nrb - 1;  // tape reads of an idle trailing tile stay in bounds
+  const rsrc_t rx = tile_rsrc(xd, row0, B, Tn, K), rh = tile_rsrc(hds, row0, B, Tn, H);
+  const rsrc_t rt = tape_rsrc(tape, rb, nrb, Tn), rtt = tape_rsrc(ttape, rb, nrb, Tn);  // idle tile: 0 records
   for (int i = ltid; i < 2 * 32 * LH; i += 256) hb[i] = 0;
   float cd[16], cprev[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) { cd[r] = 0.f; cprev[r] = 0.f; }
   XPref pf;
   __syncthreads();
-  x_load<KX>(pf, xd, row0, B, Tn, 0, K, ltid);
+  x_load<KX>(pf, rx, Tn, 0, true, K, ltid);
   x_store_lds<KX>(pf, xb, K, LX, ltid);
   // primal tape of step 0 (gates + cell)
   Slot16 tg[TAPE_SLOTS];
-  {
-    const bf16_t* tp = tape + tape_base(rbt, 0, Tn, w) + lane * 8;
 #pragma unroll
-    for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
-  }
+  for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = ld_slot(rt, uok, lane * 8, tape_off(0, wu) + s * SLOT_ELEMS);
   __syncthreads();
 
   for (int t = 0; t < Tn; ++t) {
     const bf16_t* xcur = xb + (t & 1) * 32 * LX;
     const bf16_t* hcur = hb + (t & 1) * 32 * LH;
     bf16_t* hnext = hb + ((t + 1) & 1) * 32 * LH;
-    if (t > 0) tile_to_hbm(hcur, LH, hds, row0, B, Tn, t - 1, H, ltid);
+    // next step's x tile and primal tape first, then this tile's pending h stores
+    const bool nx = t + 1 < Tn;
+    x_load<KX>(pf, rx, Tn, t + 1, nx, K, ltid);
     Slot16 tn[TAPE_SLOTS];
-    if (t + 1 < Tn) {
-      x_load<KX>(pf, xd, row0, B, Tn, t + 1, K, ltid);
-      const bf16_t* tp = tape + tape_base(rbt, t + 1, Tn, w) + lane * 8;
 #pragma unroll
-      for (int s = 0; s < TAPE_SLOTS; ++s) tn[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
-    }
+    for (int s = 0; s < TAPE_SLOTS; ++s) tn[s] = ld_slot(rt, uok && nx, lane * 8, tape_off(t + 1, wu) + s * SLOT_ELEMS);
+    tile8_store<H>(hcur, LH, rh, Tn, t - 1, t > 0, ltid);
     f32x16 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = zero16();
@@ -462,21 +520,16 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
         put4(pk[0], i, acc[0][r]); put4(pk[1], i, acc[1][r]); put4(pk[2], i, acc[2][r]); put4(pk[3], i, acc[3][r]);
         put4(pk[4], i, cdn);
       }
-      bf16_t* tp = ttape + tape_base(rb, t, Tn, w) + lane * 8 + half * SLOT_HALF;
-      if (rbok && uok) {
+      const int to = tape_off(t, wu) + half * SLOT_HALF;
 #pragma unroll
-        for (int s = 0; s < TAPE_SLOTS; ++s)
-          *reinterpret_cast<uint4*>(tp + s * SLOT_ELEMS) = make_uint4(pk[s][0], pk[s][1], pk[s][2], pk[s][3]);
-      }
+      for (int s = 0; s < TAPE_SLOTS; ++s) st_slot(rtt, uok, lane * 8, to + s * SLOT_ELEMS, pk[s]);
     }
-    if (t + 1 < Tn) {
-      x_store_lds<KX>(pf, xb + ((t + 1) & 1) * 32 * LX, K, LX, ltid);
+    if (nx) x_store_lds<KX>(pf, xb + ((t + 1) & 1) * 32 * LX, K, LX, ltid);
 #pragma unroll
-      for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = tn[s];
-    }
+    for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = tn[s];
     lds_barrier();  // step hand-off: LDS only, stores stay in flight
   }
-  tile_to_hbm(hb + (Tn & 1) * 32 * LH, LH, hds, row0, B, Tn, Tn - 1, H, ltid);
+  tile8_store<H>(hb + (Tn & 1) * 32 * LH, LH, rh, Tn, Tn - 1, true, ltid);
   __syncthreads();
   }
 }
@@ -497,6 +550,7 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
   bf16_t* zb = reinterpret_cast<bf16_t*>(smem) + tile * (2 * 32 * LG + 2 * 32 * LH);  // [2][32][LG]
   bf16_t* dhb = zb + 2 * 32 * LG;                                                     // [2][32][LH]
   const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) & 3;
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index as a scalar (uniform offsets)
   const int u = w * 32 + (lane & 31);
   const bool uok = u < H;
   const int nrb = (B + 31) / 32, ngrp = (nrb + TILES - 1) / TILES;
@@ -514,66 +568,61 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
   if constexpr (DX) make_wt<NKG>(wt, W, K, G, kc, lane);
   for (int i = ltid; i < 2 * 32 * LG; i += 256) zb[i] = 0;
 
+  (void)dbg;
+  const int lo = lane * 8;
   for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
   const int rb = grp * TILES + tile, row0 = rb * 32;
-  const int rbt = rb < nrb ? rb : nrb - 1;  // tape reads of an idle trailing tile stay in bounds
+  const int nr = min(32, B - row0);  // valid rows of this tile
+  const rsrc_t rdh = tile_rsrc(dH, row0, B, Tn, H), rz = tile_rsrc(dZ, row0, B, Tn, G);
+  const rsrc_t rdx = tile_rsrc(DX ? dX : nullptr, row0, B, Tn, DX ? K : 1), rt = tape_rsrc(tape, rb, nrb, Tn);
   float dc[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) dc[r] = 0.f;
   __syncthreads();
-  tile_from_hbm(dhb + ((Tn - 1) & 1) * 32 * LH, LH, dH, row0, B, Tn, Tn - 1, H, ltid);
-  Slot16 tg[4], cc, cp;
   {
-    const bf16_t* tp = tape + tape_base(rbt, Tn - 1, Tn, w) + lane * 8;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) tg[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
-    cc = ld_slot(uok, tp + 4 * SLOT_ELEMS);
-    cp.a = make_uint4(0, 0, 0, 0); cp.b = cp.a;
-    if (Tn > 1) cp = ld_slot(uok, tape + tape_base(rbt, Tn - 2, Tn, w) + lane * 8 + 4 * SLOT_ELEMS);
+    Tile8<H> d0;
+    d0.load(rdh, Tn, Tn - 1, true, ltid);
+    d0.to_lds(dhb + ((Tn - 1) & 1) * 32 * LH, LH, ltid);
   }
+  Slot16 tg[4], cc, cp;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) tg[s] = ld_slot(rt, uok, lo, tape_off(Tn - 1, wu) + s * SLOT_ELEMS);
+  cc = ld_slot(rt, uok, lo, tape_off(Tn - 1, wu) + 4 * SLOT_ELEMS);
+  cp = ld_slot(rt, uok && Tn > 1, lo, tape_off(max(Tn - 2, 0), wu) + 4 * SLOT_ELEMS);
   __syncthreads();
 
   for (int t = Tn - 1; t >= 0; --t) {
     const bf16_t* zprev = zb + ((t + 1) & 1) * 32 * LG;  // dz_{t+1}
     bf16_t* zcur = zb + (t & 1) * 32 * LG;               // dz_t
     const bf16_t* dhcur = dhb + (t & 1) * 32 * LH;
-    // dZ == nullptr: the caller needs only dX (gradient-penalty input gradient, generator step)
-    if (t < Tn - 1 && dZ && !(dbg & 1)) tile16_to_hbm<G>(zprev, LG, dZ, row0, B, Tn, t + 1, ltid);
-    // prefetch the next (t-1) step: tape gates(t-1), cell(t-2), dH(t-1)
+    // prefetch step t-1 (tape gates(t-1), cell(t-2), dH(t-1)) BEFORE this step's stores, so that
+    // its wait at the end of the step does not cover them
+    const bool pv = t > 0;
     Slot16 ng[4], ncp;
-    uint2 ndh[4];
-    if (t > 0 && !(dbg & 2)) {
-      const bf16_t* tp = tape + tape_base(rbt, t - 1, Tn, w) + lane * 8;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) ng[s] = ld_slot(uok, tp + s * SLOT_ELEMS);
-      ncp.a = make_uint4(0, 0, 0, 0); ncp.b = ncp.a;
-      if (t > 1) ncp = ld_slot(uok, tape + tape_base(rbt, t - 2, Tn, w) + lane * 8 + 4 * SLOT_ELEMS);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int e = ltid + 256 * j;
-        const int r = e / (H / 4), c4 = e - r * (H / 4);
-        const int row = row0 + r;
-        ndh[j] = make_uint2(0, 0);
-        if (r < 32 && row < B) ndh[j] = *reinterpret_cast<const uint2*>(dH + ((size_t)row * Tn + (t - 1)) * H + 4 * c4);
-      }
-    }
-    f32x16 acc = zero16();
-    if (t < Tn - 1 && !(dbg & 4)) {
+    for (int s = 0; s < 4; ++s) ng[s] = ld_slot(rt, uok && pv, lo, tape_off(max(t - 1, 0), wu) + s * SLOT_ELEMS);
+    ncp = ld_slot(rt, uok && t > 1, lo, tape_off(max(t - 2, 0), wu) + 4 * SLOT_ELEMS);
+    Tile8<H> ndh;
+    ndh.load(rdh, Tn, t - 1, pv, ltid);
+    // dZ == nullptr (zero records): the caller needs only dX (gradient-penalty input gradient,
+    // generator step) and the stores are dropped
+    tile16_store<G>(zprev, LG, rz, Tn, t + 1, t < Tn - 1, ltid);
+    f32x16 acc = zero16(), ax = zero16();
+    if (t < Tn - 1) {
       const bf16_t* arow = zprev + (lane & 31) * LG;
       if (xw) {
-        f32x16 ax = zero16();
 #pragma unroll
         for (int ks = 0; ks < NKG; ++ks) {
           const typename P::frag a = P::lda(arow, ks, lane);
           acc = P::mma(a, ut[ks], acc);
           if constexpr (DX) ax = P::mma(a, wt[ks], ax);
         }
-        store_dx(ax, dX, row0, B, Tn, t + 1, K, kc, lane);
       } else {
 #pragma unroll
         for (int ks = 0; ks < NKG; ++ks) acc = P::mma(P::lda(arow, ks, lane), ut[ks], acc);
       }
     }
+    if constexpr (DX) store_dx(ax, rdx, Tn, t + 1, xw && t < Tn - 1, nr, K, kc, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rr = acc32_row(r, lane);
@@ -588,35 +637,29 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
       float z1 = dct * cpv * fg * (1.f - fg);
       float z2 = dct * ig * act_dy(act, gg);
       float z3 = dov * og * (1.f - og);
-      if (uok && !(dbg & 8)) {
+      if (uok) {
         bf16_t* zr = zcur + rr * LG + u;
         zr[0] = f2bf(z0); zr[H] = f2bf(z1); zr[2 * H] = f2bf(z2); zr[3 * H] = f2bf(z3);
       }
     }
-    if (t > 0 && !(dbg & 2)) {
-      bf16_t* dnext = dhb + ((t - 1) & 1) * 32 * LH;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int e = ltid + 256 * j;
-        const int r = e / (H / 4), c4 = e - r * (H / 4);
-        if (r < 32) *reinterpret_cast<uint2*>(dnext + r * LH + 4 * c4) = ndh[j];
-      }
+    if (pv) {
+      ndh.to_lds(dhb + ((t - 1) & 1) * 32 * LH, LH, ltid);
 #pragma unroll
       for (int s = 0; s < 4; ++s) tg[s] = ng[s];
       cc = cp;
       cp = ncp;
     }
-    if (!(dbg & 32)) lds_barrier();  // step hand-off: LDS only, stores stay in flight
+    lds_barrier();  // step hand-off: LDS only, stores stay in flight
   }
-  if (dZ) tile16_to_hbm<G>(zb, LG, dZ, row0, B, Tn, 0, ltid);
+  tile16_store<G>(zb, LG, rz, Tn, 0, true, ltid);
   if constexpr (DX) {
+    f32x16 ax = zero16();
     if (xw) {
-      f32x16 ax = zero16();
       const bf16_t* arow = zb + (lane & 31) * LG;
 #pragma unroll
       for (int ks = 0; ks < NKG; ++ks) ax = P::mma(P::lda(arow, ks, lane), wt[ks], ax);
-      store_dx(ax, dX, row0, B, Tn, 0, K, kc, lane);
     }
+    store_dx(ax, rdx, Tn, 0, xw, nr, K, kc, lane);
   }
   __syncthreads();
   }
@@ -642,6 +685,7 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
   bf16_t* dhb = zdb + 2 * 32 * LG;                // [2][32][LH]  (dH)
   bf16_t* dhdb = dhb + 2 * 32 * LH;               // [2][32][LH]  (dHdot)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index as a scalar (uniform offsets)
   const int u = w * 32 + (lane & 31);
   const bool uok = u < H;
   const int nrb = (B + 31) / 32;
@@ -660,53 +704,58 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
   for (int i = threadIdx.x; i < 2 * 32 * LG; i += 256) { zb[i] = 0; zdb[i] = 0; }
   for (int i = threadIdx.x; i < 2 * 32 * LH; i += 256) dhb[i] = 0;
 
+  const int lo = lane * 8;
   for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
   const int row0 = rb * 32;
+  const int nr = min(32, B - row0);  // valid rows of this tile
+  // dH == nullptr (no primal output seed): zero records, the tile loads read zeros
+  const rsrc_t rdh = tile_rsrc(dH, row0, B, Tn, H), rdhd = tile_rsrc(dHd, row0, B, Tn, H);
+  const rsrc_t rz = tile_rsrc(dZ, row0, B, Tn, G), rzd = tile_rsrc(dZd, row0, B, Tn, G);
+  const rsrc_t rdx = tile_rsrc(DX ? dX : nullptr, row0, B, Tn, DX ? K : 1);
+  const rsrc_t rdxd = tile_rsrc(DX ? dXd : nullptr, row0, B, Tn, DX ? K : 1);
+  const rsrc_t rt = tape_rsrc(tape, rb, nrb, Tn), rtt = tape_rsrc(ttape, rb, nrb, Tn);
   float ac[16], acd[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) { ac[r] = 0.f; acd[r] = 0.f; }
   __syncthreads();
-  if (dH) tile_from_hbm(dhb + ((Tn - 1) & 1) * 32 * LH, LH, dH, row0, B, Tn, Tn - 1, H, ltid);
-  tile_from_hbm(dhdb + ((Tn - 1) & 1) * 32 * LH, LH, dHd, row0, B, Tn, Tn - 1, H, ltid);
-  Slot16 cc, cdc;  // c_t and cdot_t carried (loaded at the previous iteration as "prev")
   {
-    const size_t b = tape_base(rb, Tn - 1, Tn, w) + lane * 8 + 4 * SLOT_ELEMS;
-    cc = ld_slot(uok, tape + b);
-    cdc = ld_slot(uok, ttape + b);
+    Tile8<H> d0, d1;
+    d0.load(rdh, Tn, Tn - 1, true, ltid);
+    d1.load(rdhd, Tn, Tn - 1, true, ltid);
+    d0.to_lds(dhb + ((Tn - 1) & 1) * 32 * LH, LH, ltid);
+    d1.to_lds(dhdb + ((Tn - 1) & 1) * 32 * LH, LH, ltid);
   }
+  // c_t and cdot_t carried (loaded at the previous iteration as "prev")
+  Slot16 cc = ld_slot(rt, uok, lo, tape_off(Tn - 1, wu) + 4 * SLOT_ELEMS);
+  Slot16 cdc = ld_slot(rtt, uok, lo, tape_off(Tn - 1, wu) + 4 * SLOT_ELEMS);
   __syncthreads();
 
   for (int t = Tn - 1; t >= 0; --t) {
     const int cb = t & 1, nb = (t + 1) & 1;
-    if (t < Tn - 1) {
-      if constexpr (DX) {  // (the 16-byte copy perturbs this variant's register allocation into spills)
-        tile_to_hbm(zb + nb * 32 * LG, LG, dZ, row0, B, Tn, t + 1, G, ltid);
-        tile_to_hbm(zdb + nb * 32 * LG, LG, dZd, row0, B, Tn, t + 1, G, ltid);
-      } else {
-        tile16_to_hbm<G>(zb + nb * 32 * LG, LG, dZ, row0, B, Tn, t + 1, ltid);
-        tile16_to_hbm<G>(zdb + nb * 32 * LG, LG, dZd, row0, B, Tn, t + 1, ltid);
-      }
+    const bool pv = t > 0;
+    // loads first (next step's dH / dHd tiles, this step's tapes), then this tile's pending
+    // dz / dzdot stores: the tape wait below then covers no store of this step
+    // (the DX variant has no registers for the dH / dHd prefetch: it loads them at the end)
+    Tile8<H> ndh, ndhd;
+    if constexpr (!DX) {
+      ndh.load(rdh, Tn, t - 1, pv, ltid);
+      ndhd.load(rdhd, Tn, t - 1, pv, ltid);
     }
-    // this step's tapes
     Slot16 tg[4], zd[4], cp, cdp;
-    {
-      const bf16_t* tp = tape + tape_base(rb, t, Tn, w) + lane * 8;
-      const bf16_t* tq = ttape + tape_base(rb, t, Tn, w) + lane * 8;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) { tg[s] = ld_slot(uok, tp + s * SLOT_ELEMS); zd[s] = ld_slot(uok, tq + s * SLOT_ELEMS); }
-      cp.a = make_uint4(0, 0, 0, 0); cp.b = cp.a; cdp = cp;
-      if (t > 0) {
-        const size_t b = tape_base(rb, t - 1, Tn, w) + lane * 8 + 4 * SLOT_ELEMS;
-        cp = ld_slot(uok, tape + b);
-        cdp = ld_slot(uok, ttape + b);
-      }
+    for (int s = 0; s < 4; ++s) {
+      tg[s] = ld_slot(rt, uok, lo, tape_off(t, wu) + s * SLOT_ELEMS);
+      zd[s] = ld_slot(rtt, uok, lo, tape_off(t, wu) + s * SLOT_ELEMS);
     }
-    f32x16 ah = zero16(), ahd = zero16();
+    cp = ld_slot(rt, uok && pv, lo, tape_off(max(t - 1, 0), wu) + 4 * SLOT_ELEMS);
+    cdp = ld_slot(rtt, uok && pv, lo, tape_off(max(t - 1, 0), wu) + 4 * SLOT_ELEMS);
+    tile16_store<G>(zb + nb * 32 * LG, LG, rz, Tn, t + 1, t < Tn - 1, ltid);
+    tile16_store<G>(zdb + nb * 32 * LG, LG, rzd, Tn, t + 1, t < Tn - 1, ltid);
+    f32x16 ah = zero16(), ahd = zero16(), ax = zero16(), axd = zero16();
     if (t < Tn - 1) {
       const bf16_t* arow = zb + nb * 32 * LG + (lane & 31) * LG;
       const bf16_t* drow = zdb + nb * 32 * LG + (lane & 31) * LG;
       if (xw) {
-        f32x16 ax = zero16(), axd = zero16();
 #pragma unroll
         for (int ks = 0; ks < NKG; ++ks) {
           const typename P::frag a = P::lda(arow, ks, lane), ad = P::lda(drow, ks, lane);
@@ -717,8 +766,6 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
             axd = P::mma(ad, wt[ks], axd);
           }
         }
-        store_dx(ax, dX, row0, B, Tn, t + 1, K, kc, lane);
-        store_dx(axd, dXd, row0, B, Tn, t + 1, K, kc, lane);
       } else {
 #pragma unroll
         for (int ks = 0; ks < NKG; ++ks) {
@@ -726,6 +773,10 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
           ahd = P::mma(P::lda(drow, ks, lane), ut[ks], ahd);
         }
       }
+    }
+    if constexpr (DX) {
+      store_dx(ax, rdx, Tn, t + 1, xw && t < Tn - 1, nr, K, kc, lane);
+      store_dx(axd, rdxd, Tn, t + 1, xw && t < Tn - 1, nr, K, kc, lane);
     }
     const bf16_t* dh_t = dhb + cb * 32 * LH;
     const bf16_t* dhd_t = dhdb + cb * 32 * LH;
@@ -767,19 +818,23 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
         dr[3 * H] = f2bf(a_od * so);
       }
     }
-    if (t > 0) {
-      if (dH) tile_from_hbm(dhb + nb * 32 * LH, LH, dH, row0, B, Tn, t - 1, H, ltid);
-      tile_from_hbm(dhdb + nb * 32 * LH, LH, dHd, row0, B, Tn, t - 1, H, ltid);
+    if constexpr (DX) {
+      ndh.load(rdh, Tn, t - 1, pv, ltid);
+      ndhd.load(rdhd, Tn, t - 1, pv, ltid);
+    }
+    if (pv) {
+      ndh.to_lds(dhb + nb * 32 * LH, LH, ltid);
+      ndhd.to_lds(dhdb + nb * 32 * LH, LH, ltid);
       cc = cp;
       cdc = cdp;
     }
     lds_barrier();  // step hand-off: LDS only, stores stay in flight
   }
-  tile16_to_hbm<G>(zb, LG, dZ, row0, B, Tn, 0, ltid);
-  tile16_to_hbm<G>(zdb, LG, dZd, row0, B, Tn, 0, ltid);
+  tile16_store<G>(zb, LG, rz, Tn, 0, true, ltid);
+  tile16_store<G>(zdb, LG, rzd, Tn, 0, true, ltid);
   if constexpr (DX) {
+    f32x16 ax = zero16(), axd = zero16();
     if (xw) {
-      f32x16 ax = zero16(), axd = zero16();
       const bf16_t* arow = zb + (lane & 31) * LG;
       const bf16_t* drow = zdb + (lane & 31) * LG;
 #pragma unroll
@@ -787,9 +842,9 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
         ax = P::mma(P::lda(arow, ks, lane), wt[ks], ax);
         axd = P::mma(P::lda(drow, ks, lane), wt[ks], axd);
       }
-      store_dx(ax, dX, row0, B, Tn, 0, K, kc, lane);
-      store_dx(axd, dXd, row0, B, Tn, 0, K, kc, lane);
     }
+    store_dx(ax, rdx, Tn, 0, xw, nr, K, kc, lane);
+    store_dx(axd, rdxd, Tn, 0, xw, nr, K, kc, lane);
   }
   __syncthreads();
   }

@@ -15,7 +15,9 @@ import threading
 
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_hfrep_native.so")
+# HFREP_NATIVE_LIB: an alternative build of the same library (A/B kernel experiments only)
+_LIB_PATH = os.environ.get("HFREP_NATIVE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                               "_hfrep_native.so")
 _lock = threading.Lock()
 _loaded = None  # None = not tried, True/False afterwards
 _err: Exception | None = None

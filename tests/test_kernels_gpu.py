@@ -280,7 +280,10 @@ def test_lstm2_fused_layer(cuda, act, B, T, K):
         _close(dZd2, rzd, torch.bfloat16)
         dZ3, dZd3, dX3, dXd3 = Fn.lstm_layer_tbwd(dH.to(cuda) if with_dh else None, dHd.to(cuda), tape, ttape,
                                                   U.to(cuda), act, W=W.to(cuda))
-        assert torch.equal(dZ3, dZ2) and torch.equal(dZd3, dZd2)
+        # the DX instantiation may contract the gate math differently (1-ulp bf16 differences
+        # that the recurrence carries back in time): compare both variants to the reference
+        _close(dZ3, rz, torch.bfloat16)
+        _close(dZd3, rzd, torch.bfloat16)
         Wd = W.double()
         _close(dX3, rz @ Wd.t(), torch.bfloat16, scale=(rz.abs() @ Wd.abs().t()).max().item())
         _close(dXd3, rzd @ Wd.t(), torch.bfloat16, scale=(rzd.abs() @ Wd.abs().t()).max().item())
@@ -441,3 +444,35 @@ def test_lstm2_bwd_dx_only(cuda):
     dZ, dX = Fn.lstm_layer_bwd(dH, tape, U, 2, W=W)
     dZ2, dX2 = Fn.lstm_layer_bwd(dH, tape, U, 2, W=W, need_dz=False)
     assert dZ2 is None and torch.equal(dX, dX2)
+
+
+def test_lstm2_persistent_multi_pass(cuda):
+    """Persistent v2 kernels when every workgroup walks several row blocks (B > 2 * 32 * CUs) and
+    the last block is partial: buffer-descriptor range checks replace the per-row branches."""
+    from hfrep.ops import functional as Fn
+
+    H, T, K, act = 100, 3, 32, 2
+    B = 2 * 32 * 2 * torch.cuda.get_device_properties(0).multi_processor_count + 37
+    g = torch.Generator().manual_seed(61)
+    x = (torch.randn(B, T, K, generator=g) * 0.5).to(torch.bfloat16)
+    W = torch.randn(K, 4 * H, generator=g) * K ** -0.5
+    b = torch.randn(4 * H, generator=g) * 0.1
+    U = torch.randn(H, 4 * H, generator=g) * H ** -0.5
+    hs, tape = Fn.lstm_layer_fwd(x.to(cuda), W.to(cuda), b.to(cuda), U.to(cuda), act, True)
+    rh, rg, rc = R.lstm_seq_fwd(x.double() @ W.double() + b.double(), U.double(), act)
+    _close(hs, rh, torch.bfloat16)
+    dH = torch.randn(B, T, H, generator=g).to(torch.bfloat16)
+    dZ, dX = Fn.lstm_layer_bwd(dH.to(cuda), tape, U.to(cuda), act, W=W.to(cuda))
+    rdz = R.lstm_seq_bwd(dH.double(), rg, rc, U.double(), act)
+    _close(dZ, rdz, torch.bfloat16)
+    _close(dX, rdz @ W.double().t(), torch.bfloat16, scale=(rdz.abs() @ W.double().abs().t()).max().item())
+    xd = (torch.randn(B, T, K, generator=g) * 0.3).to(torch.bfloat16)
+    hds, ttape = Fn.lstm_layer_tfwd(xd.to(cuda), W.to(cuda), tape, U.to(cuda), act)
+    th, tz, tc = R.lstm_seq_tfwd(xd.double() @ W.double(), rg, rc, U.double(), act)
+    _close(hds, th, torch.bfloat16)
+    dHd = torch.randn(B, T, H, generator=g).to(torch.bfloat16)
+    dZ2, dZd2, dX2, dXd2 = Fn.lstm_layer_tbwd(dH.to(cuda), dHd.to(cuda), tape, ttape, U.to(cuda), act, W=W.to(cuda))
+    rz, rzd = R.lstm_seq_tbwd(dH.double(), dHd.double(), rg, rc, tz, tc, U.double(), act)
+    _close(dZ2, rz, torch.bfloat16)
+    _close(dZd2, rzd, torch.bfloat16)
+    _close(dXd2, rzd @ W.double().t(), torch.bfloat16, scale=(rzd.abs() @ W.double().abs().t()).max().item())
