@@ -666,6 +666,148 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
 }
 
 // ==========================================================================================
+// BPTT v3: role-split workgroup (8 waves, 2 per SIMD).  The v2 BPTT keeps U^T AND W^T fragments in
+// one wave (420 registers: one wave per SIMD, nothing hides its latencies).  Here waves 0-3 run
+// the recurrence (U^T fragments, tape loads, gate math: dz_t into LDS) and waves 4-7 move data and
+// produce the input gradient (W^T fragments: dx_{t+1} = dz_{t+1} W^T, the dz tile copy LDS -> HBM,
+// the dH tiles HBM -> LDS two steps ahead).  Each SIMD pairs one wave of each role, so the gate
+// math of one overlaps the MFMAs / stores of the other, and the recurrence waves issue only loads
+// (their waits never cover a store).  The two roles run separate loops with the same barrier
+// sequence (3 per row block + 1 per step).
+// ==========================================================================================
+template <int H, int ACT, bool DX>
+__global__ void __launch_bounds__(512)
+lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape, const float* __restrict__ U,
+                 bf16_t* __restrict__ dZ, const float* __restrict__ W, bf16_t* __restrict__ dX, int B, int Tn, int K) {
+  constexpr int act = ACT;
+  using P = MF<bf16_t>;
+  constexpr int G = 4 * H, NKG = (G + 15) / 16, LG = NKG * 16 + 8, NKH = (H + 15) / 16, LH = NKH * 16 + 8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* zb = reinterpret_cast<bf16_t*>(smem);  // [2][32][LG]  dz_t tiles
+  bf16_t* dhb = zb + 2 * 32 * LG;                 // [2][32][LH]  dH_t tiles
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, w = wave & 3;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int ltid = threadIdx.x & 255;  // thread index within the role group
+  const int u = w * 32 + (lane & 31);
+  const bool uok = u < H;
+  const int nrb = (B + 31) / 32;
+
+  if (wave < 4) {
+    // ---------------- recurrence waves ----------------
+    typename P::frag ut[NKG];
+#pragma unroll
+    for (int ks = 0; ks < NKG; ++ks)
+      ut[ks] = P::make([&](int k) {
+        const float v = U[(uok ? u : H - 1) * G + min(k, G - 1)];
+        return (uok && k < G) ? v : 0.f;
+      }, ks, lane);
+    const int lo = lane * 8;
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      const rsrc_t rt = tape_rsrc(tape, rb, nrb, Tn);
+      float dc[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dc[r] = 0.f;
+      Slot16 tg[4], cc, cp;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) tg[s] = ld_slot(rt, uok, lo, tape_off(Tn - 1, wu) + s * SLOT_ELEMS);
+      cc = ld_slot(rt, uok, lo, tape_off(Tn - 1, wu) + 4 * SLOT_ELEMS);
+      cp = ld_slot(rt, uok && Tn > 1, lo, tape_off(max(Tn - 2, 0), wu) + 4 * SLOT_ELEMS);
+      __syncthreads();  // (A) previous row block done with the LDS tiles
+      __syncthreads();  // (B) dH_{T-1} staged
+      for (int t = Tn - 1; t >= 0; --t) {
+        const bf16_t* zprev = zb + ((t + 1) & 1) * 32 * LG;  // dz_{t+1}
+        bf16_t* zcur = zb + (t & 1) * 32 * LG;               // dz_t
+        const bf16_t* dhcur = dhb + (t & 1) * 32 * LH;
+        // next step's tape (gates t-1, cell t-2): this wave issues loads only
+        const bool pv = t > 0;
+        Slot16 ng[4], ncp;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) ng[s] = ld_slot(rt, uok && pv, lo, tape_off(max(t - 1, 0), wu) + s * SLOT_ELEMS);
+        ncp = ld_slot(rt, uok && t > 1, lo, tape_off(max(t - 2, 0), wu) + 4 * SLOT_ELEMS);
+        f32x16 acc = zero16();
+        if (t < Tn - 1) {
+          const bf16_t* arow = zprev + (lane & 31) * LG;
+#pragma unroll
+          for (int ks = 0; ks < NKG; ++ks) acc = P::mma(P::lda(arow, ks, lane), ut[ks], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rr = acc32_row(r, lane);
+          const float ig = tg[0].get(r), fg = tg[1].get(r), gg = tg[2].get(r), og = tg[3].get(r);
+          const float c = cc.get(r), cpv = cp.get(r);
+          const float dht = (uok ? bf2f(dhcur[rr * LH + u]) : 0.f) + acc[r];
+          const float ca = act_f(act, c);
+          const float dov = dht * ca;
+          const float dct = dc[r] + dht * og * act_dy(act, ca);
+          dc[r] = uok ? dct * fg : 0.f;
+          if (uok) {
+            bf16_t* zr = zcur + rr * LG + u;
+            zr[0] = f2bf(dct * gg * ig * (1.f - ig));
+            zr[H] = f2bf(dct * cpv * fg * (1.f - fg));
+            zr[2 * H] = f2bf(dct * ig * act_dy(act, gg));
+            zr[3 * H] = f2bf(dov * og * (1.f - og));
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) tg[s] = ng[s];
+        cc = cp;
+        cp = ncp;
+        lds_barrier();  // step hand-off
+      }
+      __syncthreads();  // (C) the data waves have stored dz_0 / dx_0
+    }
+  } else {
+    // ---------------- data / input-gradient waves ----------------
+    const int kc = u;
+    typename P::frag wt[DX ? NKG : 1];
+    if constexpr (DX) make_wt<NKG>(wt, W, K, G, kc, lane);
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      const int row0 = rb * 32;
+      const int nr = min(32, B - row0);
+      const rsrc_t rdh = tile_rsrc(dH, row0, B, Tn, H), rz = tile_rsrc(dZ, row0, B, Tn, G);
+      const rsrc_t rdx = tile_rsrc(DX ? dX : nullptr, row0, B, Tn, DX ? K : 1);
+      Tile8<H> d0, d1;  // dH_{t-1}, dH_{t-2} in flight (two steps of prefetch)
+      d0.load(rdh, Tn, Tn - 1, true, ltid);
+      d1.load(rdh, Tn, Tn - 2, Tn > 1, ltid);
+      __syncthreads();  // (A)
+      d0.to_lds(dhb + ((Tn - 1) & 1) * 32 * LH, LH, ltid);
+      d0 = d1;
+      d1.load(rdh, Tn, Tn - 3, Tn > 2, ltid);
+      __syncthreads();  // (B)
+      for (int t = Tn - 1; t >= 0; --t) {
+        const bf16_t* zprev = zb + ((t + 1) & 1) * 32 * LG;  // dz_{t+1}, final since the last barrier
+        const bool live = t < Tn - 1;
+        tile16_store<G>(zprev, LG, rz, Tn, t + 1, live, ltid);
+        if constexpr (DX) {
+          f32x16 ax = zero16();
+          if (live && wu * 32 < K) {  // (K = 32: waves 5-7 own no input column)
+            const bf16_t* arow = zprev + (lane & 31) * LG;
+#pragma unroll
+            for (int ks = 0; ks < NKG; ++ks) ax = P::mma(P::lda(arow, ks, lane), wt[ks], ax);
+          }
+          store_dx(ax, rdx, Tn, t + 1, live, nr, K, kc, lane);
+        }
+        if (t > 0) d0.to_lds(dhb + ((t - 1) & 1) * 32 * LH, LH, ltid);  // dH_{t-1} for the next step
+        d0 = d1;
+        d1.load(rdh, Tn, t - 3, t > 2, ltid);
+        lds_barrier();  // step hand-off
+      }
+      tile16_store<G>(zb, LG, rz, Tn, 0, true, ltid);
+      if constexpr (DX) {
+        f32x16 ax = zero16();
+        if (wu * 32 < K) {
+          const bf16_t* arow = zb + (lane & 31) * LG;
+#pragma unroll
+          for (int ks = 0; ks < NKG; ++ks) ax = P::mma(P::lda(arow, ks, lane), wt[ks], ax);
+        }
+        store_dx(ax, rdx, Tn, 0, true, nr, K, kc, lane);
+      }
+      __syncthreads();  // (C)
+    }
+  }
+}
+
+// ==========================================================================================
 // reverse of the tangent system: (dZ, dZd) from (dH?, dHd), primal tape and tangent tape
 // ==========================================================================================
 template <int H, int ACT, int TILES, bool DX>
@@ -963,6 +1105,13 @@ void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const voi
   else HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 0, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
 }
 
+#define HFREP_BWD3_LAUNCH(DXV, ...)                                                            \
+  switch (act) {                                                                                 \
+    case 0: launch(lstm_bwd3_kernel<100, 0, DXV>, __VA_ARGS__); break;                           \
+    case 1: launch(lstm_bwd3_kernel<100, 1, DXV>, __VA_ARGS__); break;                           \
+    default: launch(lstm_bwd3_kernel<100, 2, DXV>, __VA_ARGS__); break;                          \
+  }
+
 #define HFREP_BWD_LAUNCH(KERNEL, TL, DXV, ...)                                                  \
   switch (act) {                                                                                 \
     case 0: launch(KERNEL<100, 0, TL, DXV>, __VA_ARGS__); break;                                 \
@@ -970,10 +1119,28 @@ void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const voi
     default: launch(KERNEL<100, 2, TL, DXV>, __VA_ARGS__); break;                                \
   }
 
+static int lstm_bwd_version() {  // HFREP_LSTM_BWD=2: the single-role v2 BPTT (A/B only)
+  static int v = 0;
+  if (!v) {
+    const char* e = getenv("HFREP_LSTM_BWD");
+    v = (e && atoi(e) == 2) ? 2 : 3;
+  }
+  return v;
+}
+
 void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, const float* W, void* dX, int K,
                       int B, int Tn, int H, int act, hipStream_t s) {
   const bf16_t* dh = (const bf16_t*)dH;
   const bf16_t* tp = (const bf16_t*)tape;
+  if (lstm_bwd_version() == 3) {
+    const int g = persistent_grid(B, 1);
+    const size_t sm = bwd_smem(H, 1);
+    if (dX)
+      HFREP_BWD3_LAUNCH(true, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn, K)
+    else
+      HFREP_BWD3_LAUNCH(false, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, (const float*)nullptr, (bf16_t*)nullptr, B, Tn, 0)
+    return;
+  }
   if (dX)  // fused input gradient: U^T and W^T fragments in registers -> one row tile per workgroup
     HFREP_BWD_LAUNCH(lstm_bwd2_kernel, 1, true, persistent_grid(B, 1), 256, bwd_smem(H, 1), s, dh, tp, U, (bf16_t*)dZ,
                      W, (bf16_t*)dX, B, Tn, K, lstm_dbg())
