@@ -250,7 +250,7 @@ class LayerNormalization(Layer):
         return R.layer_norm(x, self.w("gamma"), self.w("beta"), self.eps)
 
     def efwd(self, x, save):
-        y, xhat, rstd = Fn.layer_norm_fwd(x, self.p("gamma"), self.p("beta"), self.eps)
+        y, xhat, rstd = Fn.layer_norm_fwd(x, self.p("gamma"), self.p("beta"), self.eps, save=save)
         return y, ({"x": x, "xhat": xhat, "rstd": rstd} if save else None)
 
     def ebwd(self, ctx, dy, need_dx, wgrad=True):

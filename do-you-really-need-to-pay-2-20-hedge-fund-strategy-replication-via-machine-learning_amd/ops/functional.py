@@ -135,9 +135,10 @@ def shift_prev(h_seq: torch.Tensor) -> torch.Tensor:
 # ---------------------------------------------------------------------------------------
 # LayerNorm
 # ---------------------------------------------------------------------------------------
-def layer_norm_fwd(x, gamma, beta, eps: float):
+def layer_norm_fwd(x, gamma, beta, eps: float, save: bool = True):
+    """(y, xhat, rstd); with save=False the native kernel skips xhat / rstd (returned empty)."""
     if _nat(x):
-        y, xhat, rstd = _ops().layernorm_fwd(x.contiguous(), gamma, beta, float(eps))
+        y, xhat, rstd = _ops().layernorm_fwd(x.contiguous(), gamma, beta, float(eps), bool(save))
         return y, xhat, rstd
     return R.layer_norm_fwd(x, gamma.to(x.dtype), beta.to(x.dtype), eps)
 

@@ -25,7 +25,7 @@ st = _native.native().lstm2_stamps().double()
 nw = min(4096, (B + 63) // 64 * 8)  # waves that ran (2 tiles x 4 waves per workgroup)
 st = st[:nw]
 st = st[st.sum(1) > 0]
-names = ["h_store", "x_load_issue", "mfma_x", "mfma_h", "gates_tape", "x_store_lds", "barrier", "loop_top"]
+names = ["x_load_issue", "h_store", "mfma_x", "mfma_h", "gates_tape", "x_store_lds", "barrier", "loop_top"]
 tot = st.sum(1).mean().item()
 print(json.dumps({"waves": int(st.shape[0]), "cycles_per_wave": tot,
                   "share": {n: round(st[:, i].mean().item() / tot, 4) for i, n in enumerate(names)}}))

@@ -124,17 +124,22 @@ def test_lstm_tangent(cuda, dt, act):
     _close(dZd0, rZd0, dt)
 
 
+@pytest.mark.parametrize("D", [100, 35])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_layernorm(cuda, dt):
+def test_layernorm(cuda, dt, D):
     g = torch.Generator().manual_seed(7)
-    x = (torch.randn(37, 11, 100, generator=g) * 2 + 0.5).to(dt)
-    gamma, beta = torch.randn(100, generator=g), torch.randn(100, generator=g)
+    x = (torch.randn(37, 11, D, generator=g) * 2 + 0.5).to(dt)
+    gamma, beta = torch.randn(D, generator=g), torch.randn(D, generator=g)
     y, xhat, rstd = _ops().layernorm_fwd(x.to(cuda), gamma.to(cuda), beta.to(cuda), 1e-3)
     ry, rxh, rrs = R.layer_norm_fwd(x.double(), gamma.double(), beta.double(), 1e-3)
     _close(y, ry, dt)
+    _close(xhat, rxh, dt)
     _close(rstd, rrs, dt)
-    dy = torch.randn(37, 11, 100, generator=g).to(dt)
-    gg, gb = torch.zeros(100, device=cuda), torch.zeros(100, device=cuda)
+    # no-grad form: same y, nothing saved
+    y2, xh2, rs2 = _ops().layernorm_fwd(x.to(cuda), gamma.to(cuda), beta.to(cuda), 1e-3, False)
+    assert torch.equal(y2, y) and xh2.numel() == 0 and rs2.numel() == 0
+    dy = torch.randn(37, 11, D, generator=g).to(dt)
+    gg, gb = torch.zeros(D, device=cuda), torch.zeros(D, device=cuda)
     dx = _ops().layernorm_bwd_(dy.to(cuda), xhat, rstd, gamma.to(cuda), gg, gb)
     rdx, rdg, rdb = R.layer_norm_bwd(dy.double(), xhat.double().cpu(), rstd.double().cpu(), gamma.double())
     _close(dx, rdx, dt)
