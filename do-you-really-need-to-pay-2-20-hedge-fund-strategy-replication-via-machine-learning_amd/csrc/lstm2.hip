@@ -993,6 +993,310 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 }
 
 // ==========================================================================================
+// Tangent reverse v4: 16x16x32 MFMAs, 16 units per wave.
+//
+// The v2 kernel (32 units per wave, 32x32x16) holds U^T and W^T fragments (200 VGPRs) plus 12
+// tape slots, both adjoint accumulators and the carried cell adjoints in one wave: ~500 registers,
+// one wave per SIMD, spills in the dX variant, and nothing to hide its latencies.  A role split
+// (as BPTT v3) does not fit either: the recurrence alone needs ~290 registers.  Halving the wave's
+// column count halves every per-lane array instead: with v_mfma_f32_16x16x32_bf16 a wave owns
+// 16 units x 32 rows (U^T / W^T fragments 52 VGPRs each, 8 values per tape slot), so seven
+// compute waves (112 units >= H) fit at two waves per SIMD with the input gradient fused, and
+// the eighth wave is a data wave: dz / dzdot tile stores and the dH / dHdot tiles HBM -> LDS.
+// The compute waves issue tape loads and the dX stores only, loads first.  The tapes keep the
+// 32x32 layout written by lstm_fwd2 / lstm_tfwd2: a 16x16 accumulator lane's four rows of one
+// 16-row block are four contiguous values of one 32x32 lane's slot half (one 8-byte load).
+// ==========================================================================================
+struct Slot8 {  // 8 bf16 of one 16x16-layout lane: block m = 0, 1 (rows 16 m + 4 (lane >> 4) + i)
+  uint2 m0, m1;
+  __device__ __forceinline__ float get(int m, int i) const {
+    const uint32_t w = m == 0 ? ((i >> 1) ? m0.y : m0.x) : ((i >> 1) ? m1.y : m1.x);
+    return (i & 1) ? hi_bf(w) : lo_bf(w);
+  }
+};
+__device__ __forceinline__ Slot8 ld_slot8(rsrc_t rs, bool on, int lane_off, int uoff) {
+  Slot8 s;
+  const int v = on ? lane_off * 2 : kOOB;
+  s.m0 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, v, uoff * 2, 0));
+  s.m1 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, v, (uoff + SLOT_HALF) * 2, 0));
+  return s;
+}
+__device__ __forceinline__ f32x4 mma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// dX rows of a 16x16 accumulator pair: 8 two-byte stores per lane, always issued
+__device__ __forceinline__ void store_dx16(const f32x4 (&ax)[2], rsrc_t rd, int Tn, int t, bool on, int nr, int K,
+                                           int kc, int g4) {
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 16 * m + 4 * g4 + i;
+      const int off = (on && kc < K && row < nr) ? (row * Tn * K + kc) * 2 : kOOB;
+      __builtin_amdgcn_raw_buffer_store_b16(f2bf(ax[m][i]), rd, off, t * K * 2, 0);
+    }
+}
+// one wave moves a [32 x W] LDS tile to step t of a tile descriptor (16-byte chunks, soffset 0)
+template <int W>
+__device__ __forceinline__ void tile16_store_w(const bf16_t* buf, int LD, rsrc_t rd, int Tn, int t, bool on, int lane) {
+  constexpr int CPR = W / 8, NJ = (32 * CPR + 63) / 64;
+#pragma unroll 5
+  for (int j = 0; j < NJ; ++j) {
+    const int e = lane + 64 * j;
+    const int r = e / CPR, c = e - r * CPR;
+    const bool ok = r < 32;
+    const v4i v = *reinterpret_cast<const v4i*>(buf + (ok ? r : 31) * LD + 8 * c);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rd, (on && ok) ? ((r * Tn + t) * W + 8 * c) * 2 : kOOB, 0, 0);
+  }
+}
+// one wave's share of a [32 x W] tile in 8-byte chunks, HBM -> registers -> LDS
+template <int W>
+struct Tile8w {
+  static constexpr int CPR = W / 4, NJ = (32 * CPR + 63) / 64;
+  v2i v[NJ];
+  __device__ __forceinline__ void load(rsrc_t rs, int Tn, int t, bool on, int lane) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int e = lane + 64 * j;
+      const int r = e / CPR, c = e - r * CPR;
+      v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, (on && r < 32) ? (r * Tn * W + 4 * c) * 2 : kOOB, t * W * 2, 0);
+    }
+  }
+  __device__ __forceinline__ void to_lds(bf16_t* buf, int LD, int lane) const {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int e = lane + 64 * j;
+      const int r = e / CPR, c = e - r * CPR;
+      if (r < 32) *reinterpret_cast<v2i*>(buf + r * LD + 4 * c) = v[j];
+    }
+  }
+};
+
+template <int H>
+struct Tb4Geo {
+  static constexpr int G = 4 * H, NK = (G + 31) / 32, LG = NK * 32 + 8, LH = ((H + 3) / 4) * 4 + 4;
+  static constexpr int NCW = (H + 15) / 16;  // compute waves
+  static_assert(NCW <= 7, "tbwd4: H <= 112 (7 compute waves + 1 data wave)");
+  static constexpr size_t smem = (size_t)(4 * 32 * LG + 4 * 32 * LH) * 2;
+};
+
+template <int H, int ACT, bool DX>
+__global__ void __launch_bounds__(512)
+lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd, const bf16_t* __restrict__ tape,
+                  const bf16_t* __restrict__ ttape, const float* __restrict__ U, bf16_t* __restrict__ dZ,
+                  bf16_t* __restrict__ dZd, const float* __restrict__ W, bf16_t* __restrict__ dX,
+                  bf16_t* __restrict__ dXd, int B, int Tn, int K) {
+  constexpr int act = ACT;
+  using Geo = Tb4Geo<H>;
+  constexpr int G = Geo::G, NK = Geo::NK, LG = Geo::LG, LH = Geo::LH;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* zb = reinterpret_cast<bf16_t*>(smem);  // [2][32][LG]  dz_t
+  bf16_t* zdb = zb + 2 * 32 * LG;                 // [2][32][LG]  dzdot_t
+  bf16_t* dhb = zdb + 2 * 32 * LG;                // [2][32][LH]  dH_t
+  bf16_t* dhdb = dhb + 2 * 32 * LH;               // [2][32][LH]  dHdot_t
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nrb = (B + 31) / 32;
+  // the K padding columns [G, 32 NK) of the dz tiles are read by the last MFMA k-step: zero them
+  // once (nothing writes them afterwards; garbage there could be a NaN times a zero fragment)
+  for (int i = threadIdx.x; i < 4 * 32 * (32 * NK - G); i += 512) {
+    const int buf = i / (32 * (32 * NK - G)), rem = i - buf * 32 * (32 * NK - G);
+    const int r = rem / (32 * NK - G), c = G + rem - r * (32 * NK - G);
+    zb[buf * 32 * LG + r * LG + c] = 0;  // buf 0..3 spans zb[0..1] and zdb[0..1]
+  }
+
+  if (wave < Geo::NCW) {
+    // ---------------- compute waves: 16 units each ----------------
+    const int g4 = lane >> 4, c = 16 * wave + (lane & 15);
+    const bool uok = c < H;
+    const int wt32 = __builtin_amdgcn_readfirstlane(wave >> 1);  // the 32x32 tape wave holding unit c
+    const int lo8 = (32 * (g4 & 1) + (c & 31)) * 8 + 4 * (g4 >> 1);
+    bf16x8 ut[NK];
+#pragma unroll
+    for (int ks = 0; ks < NK; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * ks + 8 * g4 + j;
+        const float v = U[(size_t)(uok ? c : H - 1) * G + min(k, G - 1)];
+        ut[ks][j] = (short)f2bf((uok && k < G) ? v : 0.f);
+      }
+    const bool xw = DX && 16 * wave < K;  // this wave owns input columns (wave-uniform)
+    bf16x8 wt[DX ? NK : 1];
+    if constexpr (DX) {
+#pragma unroll
+      for (int ks = 0; ks < NK; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 32 * ks + 8 * g4 + j;
+          const float v = W[(size_t)min(c, K - 1) * G + min(k, G - 1)];
+          wt[ks][j] = (short)f2bf((c < K && k < G) ? v : 0.f);
+        }
+    }
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      const int row0 = rb * 32, nr = min(32, B - row0);
+      const rsrc_t rt = tape_rsrc(tape, rb, nrb, Tn), rtt = tape_rsrc(ttape, rb, nrb, Tn);
+      const rsrc_t rdx = tile_rsrc(DX ? dX : nullptr, row0, B, Tn, DX ? K : 1);
+      const rsrc_t rdxd = tile_rsrc(DX ? dXd : nullptr, row0, B, Tn, DX ? K : 1);
+      float ac[8], acd[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { ac[e] = 0.f; acd[e] = 0.f; }
+      Slot8 cc = ld_slot8(rt, uok, lo8, tape_off(Tn - 1, wt32) + 4 * SLOT_ELEMS);
+      Slot8 cdc = ld_slot8(rtt, uok, lo8, tape_off(Tn - 1, wt32) + 4 * SLOT_ELEMS);
+      __syncthreads();  // (A) LDS free (previous row block stored)
+      __syncthreads();  // (B) dH_{T-1} / dHd_{T-1} staged
+      for (int t = Tn - 1; t >= 0; --t) {
+        const int cb = t & 1, nb = (t + 1) & 1;
+        const bool pv = t > 0, live = t < Tn - 1;
+        Slot8 tg[4], zd[4], cp, cdp;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          tg[s] = ld_slot8(rt, uok, lo8, tape_off(t, wt32) + s * SLOT_ELEMS);
+          zd[s] = ld_slot8(rtt, uok, lo8, tape_off(t, wt32) + s * SLOT_ELEMS);
+        }
+        cp = ld_slot8(rt, uok && pv, lo8, tape_off(max(t - 1, 0), wt32) + 4 * SLOT_ELEMS);
+        cdp = ld_slot8(rtt, uok && pv, lo8, tape_off(max(t - 1, 0), wt32) + 4 * SLOT_ELEMS);
+        f32x4 ah[2], ahd[2], ax[2], axd[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          ah[m] = f32x4{0.f, 0.f, 0.f, 0.f}; ahd[m] = ah[m]; ax[m] = ah[m]; axd[m] = ah[m];
+        }
+        if (live) {
+#pragma unroll
+          for (int m = 0; m < 2; ++m) {
+            const bf16_t* arow = zb + nb * 32 * LG + (16 * m + (lane & 15)) * LG + 8 * g4;
+            const bf16_t* drow = zdb + nb * 32 * LG + (16 * m + (lane & 15)) * LG + 8 * g4;
+            if (xw) {
+#pragma unroll
+              for (int ks = 0; ks < NK; ++ks) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(arow + 32 * ks);
+                const bf16x8 ad = *reinterpret_cast<const bf16x8*>(drow + 32 * ks);
+                ah[m] = mma16(a, ut[ks], ah[m]);
+                ahd[m] = mma16(ad, ut[ks], ahd[m]);
+                if constexpr (DX) {
+                  ax[m] = mma16(a, wt[ks], ax[m]);
+                  axd[m] = mma16(ad, wt[ks], axd[m]);
+                }
+              }
+            } else {
+#pragma unroll
+              for (int ks = 0; ks < NK; ++ks) {
+                ah[m] = mma16(*reinterpret_cast<const bf16x8*>(arow + 32 * ks), ut[ks], ah[m]);
+                ahd[m] = mma16(*reinterpret_cast<const bf16x8*>(drow + 32 * ks), ut[ks], ahd[m]);
+              }
+            }
+          }
+        }
+        if constexpr (DX) {
+          store_dx16(ax, rdx, Tn, t + 1, xw && live, nr, K, c, g4);
+          store_dx16(axd, rdxd, Tn, t + 1, xw && live, nr, K, c, g4);
+        }
+        const bf16_t* dh_t = dhb + cb * 32 * LH;
+        const bf16_t* dhd_t = dhdb + cb * 32 * LH;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int e = 4 * m + i, rr = 16 * m + 4 * g4 + i;
+            const float ig = tg[0].get(m, i), fg = tg[1].get(m, i), gg = tg[2].get(m, i), og = tg[3].get(m, i);
+            const float cv = cc.get(m, i), cpv = cp.get(m, i), cd = cdc.get(m, i), cdpv = cdp.get(m, i);
+            const float zdi = zd[0].get(m, i), zdf = zd[1].get(m, i), zdg = zd[2].get(m, i), zdo = zd[3].get(m, i);
+            const float si = ig * (1.f - ig), sf = fg * (1.f - fg), so = og * (1.f - og);
+            const float sg = act_dy(act, gg);
+            const float idot = si * zdi, fdot = sf * zdf, gdot = sg * zdg, odot = so * zdo;
+            const float ca = act_f(act, cv);
+            const float e1 = act_dy(act, ca), e2 = act_d2y(act, ca);
+            const float a_h = (uok ? bf2f(dh_t[rr * LH + c]) : 0.f) + ah[m][i];
+            const float a_hd = (uok ? bf2f(dhd_t[rr * LH + c]) : 0.f) + ahd[m][i];
+            const float a_od = a_hd * ca;
+            const float a_o = a_h * ca + a_hd * e1 * cd;
+            const float a_cd = acd[e] + a_hd * og * e1;
+            const float a_c = ac[e] + a_h * og * e1 + a_hd * (odot * e1 + og * e2 * cd);
+            const float a_fd = a_cd * cpv, a_id = a_cd * gg, a_gd = a_cd * ig;
+            const float a_f = a_c * cpv + a_cd * cdpv;
+            const float a_i = a_c * gg + a_cd * gdot;
+            const float a_g = a_c * ig + a_cd * idot;
+            ac[e] = uok ? a_c * fg + a_cd * fdot : 0.f;
+            acd[e] = uok ? a_cd * fg : 0.f;
+            const float s2i = si * (1.f - 2.f * ig), s2f = sf * (1.f - 2.f * fg), s2o = so * (1.f - 2.f * og);
+            const float s2g = act_d2y(act, gg);
+            if (uok) {
+              bf16_t* zr = zb + cb * 32 * LG + rr * LG + c;
+              bf16_t* dr = zdb + cb * 32 * LG + rr * LG + c;
+              zr[0] = f2bf(a_i * si + a_id * s2i * zdi);
+              zr[H] = f2bf(a_f * sf + a_fd * s2f * zdf);
+              zr[2 * H] = f2bf(a_g * sg + a_gd * s2g * zdg);
+              zr[3 * H] = f2bf(a_o * so + a_od * s2o * zdo);
+              dr[0] = f2bf(a_id * si);
+              dr[H] = f2bf(a_fd * sf);
+              dr[2 * H] = f2bf(a_gd * sg);
+              dr[3 * H] = f2bf(a_od * so);
+            }
+          }
+        cc = cp;
+        cdc = cdp;
+        lds_barrier();  // step hand-off
+      }
+      if constexpr (DX) {  // dx_0 / dxdot_0 from the last dz tiles (final after the last barrier)
+        f32x4 ax[2], axd[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          ax[m] = f32x4{0.f, 0.f, 0.f, 0.f}; axd[m] = ax[m];
+          if (xw) {
+            const bf16_t* arow = zb + (16 * m + (lane & 15)) * LG + 8 * g4;
+            const bf16_t* drow = zdb + (16 * m + (lane & 15)) * LG + 8 * g4;
+#pragma unroll
+            for (int ks = 0; ks < NK; ++ks) {
+              ax[m] = mma16(*reinterpret_cast<const bf16x8*>(arow + 32 * ks), wt[ks], ax[m]);
+              axd[m] = mma16(*reinterpret_cast<const bf16x8*>(drow + 32 * ks), wt[ks], axd[m]);
+            }
+          }
+        }
+        store_dx16(ax, rdx, Tn, 0, xw, nr, K, c, g4);
+        store_dx16(axd, rdxd, Tn, 0, xw, nr, K, c, g4);
+      }
+      __syncthreads();  // (C)
+    }
+  } else if (wave == 7) {
+    // ---------------- data wave ----------------
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      const int row0 = rb * 32;
+      const rsrc_t rdh = tile_rsrc(dH, row0, B, Tn, H), rdhd = tile_rsrc(dHd, row0, B, Tn, H);
+      const rsrc_t rz = tile_rsrc(dZ, row0, B, Tn, G), rzd = tile_rsrc(dZd, row0, B, Tn, G);
+      Tile8w<H> a, ad;
+      a.load(rdh, Tn, Tn - 1, true, lane);
+      ad.load(rdhd, Tn, Tn - 1, true, lane);
+      __syncthreads();  // (A)
+      a.to_lds(dhb + ((Tn - 1) & 1) * 32 * LH, LH, lane);
+      ad.to_lds(dhdb + ((Tn - 1) & 1) * 32 * LH, LH, lane);
+      __syncthreads();  // (B)
+      for (int t = Tn - 1; t >= 0; --t) {
+        const int nb = (t + 1) & 1;
+        const bool pv = t > 0, live = t < Tn - 1;
+        a.load(rdh, Tn, t - 1, pv, lane);  // loads first: their wait covers no store of this step
+        ad.load(rdhd, Tn, t - 1, pv, lane);
+        tile16_store_w<G>(zb + nb * 32 * LG, LG, rz, Tn, t + 1, live, lane);
+        tile16_store_w<G>(zdb + nb * 32 * LG, LG, rzd, Tn, t + 1, live, lane);
+        if (pv) {
+          a.to_lds(dhb + nb * 32 * LH, LH, lane);  // dH_{t-1}: (t - 1) & 1 == nb
+          ad.to_lds(dhdb + nb * 32 * LH, LH, lane);
+        }
+        lds_barrier();
+      }
+      tile16_store_w<G>(zb, LG, rz, Tn, 0, true, lane);
+      tile16_store_w<G>(zdb, LG, rzd, Tn, 0, true, lane);
+      __syncthreads();  // (C)
+    }
+  } else {
+    // idle waves (H <= 96): keep the barrier sequence
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      __syncthreads();
+      __syncthreads();
+      for (int t = Tn - 1; t >= 0; --t) lds_barrier();
+      __syncthreads();
+    }
+  }
+}
+
+// ==========================================================================================
 // host side
 // ==========================================================================================
 size_t lstm2_tape_elems(int B, int Tn) { return (size_t)((B + 31) / 32) * Tn * NW2 * TAPE_SLOTS * SLOT_ELEMS; }
@@ -1148,9 +1452,37 @@ void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ
     HFREP_BWD_LAUNCH(lstm_bwd2_kernel, 1, false, persistent_grid(B, 1), 256, bwd_smem(H, 1), s, dh, tp, U, (bf16_t*)dZ,
                      (const float*)nullptr, (bf16_t*)nullptr, B, Tn, 0, lstm_dbg())
 }
+static int lstm_tbwd_version() {  // HFREP_LSTM_TBWD=2: the v2 tangent reverse (A/B only)
+  static int v = 0;
+  if (!v) {
+    const char* e = getenv("HFREP_LSTM_TBWD");
+    v = (e && atoi(e) == 2) ? 2 : 4;
+  }
+  return v;
+}
+
+#define HFREP_TBWD4_LAUNCH(DXV, ...)                                                           \
+  switch (act) {                                                                                 \
+    case 0: launch(lstm_tbwd4_kernel<100, 0, DXV>, __VA_ARGS__); break;                          \
+    case 1: launch(lstm_tbwd4_kernel<100, 1, DXV>, __VA_ARGS__); break;                          \
+    default: launch(lstm_tbwd4_kernel<100, 2, DXV>, __VA_ARGS__); break;                         \
+  }
+
 void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const void* ttape, const float* U, void* dZ,
                        void* dZd, const float* W, void* dX, void* dXd, int K, int B, int Tn, int H, int act,
                        hipStream_t s) {
+  if (lstm_tbwd_version() == 4) {
+    const int g = persistent_grid(B, 1);
+    const size_t sm = Tb4Geo<100>::smem;
+    if (dX)
+      HFREP_TBWD4_LAUNCH(true, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
+                         (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, W, (bf16_t*)dX, (bf16_t*)dXd, B, Tn, K)
+    else
+      HFREP_TBWD4_LAUNCH(false, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
+                         (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, (const float*)nullptr, (bf16_t*)nullptr,
+                         (bf16_t*)nullptr, B, Tn, 0)
+    return;
+  }
   if (dX)
     HFREP_BWD_LAUNCH(lstm_tbwd2_kernel, 1, true, persistent_grid(B, 1), 256, tbwd_smem(H), s, (const bf16_t*)dH,
                      (const bf16_t*)dHd, (const bf16_t*)tape, (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, W,
