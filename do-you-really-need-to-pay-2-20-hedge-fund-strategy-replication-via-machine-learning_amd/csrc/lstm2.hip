@@ -1049,6 +1049,19 @@ __device__ __forceinline__ void tile16_store_w(const bf16_t* buf, int LD, rsrc_t
     __builtin_amdgcn_raw_buffer_store_b128(v, rd, (on && ok) ? ((r * Tn + t) * W + 8 * c) * 2 : kOOB, 0, 0);
   }
 }
+// one wave stores a [32 x W] LDS tile to step t of a tile descriptor in 8-byte chunks
+template <int W>
+__device__ __forceinline__ void tile8_store_w(const bf16_t* buf, int LD, rsrc_t rd, int Tn, int t, bool on, int lane) {
+  constexpr int CPR = W / 4, NJ = (32 * CPR + 63) / 64;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int e = lane + 64 * j;
+    const int r = e / CPR, c = e - r * CPR;
+    const bool ok = r < 32;
+    const v2i v = *reinterpret_cast<const v2i*>(buf + (ok ? r : 31) * LD + 4 * c);
+    __builtin_amdgcn_raw_buffer_store_b64(v, rd, (on && ok) ? (r * Tn * W + 4 * c) * 2 : kOOB, t * W * 2, 0);
+  }
+}
 // one wave's share of a [32 x W] tile in 8-byte chunks, HBM -> registers -> LDS
 template <int W>
 struct Tile8w {
@@ -1297,6 +1310,299 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 }
 
 // ==========================================================================================
+// Forward / tangent forward v4: 16x16x32 MFMAs, 16 units per wave, 7 compute waves + 1 data wave.
+//
+// Same decomposition as the tangent reverse v4: a compute wave owns 16 units of one 32-row tile
+// and keeps BOTH weight operands as register fragments (W^T for the input projection, U^T for
+// the recurrence: 4 gates x ceil(K/32) and 4 gates x 4 k-steps of 8 bf16), so the step loop reads
+// only the x / h tiles from LDS (v2 re-read the staged W^T from LDS every step: 28 KB per wave per
+// step).  The data wave streams x_{t+1} (or xdot_{t+1}) HBM -> LDS and h_{t-1} (hdot) LDS -> HBM;
+// the compute waves issue only the tape stores (and, for the tangent, the primal tape loads one
+// step ahead).  Tapes are written in the 32x32 layout the BPTT / tangent reverse kernels read: a
+// lane's four rows of a 16-row block are four contiguous values of a slot half (8-byte stores).
+// TAN = false: z = x W + h U + b, tape = gate activations + cell.  TAN = true: zdot = xdot W +
+// hdot U at the taped primal point, tape = tangent pre-activations + cell tangent.
+// ==========================================================================================
+// a K extent as full 32-wide k-steps plus at most one 16-wide tail step (v_mfma_f32_16x16x16_bf16):
+// K = 100 -> 3 x 32 + 16 = 112 instead of 128 (fewer fragment registers and MFMAs)
+template <int KD>
+struct KSplit {
+  static constexpr bool TAIL = KD > 0 && (KD % 32) != 0 && (KD % 32) <= 16;
+  static constexpr int NF = KD > 0 ? (TAIL ? KD / 32 : (KD + 31) / 32) : 4;  // (KD = 0: runtime K <= 128)
+  static constexpr int KP = 32 * NF + (TAIL ? 16 : 0);
+};
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mma16k16(const bf16x4& a, const bf16x4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+template <int H, int KX>
+struct Fw4Geo {
+  static constexpr int G = 4 * H, KPH = KSplit<H>::KP, LH = KPH + 8;
+};
+// x tile loader of the data wave: XJ chunks per lane (8-byte chunks if K % 4 == 0, else 2-byte)
+template <int KX>
+struct XTile {
+  static constexpr bool VEC = KX > 0 && KX % 4 == 0;
+  static constexpr int NJ = VEC ? (32 * (KX / 4) + 63) / 64 : (32 * (KX ? KX : 128) + 63) / 64;
+  uint32_t v[VEC ? 2 * NJ : (NJ + 1) / 2];
+  __device__ __forceinline__ void load(rsrc_t rx, int Tn, int t, bool on, int K, int lane) {
+    if constexpr (VEC) {
+      constexpr int K4 = KX / 4;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int e = lane + 64 * j;
+        const int r = e / K4, c = e - r * K4;
+        const v2i d = __builtin_amdgcn_raw_buffer_load_b64(rx, (on && r < 32) ? (r * Tn * KX + 4 * c) * 2 : kOOB,
+                                                           t * KX * 2, 0);
+        v[2 * j] = (uint32_t)d[0];
+        v[2 * j + 1] = (uint32_t)d[1];
+      }
+    } else {
+      if constexpr (KX > 0) K = KX;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int e = lane + 64 * j;
+        const int r = e / K, k = e - r * K;
+        const uint32_t d = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(
+            rx, (on && r < 32) ? (r * Tn * K + k) * 2 : kOOB, t * K * 2, 0);
+        if (j & 1) v[j >> 1] |= d << 16;
+        else v[j >> 1] = d;
+      }
+    }
+  }
+  __device__ __forceinline__ void to_lds(bf16_t* xb, int LX, int K, int lane) const {
+    if constexpr (VEC) {
+      constexpr int K4 = KX / 4;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int e = lane + 64 * j;
+        const int r = e / K4, c = e - r * K4;
+        if (r < 32) *reinterpret_cast<uint2*>(xb + r * LX + 4 * c) = make_uint2(v[2 * j], v[2 * j + 1]);
+      }
+    } else {
+      if constexpr (KX > 0) K = KX;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int e = lane + 64 * j;
+        const int r = e / K, k = e - r * K;
+        if (r < 32) xb[r * LX + k] = (bf16_t)((j & 1) ? (v[j >> 1] >> 16) : (v[j >> 1] & 0xffffu));
+      }
+    }
+  }
+};
+
+template <int H, int ACT, int KX, bool TAPE, bool TAN>
+__global__ void __launch_bounds__(512)
+lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
+                 const float* __restrict__ U, const bf16_t* __restrict__ ptape, bf16_t* __restrict__ hs,
+                 bf16_t* __restrict__ tape, int B, int Tn, int K_rt) {
+  constexpr int act = ACT;
+  using Geo = Fw4Geo<H, KX>;
+  using KS = KSplit<KX>;
+  using HS = KSplit<H>;
+  constexpr int G = Geo::G, LH = Geo::LH;
+  constexpr int NCW = (H + 15) / 16;
+  static_assert(NCW <= 7, "fwd4: H <= 112");
+  const int K = KX ? KX : K_rt;
+  const int KP = KX ? KS::KP : (K + 31) & ~31, LX = KP + 8, NKX = KX ? KS::NF : KP / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* xb = reinterpret_cast<bf16_t*>(smem);  // [2][32][LX]
+  bf16_t* hb = xb + 2 * 32 * LX;                  // [2][32][LH]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nrb = (B + 31) / 32;
+  // K / H padding columns of both tile buffers stay zero (the data wave writes K columns, the
+  // compute waves write units < H)
+  for (int i = threadIdx.x; i < 2 * 32 * LX; i += 512) xb[i] = 0;
+  for (int i = threadIdx.x; i < 2 * 32 * LH; i += 512) hb[i] = 0;
+  __syncthreads();
+
+  if (wave < NCW) {
+    const int g4 = lane >> 4, c = 16 * wave + (lane & 15);
+    const bool uok = c < H;
+    const int cc_ = uok ? c : H - 1;
+    const int wt32 = __builtin_amdgcn_readfirstlane(wave >> 1);
+    const int lo8 = (32 * (g4 & 1) + (c & 31)) * 8 + 4 * (g4 >> 1);
+    // register fragments: B[k][n = unit] = W[k][q H + c] (input projection), U[k][q H + c];
+    // full 32-wide k-steps (8 values per lane) + an optional 16-wide tail (4 values per lane)
+    constexpr int NKXM = KS::NF, NKH = HS::NF;
+    bf16x8 wf[4][NKXM], uf[4][NKH];
+    bf16x4 wf4[4], uf4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int ks = 0; ks < NKXM; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 32 * ks + 8 * g4 + j;
+          const float v = W[(size_t)min(k, K - 1) * G + q * H + cc_];
+          wf[q][ks][j] = (short)f2bf((uok && k < K) ? v : 0.f);
+        }
+#pragma unroll
+      for (int ks = 0; ks < NKH; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 32 * ks + 8 * g4 + j;
+          const float v = U[(size_t)min(k, H - 1) * G + q * H + cc_];
+          uf[q][ks][j] = (short)f2bf((uok && k < H) ? v : 0.f);
+        }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kx = 32 * NKXM + 4 * g4 + j, kh = 32 * NKH + 4 * g4 + j;
+        const float vx = W[(size_t)min(kx, K - 1) * G + q * H + cc_];
+        const float vh = U[(size_t)min(kh, H - 1) * G + q * H + cc_];
+        wf4[q][j] = (short)f2bf((KS::TAIL && uok && kx < K) ? vx : 0.f);
+        uf4[q][j] = (short)f2bf((HS::TAIL && uok && kh < H) ? vh : 0.f);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    float bq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bq[q] = (!TAN && uok && bias) ? bias[q * H + c] : 0.f;
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      const rsrc_t rt = tape_rsrc(TAPE ? tape : nullptr, rb, nrb, Tn);
+      const rsrc_t rp = tape_rsrc(TAN ? ptape : nullptr, rb, nrb, Tn);
+      float cs[8], cprev[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { cs[e] = 0.f; cprev[e] = 0.f; }
+      Slot8 tg[TAN ? TAPE_SLOTS : 1], tn[TAN ? TAPE_SLOTS : 1];
+      if constexpr (TAN) {
+#pragma unroll
+        for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = ld_slot8(rp, uok, lo8, tape_off(0, wt32) + s * SLOT_ELEMS);
+      }
+      __syncthreads();  // (A)
+      // h_{-1} = 0: this wave's units of buffer 0
+      if (uok)
+        for (int r = 0; r < 32; r += 4) hb[(r + g4) * LH + c] = 0;
+      __syncthreads();  // (B) x_0 staged, h_{-1} zeroed
+      for (int t = 0; t < Tn; ++t) {
+        const bf16_t* xcur = xb + (t & 1) * 32 * LX;
+        const bf16_t* hcur = hb + (t & 1) * 32 * LH;
+        bf16_t* hnext = hb + ((t + 1) & 1) * 32 * LH;
+        if constexpr (TAN) {  // primal tape of the next step (loads only; no store precedes them)
+#pragma unroll
+          for (int s = 0; s < TAPE_SLOTS; ++s)
+            tn[s] = ld_slot8(rp, uok && t + 1 < Tn, lo8, tape_off(min(t + 1, Tn - 1), wt32) + s * SLOT_ELEMS);
+        }
+        f32x4 acc[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { acc[q][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[q][1] = acc[q][0]; }
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const bf16_t* xrow = xcur + (16 * m + (lane & 15)) * LX + 8 * g4;
+#pragma unroll
+          for (int ks = 0; ks < NKXM; ++ks) {
+            if (KX == 0 && ks >= NKX) break;  // (runtime K only; uniform)
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(xrow + 32 * ks);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q][m] = mma16(a, wf[q][ks], acc[q][m]);
+          }
+          if constexpr (KS::TAIL) {  // 16-wide tail: lane holds A[row][32 NF + 4 (lane >> 4) + j]
+            const bf16x4 a = *reinterpret_cast<const bf16x4*>(xcur + (16 * m + (lane & 15)) * LX + 32 * NKXM + 4 * g4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q][m] = mma16k16(a, wf4[q], acc[q][m]);
+          }
+          const bf16_t* hrow = hcur + (16 * m + (lane & 15)) * LH + 8 * g4;
+#pragma unroll
+          for (int ks = 0; ks < NKH; ++ks) {
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(hrow + 32 * ks);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q][m] = mma16(a, uf[q][ks], acc[q][m]);
+          }
+          if constexpr (HS::TAIL) {
+            const bf16x4 a = *reinterpret_cast<const bf16x4*>(hcur + (16 * m + (lane & 15)) * LH + 32 * NKH + 4 * g4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q][m] = mma16k16(a, uf4[q], acc[q][m]);
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          uint32_t pk[TAPE_SLOTS][2];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int e = 4 * m + i, rr = 16 * m + 4 * g4 + i;
+            float v0, v1, v2, v3, v4, hv;
+            if constexpr (!TAN) {
+              const float ig = sigmoidf_(acc[0][m][i] + bq[0]), fg = sigmoidf_(acc[1][m][i] + bq[1]);
+              const float gg = act_f(act, acc[2][m][i] + bq[2]), og = sigmoidf_(acc[3][m][i] + bq[3]);
+              float cn = fg * cs[e] + ig * gg;
+              float h = og * act_f(act, cn);
+              if (!uok) { cn = 0.f; h = 0.f; }
+              cs[e] = cn;
+              v0 = ig; v1 = fg; v2 = gg; v3 = og; v4 = cn; hv = h;
+            } else {
+              const float ig = tg[0].get(m, i), fg = tg[1].get(m, i), gg = tg[2].get(m, i), og = tg[3].get(m, i);
+              const float cv = tg[4].get(m, i);
+              const float idot = ig * (1.f - ig) * acc[0][m][i];
+              const float fdot = fg * (1.f - fg) * acc[1][m][i];
+              const float gdot = act_dy(act, gg) * acc[2][m][i];
+              const float odot = og * (1.f - og) * acc[3][m][i];
+              float cdn = fdot * cprev[e] + fg * cs[e] + idot * gg + ig * gdot;
+              const float ca = act_f(act, cv);
+              float hd = odot * ca + og * act_dy(act, ca) * cdn;
+              if (!uok) { cdn = 0.f; hd = 0.f; }
+              cs[e] = cdn;
+              cprev[e] = cv;
+              v0 = acc[0][m][i]; v1 = acc[1][m][i]; v2 = acc[2][m][i]; v3 = acc[3][m][i]; v4 = cdn; hv = hd;
+            }
+            if (uok) hnext[rr * LH + c] = f2bf(hv);
+            if constexpr (TAPE) {
+              const int h2 = i >> 1;
+              if (i & 1) {
+                pk[0][h2] |= (uint32_t)f2bf(v0) << 16; pk[1][h2] |= (uint32_t)f2bf(v1) << 16;
+                pk[2][h2] |= (uint32_t)f2bf(v2) << 16; pk[3][h2] |= (uint32_t)f2bf(v3) << 16;
+                pk[4][h2] |= (uint32_t)f2bf(v4) << 16;
+              } else {
+                pk[0][h2] = f2bf(v0); pk[1][h2] = f2bf(v1); pk[2][h2] = f2bf(v2); pk[3][h2] = f2bf(v3);
+                pk[4][h2] = f2bf(v4);
+              }
+            }
+          }
+          if constexpr (TAPE) {
+            const int v = uok ? lo8 * 2 : kOOB;
+#pragma unroll
+            for (int s = 0; s < TAPE_SLOTS; ++s) {
+              const v2i d = {(int)pk[s][0], (int)pk[s][1]};
+              __builtin_amdgcn_raw_buffer_store_b64(d, rt, v, (tape_off(t, wt32) + s * SLOT_ELEMS + m * SLOT_HALF) * 2, 0);
+            }
+          }
+        }
+        if constexpr (TAN) {
+#pragma unroll
+          for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = tn[s];
+        }
+        lds_barrier();  // step hand-off
+      }
+      __syncthreads();  // (C) the data wave has stored h_{T-1}
+    }
+  } else if (wave == 7) {
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      const int row0 = rb * 32;
+      const rsrc_t rx = tile_rsrc(x, row0, B, Tn, K), rh = tile_rsrc(hs, row0, B, Tn, H);
+      XTile<KX> xt;
+      xt.load(rx, Tn, 0, true, K, lane);
+      __syncthreads();  // (A)
+      xt.to_lds(xb, LX, K, lane);
+      __syncthreads();  // (B)
+      for (int t = 0; t < Tn; ++t) {
+        xt.load(rx, Tn, t + 1, t + 1 < Tn, K, lane);  // loads first
+        tile8_store_w<H>(hb + (t & 1) * 32 * LH, LH, rh, Tn, t - 1, t > 0, lane);
+        if (t + 1 < Tn) xt.to_lds(xb + ((t + 1) & 1) * 32 * LX, LX, K, lane);
+        lds_barrier();
+      }
+      tile8_store_w<H>(hb + (Tn & 1) * 32 * LH, LH, rh, Tn, Tn - 1, true, lane);
+      __syncthreads();  // (C)
+    }
+  } else {
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      __syncthreads();
+      __syncthreads();
+      for (int t = 0; t < Tn; ++t) lds_barrier();
+      __syncthreads();
+    }
+  }
+}
+
+// ==========================================================================================
 // host side
 // ==========================================================================================
 size_t lstm2_tape_elems(int B, int Tn) { return (size_t)((B + 31) / 32) * Tn * NW2 * TAPE_SLOTS * SLOT_ELEMS; }
@@ -1371,9 +1677,46 @@ static int lstm_tiles() {
   return t;
 }
 
+static int lstm_fwd_version() {  // HFREP_LSTM_FWD=2: the v2 forward / tangent forward (A/B only)
+  static int v = 0;
+  if (!v) {
+    const char* e = getenv("HFREP_LSTM_FWD");
+    v = (e && atoi(e) == 2) ? 2 : 4;
+  }
+  return v;
+}
+static size_t fwd4_smem(int H, int K) {  // generous: the 32-rounded extents (>= the tail-split ones)
+  const int LX = ((K + 31) & ~31) + 8, LH = ((H + 31) / 32) * 32 + 8;
+  return (size_t)(2 * 32 * LX + 2 * 32 * LH) * 2;
+}
+#define HFREP_FWD4_ACT(KXV, TP, TN, ...)                                                          \
+  switch (act) {                                                                                 \
+    case 0: launch(lstm_fwd4_kernel<100, 0, KXV, TP, TN>, __VA_ARGS__); break;                   \
+    case 1: launch(lstm_fwd4_kernel<100, 1, KXV, TP, TN>, __VA_ARGS__); break;                   \
+    default: launch(lstm_fwd4_kernel<100, 2, KXV, TP, TN>, __VA_ARGS__); break;                  \
+  }
+#define HFREP_FWD4_K(TP, TN, ...)                                                                \
+  switch (K) {                                                                                   \
+    case 32: HFREP_FWD4_ACT(32, TP, TN, __VA_ARGS__) break;                                      \
+    case 35: HFREP_FWD4_ACT(35, TP, TN, __VA_ARGS__) break;                                      \
+    case 36: HFREP_FWD4_ACT(36, TP, TN, __VA_ARGS__) break;                                      \
+    case 100: HFREP_FWD4_ACT(100, TP, TN, __VA_ARGS__) break;                                    \
+    default: HFREP_FWD4_ACT(0, TP, TN, __VA_ARGS__) break;                                       \
+  }
+
 void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float* U, void* hs, void* tape, int B, int Tn,
                       int K, int H, int act, hipStream_t s) {
   const bf16_t* xp = (const bf16_t*)x;
+  if (lstm_fwd_version() == 4 && !(lstm_dbg() & 64)) {
+    const int g = persistent_grid(B, 1);
+    const size_t sm = fwd4_smem(H, K);
+    if (tape)
+      HFREP_FWD4_K(true, false, g, 512, sm, s, xp, W, b, U, (const bf16_t*)nullptr, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
+    else
+      HFREP_FWD4_K(false, false, g, 512, sm, s, xp, W, b, U, (const bf16_t*)nullptr, (bf16_t*)hs, (bf16_t*)nullptr, B,
+                   Tn, K)
+    return;
+  }
   if (K == 100 && (lstm_dbg() & 64) && act == 2) {  // diagnostic phase-timer build
     launch(lstm_fwd2_kernel<100, 2, 100, 2, true>, persistent_grid(B, 2), 512, fwd_smem(H, K, 2), s, xp, W, b, U,
            (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg() & ~64);
@@ -1400,6 +1743,12 @@ void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float
 void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const void* tape, void* hds, void* ttape, int B,
                        int Tn, int K, int H, int act, hipStream_t s) {
   const bf16_t* xp = (const bf16_t*)xd;
+  if (lstm_fwd_version() == 4) {
+    const int g = persistent_grid(B, 1);
+    HFREP_FWD4_K(true, true, g, 512, fwd4_smem(H, K), s, xp, W, (const float*)nullptr, U, (const bf16_t*)tape,
+                 (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
+    return;
+  }
   const int g = persistent_grid(B, 1);
   const size_t sm = fwd_smem(H, K, 1);
   if (K == 32) HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 32, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
