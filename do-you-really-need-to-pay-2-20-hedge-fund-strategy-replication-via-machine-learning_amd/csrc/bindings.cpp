@@ -312,7 +312,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm2_tbwd(optional<Tensor> dH, Tenso
 
 // ------------------------------------------------------------------------------------ LayerNorm
 // save == false (no-grad forward): xhat and rstd come back empty and are never written
-std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, double eps, bool save) {
+// pre_lrelu >= 0: LayerNorm(LeakyReLU(x, pre_lrelu)) in one pass (the activation never hits HBM)
+std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, double eps, bool save,
+                                                 double pre_lrelu) {
   CHECK_GPU(x); CHECK_F32(gamma); CHECK_F32(beta);
   const int D = x.size(-1);
   TORCH_CHECK(D <= 256 && gamma.numel() == D && beta.numel() == D, "layernorm: D <= 256 and param sizes");
@@ -324,7 +326,7 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(Tensor x, Tensor gamma, Tensor 
   Tensor rstd = save ? at::empty(rs, x.options().dtype(at::kFloat)) : at::empty({0}, x.options().dtype(at::kFloat));
   hfrep::launch_layernorm_fwd(dt_of(x), x.data_ptr(), gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
                               save ? xhat.data_ptr() : nullptr, save ? rstd.data_ptr<float>() : nullptr, rows, D,
-                              (float)eps, cur_stream(x));
+                              (float)eps, (float)pre_lrelu, cur_stream(x));
   return {y, xhat, rstd};
 }
 
@@ -475,7 +477,8 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstm2_stamps() -> Tensor", &lstm2_stamps);  // no tensor inputs: catch-all kernel
   m.def("lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int act) -> (Tensor, Tensor)");
   m.def("lstm2_tbwd(Tensor? dH, Tensor dHd, Tensor tape, Tensor ttape, Tensor U, int act, Tensor? W=None) -> (Tensor, Tensor, Tensor, Tensor)");
-  m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps, bool save=True) -> (Tensor, Tensor, Tensor)");
+  m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps, bool save=True, float pre_lrelu=-1.0) -> "
+        "(Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, Tensor(a!)? ggamma, Tensor(b!)? gbeta) -> Tensor");
   m.def("gp_coef(Tensor g, float weight) -> (Tensor, Tensor)");
   m.def("im2col_causal(Tensor x, int k, int dil) -> Tensor");

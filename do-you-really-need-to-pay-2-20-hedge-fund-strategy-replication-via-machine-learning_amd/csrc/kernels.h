@@ -83,7 +83,7 @@ void launch_act_bwd(int dt, const void* dy, const void* y, void* dx, int64_t n, 
 void launch_act_tangent_bwd(int dt, const void* dyd, const void* y, const void* zd, void* out, int64_t n, int act,
                             hipStream_t s);
 void launch_layernorm_fwd(int dt, const void* x, const float* gamma, const float* beta, void* y, void* xhat,
-                          float* rstd, int64_t rows, int D, float eps, hipStream_t s);
+                          float* rstd, int64_t rows, int D, float eps, float pre_alpha, hipStream_t s);
 // ggamma/gbeta (either may be null) += column sums via per-workgroup slabs in ws
 // (layernorm_bwd_splits(rows) * 2 * D floats) and a fixed-order reduce: deterministic
 int layernorm_bwd_splits(int64_t rows);

@@ -59,23 +59,30 @@ void launch_act_tangent_bwd(int dt, const void* dyd, const void* y, const void* 
 }
 
 // ------------------------------------------------------------------ LayerNorm (one wave per row)
+// pre_alpha >= 0: the input is first passed through LeakyReLU(pre_alpha) and rounded to T, exactly
+// as a separate activation kernel would store it (the generator's LReLU -> LN pairs)
+template <typename T>
+__device__ __forceinline__ float pre_lrelu(float v, float alpha) {
+  return alpha < 0.f ? v : Cvt<T>::to_f(Cvt<T>::from_f(v >= 0.f ? v : alpha * v));
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, T* __restrict__ y,
                                                             T* __restrict__ xhat, float* __restrict__ rstd_out,
-                                                            int64_t rows, int D, float eps) {
+                                                            int64_t rows, int D, float eps, float pre_alpha) {
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * 4;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += wstride) {
     const T* xr = x + row * D;
     float s = 0.f;
-    for (int j = lane; j < D; j += 64) s += ld_f(xr + j);
+    for (int j = lane; j < D; j += 64) s += pre_lrelu<T>(ld_f(xr + j), pre_alpha);
     const float mu = wave_sum(s) / D;
     float v = 0.f;
-    for (int j = lane; j < D; j += 64) { const float d = ld_f(xr + j) - mu; v += d * d; }
+    for (int j = lane; j < D; j += 64) { const float d = pre_lrelu<T>(ld_f(xr + j), pre_alpha) - mu; v += d * d; }
     const float rstd = rsqrtf(wave_sum(v) / D + eps);
     for (int j = lane; j < D; j += 64) {
-      const float xh = (ld_f(xr + j) - mu) * rstd;
+      const float xh = (pre_lrelu<T>(ld_f(xr + j), pre_alpha) - mu) * rstd;
       if (xhat) st_f(xhat + row * D + j, xh);
       st_f(y + row * D + j, xh * gamma[j] + beta[j]);
     }
@@ -145,11 +152,11 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict_
 // and without SAVE (no-grad forwards: the generator in every critic step) no xhat / rstd traffic.
 // The generic kernel above re-read x three times with 2-byte accesses and always wrote xhat:
 // 146 us per (16384 x 24) x 100 call, ~1.6 TB/s (profiles/r01_buf).
-template <bool SAVE>
+template <bool SAVE, bool PRE>
 __global__ void __launch_bounds__(256) layernorm_fwd_x4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
                                                                const float* __restrict__ beta, bf16_t* __restrict__ y,
                                                                bf16_t* __restrict__ xhat, float* __restrict__ rstd_out,
-                                                               int64_t rows, int D, float eps) {
+                                                               int64_t rows, int D, float eps, float pre_alpha) {
   const int hl = threadIdx.x & 31;
   const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
   if (row >= rows) return;  // a whole half wave (the reductions stay inside a half)
@@ -158,6 +165,10 @@ __global__ void __launch_bounds__(256) layernorm_fwd_x4_kernel(const bf16_t* __r
   const uint2 raw = on ? *reinterpret_cast<const uint2*>(x + row * D + j) : make_uint2(0, 0);
   float v[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u), __uint_as_float(raw.y << 16),
                 __uint_as_float(raw.y & 0xffff0000u)};
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = pre_lrelu<bf16_t>(v[i], pre_alpha);
+  }
   const float mu = halfwave_sum((v[0] + v[1]) + (v[2] + v[3])) / D;
   float q = 0.f;
 #pragma unroll
@@ -177,15 +188,24 @@ __global__ void __launch_bounds__(256) layernorm_fwd_x4_kernel(const bf16_t* __r
 }
 
 void launch_layernorm_fwd(int dt, const void* x, const float* gamma, const float* beta, void* y, void* xhat,
-                          float* rstd, int64_t rows, int D, float eps, hipStream_t s) {
+                          float* rstd, int64_t rows, int D, float eps, float pre_alpha, hipStream_t s) {
   if (dt == DT_BF16 && D <= 128 && D % 4 == 0) {
     const int grid = (int)std::max<int64_t>(1, (rows + 7) / 8);
-    if (xhat)
-      hipLaunchKernelGGL(layernorm_fwd_x4_kernel<true>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, gamma, beta,
-                         (bf16_t*)y, (bf16_t*)xhat, rstd, rows, D, eps);
+    const bf16_t* xp = (const bf16_t*)x;
+    bf16_t* yp = (bf16_t*)y;
+    bf16_t* hp = (bf16_t*)xhat;
+    if (xhat && pre_alpha >= 0.f)
+      hipLaunchKernelGGL((layernorm_fwd_x4_kernel<true, true>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp, hp,
+                         rstd, rows, D, eps, pre_alpha);
+    else if (xhat)
+      hipLaunchKernelGGL((layernorm_fwd_x4_kernel<true, false>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp, hp,
+                         rstd, rows, D, eps, pre_alpha);
+    else if (pre_alpha >= 0.f)
+      hipLaunchKernelGGL((layernorm_fwd_x4_kernel<false, true>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp,
+                         (bf16_t*)nullptr, (float*)nullptr, rows, D, eps, pre_alpha);
     else
-      hipLaunchKernelGGL(layernorm_fwd_x4_kernel<false>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, gamma, beta,
-                         (bf16_t*)y, (bf16_t*)nullptr, (float*)nullptr, rows, D, eps);
+      hipLaunchKernelGGL((layernorm_fwd_x4_kernel<false, false>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp,
+                         (bf16_t*)nullptr, (float*)nullptr, rows, D, eps, pre_alpha);
     return;
   }
   // one row per wave and no grid-stride loop: a wave's row is a dependent load -> reduce -> store
@@ -193,10 +213,10 @@ void launch_layernorm_fwd(int dt, const void* x, const float* gamma, const float
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 1 << 30));
   if (dt == DT_BF16)
     hipLaunchKernelGGL(layernorm_fwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, gamma, beta,
-                       (bf16_t*)y, (bf16_t*)xhat, rstd, rows, D, eps);
+                       (bf16_t*)y, (bf16_t*)xhat, rstd, rows, D, eps, pre_alpha);
   else
     hipLaunchKernelGGL(layernorm_fwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)x, gamma, beta,
-                       (float*)y, (float*)xhat, rstd, rows, D, eps);
+                       (float*)y, (float*)xhat, rstd, rows, D, eps, pre_alpha);
 }
 
 int layernorm_bwd_splits(int64_t rows) { return (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 2048)); }

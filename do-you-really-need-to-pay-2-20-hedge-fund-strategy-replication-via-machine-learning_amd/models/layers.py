@@ -258,6 +258,19 @@ class LayerNormalization(Layer):
         dx = Fn.layer_norm_bwd_(dy, ctx["xhat"], ctx["rstd"], self.p("gamma"), gg, gb)
         return dx if need_dx else None
 
+    @staticmethod
+    def _input(ctx):
+        """The LN input; after a fused LReLU -> LN forward it is rebuilt from the LReLU tape."""
+        if ctx.get("x") is None and "x_pre" in ctx:
+            ctx = dict(ctx, x=R.leaky_relu(ctx["x_pre"], ctx["alpha"]))
+        return ctx
+
+    def etfwd(self, ctx, xd):
+        return super().etfwd(self._input(ctx), xd)
+
+    def etbwd(self, ctx, tctx, dy, dyd, need_dx):
+        return super().etbwd(self._input(ctx), tctx, dy, dyd, need_dx)
+
 
 class LeakyReLU(Layer):
     kind = "leaky_re_lu"
@@ -494,9 +507,23 @@ class Sequential(torch.nn.Module):
     # ---- explicit engine -----------------------------------------------------------------
     def efwd(self, x, save: bool = True):
         tape = []
-        for l in self.layers:
+        i, n = 0, len(self.layers)
+        while i < n:
+            l = self.layers[i]
+            if isinstance(l, LeakyReLU) and i + 1 < n and isinstance(self.layers[i + 1], LayerNormalization):
+                # fused LReLU -> LN pair: one pass, the activation never hits HBM.  The LReLU tape
+                # keeps the pre-activation input: its sign is the output's (alpha > 0), which is
+                # all the LReLU backward / tangent passes read.
+                ln = self.layers[i + 1]
+                y, xhat, rstd = Fn.lrelu_layer_norm_fwd(x, ln.p("gamma"), ln.p("beta"), ln.eps, l.alpha, save)
+                tape.append({"y": x} if save else None)
+                tape.append({"x": None, "x_pre": x, "alpha": l.alpha, "xhat": xhat, "rstd": rstd} if save else None)
+                x = y
+                i += 2
+                continue
             x, ctx = l.efwd(x, save)
             tape.append(ctx)
+            i += 1
         return x, tape
 
     @torch.no_grad()

@@ -143,6 +143,14 @@ def layer_norm_fwd(x, gamma, beta, eps: float, save: bool = True):
     return R.layer_norm_fwd(x, gamma.to(x.dtype), beta.to(x.dtype), eps)
 
 
+def lrelu_layer_norm_fwd(x, gamma, beta, eps: float, alpha: float, save: bool = True):
+    """LayerNorm(LeakyReLU(x)) as one kernel (the generator's LReLU -> LN pairs); the activation
+    output is rounded to x.dtype exactly as the separate activation kernel stores it."""
+    if _nat(x):
+        return _ops().layernorm_fwd(x.contiguous(), gamma, beta, float(eps), bool(save), float(alpha))
+    return layer_norm_fwd(R.leaky_relu(x, alpha), gamma, beta, eps, save)
+
+
 def layer_norm_bwd_(dy, xhat, rstd, gamma, ggamma, gbeta):
     """Returns dx; accumulates dgamma/dbeta into the gradient views."""
     if _nat(dy):

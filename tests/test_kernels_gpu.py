@@ -138,6 +138,14 @@ def test_layernorm(cuda, dt, D):
     # no-grad form: same y, nothing saved
     y2, xh2, rs2 = _ops().layernorm_fwd(x.to(cuda), gamma.to(cuda), beta.to(cuda), 1e-3, False)
     assert torch.equal(y2, y) and xh2.numel() == 0 and rs2.numel() == 0
+    # fused LeakyReLU -> LN == the activation kernel followed by LN, bitwise
+    xa = _ops().act_fwd(x.to(cuda), 3)
+    ya, xha, rsa = _ops().layernorm_fwd(xa, gamma.to(cuda), beta.to(cuda), 1e-3)
+    for save in (True, False):
+        yf, xhf, rsf = _ops().layernorm_fwd(x.to(cuda), gamma.to(cuda), beta.to(cuda), 1e-3, save, 0.2)
+        assert torch.equal(yf, ya)
+        if save:
+            assert torch.equal(xhf, xha) and torch.equal(rsf, rsa)
     dy = torch.randn(37, 11, D, generator=g).to(dt)
     gg, gb = torch.zeros(D, device=cuda), torch.zeros(D, device=cuda)
     dx = _ops().layernorm_bwd_(dy.to(cuda), xhat, rstd, gamma.to(cuda), gg, gb)
