@@ -675,11 +675,16 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
 // (their waits never cover a store).  The two roles run separate loops with the same barrier
 // sequence (3 per row block + 1 per step).
 // ==========================================================================================
-template <int H, int ACT, bool DX>
+template <int H, int ACT, bool DX, bool ST = false>
 __global__ void __launch_bounds__(512)
 lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape, const float* __restrict__ U,
                  bf16_t* __restrict__ dZ, const float* __restrict__ W, bf16_t* __restrict__ dX, int B, int Tn, int K) {
   constexpr int act = ACT;
+  // diagnostic phase timers (ST: HFREP_LSTM_DBG & 128): recurrence waves 0 prefetch issue,
+  // 1 MFMA, 2 gate math, 3 barrier; data waves 4 dH load issue, 5 dz tile stores, 6 dX MFMA +
+  // stores + dH to LDS, 7 barrier
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+  if constexpr (ST) st_last = __builtin_amdgcn_s_memtime();
   using P = MF<bf16_t>;
   constexpr int G = 4 * H, NKG = (G + 15) / 16, LG = NKG * 16 + 8, NKH = (H + 15) / 16, LH = NKH * 16 + 8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -724,12 +729,18 @@ lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
 #pragma unroll
         for (int s = 0; s < 4; ++s) ng[s] = ld_slot(rt, uok && pv, lo, tape_off(max(t - 1, 0), wu) + s * SLOT_ELEMS);
         ncp = ld_slot(rt, uok && t > 1, lo, tape_off(max(t - 2, 0), wu) + 4 * SLOT_ELEMS);
+        HFREP_STAMP(0)
         f32x16 acc = zero16();
         if (t < Tn - 1) {
           const bf16_t* arow = zprev + (lane & 31) * LG;
 #pragma unroll
           for (int ks = 0; ks < NKG; ++ks) acc = P::mma(P::lda(arow, ks, lane), ut[ks], acc);
         }
+        if constexpr (ST) {  // (the MFMA result is consumed below; fence its issue here)
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile("s_nop 0" ::"v"(acc[0]));
+        }
+        HFREP_STAMP(1)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int rr = acc32_row(r, lane);
@@ -748,11 +759,13 @@ lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
             zr[3 * H] = f2bf(dov * og * (1.f - og));
           }
         }
+        HFREP_STAMP(2)
 #pragma unroll
         for (int s = 0; s < 4; ++s) tg[s] = ng[s];
         cc = cp;
         cp = ncp;
         lds_barrier();  // step hand-off
+        HFREP_STAMP(3)
       }
       __syncthreads();  // (C) the data waves have stored dz_0 / dx_0
     }
@@ -777,7 +790,9 @@ lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
       for (int t = Tn - 1; t >= 0; --t) {
         const bf16_t* zprev = zb + ((t + 1) & 1) * 32 * LG;  // dz_{t+1}, final since the last barrier
         const bool live = t < Tn - 1;
+        HFREP_STAMP(4)
         tile16_store<G>(zprev, LG, rz, Tn, t + 1, live, ltid);
+        HFREP_STAMP(5)
         if constexpr (DX) {
           f32x16 ax = zero16();
           if (live && wu * 32 < K) {  // (K = 32: waves 5-7 own no input column)
@@ -790,7 +805,9 @@ lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
         if (t > 0) d0.to_lds(dhb + ((t - 1) & 1) * 32 * LH, LH, ltid);  // dH_{t-1} for the next step
         d0 = d1;
         d1.load(rdh, Tn, t - 3, t > 2, ltid);
+        HFREP_STAMP(6)
         lds_barrier();  // step hand-off
+        HFREP_STAMP(7)
       }
       tile16_store<G>(zb, LG, rz, Tn, 0, true, ltid);
       if constexpr (DX) {
@@ -803,6 +820,13 @@ lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
         store_dx(ax, rdx, Tn, 0, true, nr, K, kc, lane);
       }
       __syncthreads();  // (C)
+    }
+  }
+  if constexpr (ST) {
+    if (lane == 0) {
+      const int slot = blockIdx.x * 8 + wave;
+      if (slot < 4096)
+        for (int i = 0; i < 8; ++i) g_lstm_stamps[slot * 8 + i] = st_acc[i];
     }
   }
 }
@@ -1788,6 +1812,10 @@ void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ
   if (lstm_bwd_version() == 3) {
     const int g = persistent_grid(B, 1);
     const size_t sm = bwd_smem(H, 1);
+    if (dX && act == 2 && (lstm_dbg() & 128)) {  // diagnostic phase-timer build
+      launch(lstm_bwd3_kernel<100, 2, true, true>, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn, K);
+      return;
+    }
     if (dX)
       HFREP_BWD3_LAUNCH(true, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn, K)
     else
