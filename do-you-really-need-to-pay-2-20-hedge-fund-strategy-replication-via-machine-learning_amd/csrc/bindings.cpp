@@ -261,20 +261,42 @@ static int check_dx_W(const optional<Tensor>& W, int H) {
   return (int)W->size(0);
 }
 
-std::tuple<Tensor, Tensor> lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int64_t act, optional<Tensor> W,
-                                     bool need_dz) {
-  CHECK_GPU(dH); CHECK_GPU(tape); same_dt(dH, tape);
-  const int B = dH.size(0), Tn = dH.size(1), H = dH.size(2);
+// Flatten -> Dense(1) critic-head adjoint: dH[b, t, h] = head_d[b] * head_w[t H + h] (head_d (B, 1) bf16,
+// head_w (T H) fp32 = the Dense kernel).  Generated inside the reverse kernels when they support it
+// (hfrep::lstm2_head_fusion), otherwise materialised here with the skinny-dgrad rounding.
+static Tensor head_outer(const Tensor& d, const Tensor& w, int64_t B, int64_t Tn, int64_t H) {
+  return (d.reshape({B, 1, 1}).to(at::kFloat) * w.reshape({1, Tn, H})).to(d.scalar_type());
+}
+static void check_head(const optional<Tensor>& d, const Tensor& w, const Tensor& like, int64_t B, int64_t Tn, int64_t H) {
+  if (!d.has_value()) return;
+  CHECK_GPU(*d); same_dt(*d, like);
+  TORCH_CHECK(d->numel() == B && d->is_contiguous(), "head adjoint: d must be (B, 1) contiguous");
+  CHECK_F32(w);
+  TORCH_CHECK(w.numel() == Tn * H && w.is_contiguous(), "head adjoint: w must hold T * H floats");
+}
+
+std::tuple<Tensor, Tensor> lstm2_bwd(optional<Tensor> dH_, Tensor tape, Tensor U, int64_t act, optional<Tensor> W,
+                                     bool need_dz, optional<Tensor> head_d, optional<Tensor> head_w) {
+  CHECK_GPU(tape);
+  const int H = U.size(0);
+  TORCH_CHECK(dH_.has_value() != (head_d.has_value() && head_w.has_value()), "lstm2_bwd: dH xor (head_d, head_w)");
+  const int B = dH_ ? dH_->size(0) : head_d->size(0);
+  const int Tn = dH_ ? dH_->size(1) : head_w->numel() / H;
   check_lstm_U(U, H);
+  if (dH_) { CHECK_GPU(*dH_); same_dt(*dH_, tape); TORCH_CHECK(dH_->size(2) == H, "dH shape"); }
+  else check_head(head_d, *head_w, tape, B, Tn, H);
   TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstm2_tape_elems(B, Tn), "lstm2_bwd: tape size");
   const int K = check_dx_W(W, H);
-  GUARD(dH);
+  GUARD(tape);
   TORCH_CHECK(need_dz || K, "lstm2_bwd: nothing to compute (need_dz=False without W)");
-  Tensor dZ = at::empty({need_dz ? B : 0, Tn, 4 * H}, dH.options());
-  Tensor dX = at::empty({K ? B : 0, Tn, K}, dH.options());
-  hfrep::launch_lstm2_bwd(dH.data_ptr(), tape.data_ptr(), U.data_ptr<float>(), need_dz ? dZ.data_ptr() : nullptr,
-                          K ? W->data_ptr<float>() : nullptr, K ? dX.data_ptr() : nullptr, K, B, Tn, H, (int)act,
-                          cur_stream(dH));
+  const bool gen = !dH_ && hfrep::lstm2_head_fusion();
+  Tensor dH = dH_ ? *dH_ : (gen ? Tensor() : head_outer(*head_d, *head_w, B, Tn, H));
+  Tensor dZ = at::empty({need_dz ? B : 0, Tn, 4 * H}, tape.options());
+  Tensor dX = at::empty({K ? B : 0, Tn, K}, tape.options());
+  hfrep::launch_lstm2_bwd(gen ? nullptr : dH.data_ptr(), tape.data_ptr(), U.data_ptr<float>(),
+                          need_dz ? dZ.data_ptr() : nullptr, K ? W->data_ptr<float>() : nullptr,
+                          K ? dX.data_ptr() : nullptr, K, B, Tn, H, (int)act, cur_stream(tape),
+                          gen ? head_d->data_ptr() : nullptr, gen ? head_w->data_ptr<float>() : nullptr);
   return {dZ, dX};
 }
 
@@ -292,21 +314,46 @@ std::tuple<Tensor, Tensor> lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape
   return {hds, ttape};
 }
 
-std::tuple<Tensor, Tensor, Tensor, Tensor> lstm2_tbwd(optional<Tensor> dH, Tensor dHd, Tensor tape, Tensor ttape,
-                                                      Tensor U, int64_t act, optional<Tensor> W) {
-  CHECK_GPU(dHd); CHECK_GPU(tape); CHECK_GPU(ttape); same_dt(dHd, tape); same_dt(dHd, ttape);
-  if (dH.has_value()) { CHECK_GPU(*dH); same_dt(*dH, dHd); TORCH_CHECK(dH->sizes() == dHd.sizes(), "dH shape"); }
-  const int B = dHd.size(0), Tn = dHd.size(1), H = dHd.size(2);
+// dH / dHd: tensors, or (with head_w) the outer products head_d / head_dd x head_w (either may be
+// absent = zeros); the two forms are not mixed in one call
+std::tuple<Tensor, Tensor, Tensor, Tensor> lstm2_tbwd(optional<Tensor> dH, optional<Tensor> dHd_, Tensor tape,
+                                                      Tensor ttape, Tensor U, int64_t act, optional<Tensor> W,
+                                                      optional<Tensor> head_d, optional<Tensor> head_dd,
+                                                      optional<Tensor> head_w) {
+  CHECK_GPU(tape); CHECK_GPU(ttape); same_dt(tape, ttape);
+  const int H = U.size(0);
+  const bool head = head_w.has_value();
+  TORCH_CHECK(head ? (!dH && !dHd_ && (head_d || head_dd)) : (dHd_.has_value() && !head_d && !head_dd),
+              "lstm2_tbwd: (dH?, dHd) tensors xor (head_d?, head_dd?, head_w)");
+  const int B = head ? (head_d ? head_d->size(0) : head_dd->size(0)) : dHd_->size(0);
+  const int Tn = head ? head_w->numel() / H : dHd_->size(1);
   check_lstm_U(U, H);
+  if (!head) {
+    CHECK_GPU(*dHd_); same_dt(*dHd_, tape);
+    if (dH.has_value()) { CHECK_GPU(*dH); same_dt(*dH, *dHd_); TORCH_CHECK(dH->sizes() == dHd_->sizes(), "dH shape"); }
+  } else {
+    check_head(head_d, *head_w, tape, B, Tn, H);
+    check_head(head_dd, *head_w, tape, B, Tn, H);
+  }
   TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstm2_tape_elems(B, Tn) && ttape.numel() == tape.numel(), "tape size");
-  GUARD(dHd);
+  GUARD(tape);
   const int K = check_dx_W(W, H);
-  Tensor dZ = at::empty({B, Tn, 4 * H}, dHd.options()), dZd = at::empty({B, Tn, 4 * H}, dHd.options());
-  Tensor dX = at::empty({K ? B : 0, Tn, K}, dHd.options()), dXd = at::empty({K ? B : 0, Tn, K}, dHd.options());
-  hfrep::launch_lstm2_tbwd(ptr_or_null(dH), dHd.data_ptr(), tape.data_ptr(), ttape.data_ptr(), U.data_ptr<float>(),
-                           dZ.data_ptr(), dZd.data_ptr(), K ? W->data_ptr<float>() : nullptr,
-                           K ? dX.data_ptr() : nullptr, K ? dXd.data_ptr() : nullptr, K, B, Tn, H, (int)act,
-                           cur_stream(dHd));
+  const bool gen = head && hfrep::lstm2_head_fusion();
+  optional<Tensor> dHm = dH;
+  Tensor dHd;
+  if (head && !gen) {  // materialise for the v2 kernels
+    if (head_d) dHm = head_outer(*head_d, *head_w, B, Tn, H);
+    dHd = head_dd ? head_outer(*head_dd, *head_w, B, Tn, H) : at::zeros({B, Tn, H}, tape.options());
+  } else if (!head) {
+    dHd = *dHd_;
+  }
+  Tensor dZ = at::empty({B, Tn, 4 * H}, tape.options()), dZd = at::empty({B, Tn, 4 * H}, tape.options());
+  Tensor dX = at::empty({K ? B : 0, Tn, K}, tape.options()), dXd = at::empty({K ? B : 0, Tn, K}, tape.options());
+  hfrep::launch_lstm2_tbwd(gen ? nullptr : ptr_or_null(dHm), gen ? nullptr : dHd.data_ptr(), tape.data_ptr(),
+                           ttape.data_ptr(), U.data_ptr<float>(), dZ.data_ptr(), dZd.data_ptr(),
+                           K ? W->data_ptr<float>() : nullptr, K ? dX.data_ptr() : nullptr, K ? dXd.data_ptr() : nullptr,
+                           K, B, Tn, H, (int)act, cur_stream(tape), gen ? ptr_or_null(head_d) : nullptr,
+                           gen ? ptr_or_null(head_dd) : nullptr, gen ? head_w->data_ptr<float>() : nullptr);
   return {dZ, dZd, dX, dXd};
 }
 
@@ -473,10 +520,12 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstm_tfwd(Tensor dzx, Tensor gates, Tensor cs, Tensor U, int act) -> (Tensor, Tensor, Tensor)");
   m.def("lstm_tbwd(Tensor? dH, Tensor dHd, Tensor gates, Tensor cs, Tensor zds, Tensor cds, Tensor U, int act) -> (Tensor, Tensor)");
   m.def("lstm2_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
-  m.def("lstm2_bwd(Tensor dH, Tensor tape, Tensor U, int act, Tensor? W=None, bool need_dz=True) -> (Tensor, Tensor)");
+  m.def("lstm2_bwd(Tensor? dH, Tensor tape, Tensor U, int act, Tensor? W=None, bool need_dz=True, Tensor? head_d=None, "
+        "Tensor? head_w=None) -> (Tensor, Tensor)");
   m.def("lstm2_stamps() -> Tensor", &lstm2_stamps);  // no tensor inputs: catch-all kernel
   m.def("lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int act) -> (Tensor, Tensor)");
-  m.def("lstm2_tbwd(Tensor? dH, Tensor dHd, Tensor tape, Tensor ttape, Tensor U, int act, Tensor? W=None) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("lstm2_tbwd(Tensor? dH, Tensor? dHd, Tensor tape, Tensor ttape, Tensor U, int act, Tensor? W=None, "
+        "Tensor? head_d=None, Tensor? head_dd=None, Tensor? head_w=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps, bool save=True, float pre_lrelu=-1.0) -> "
         "(Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, Tensor(a!)? ggamma, Tensor(b!)? gbeta) -> Tensor");

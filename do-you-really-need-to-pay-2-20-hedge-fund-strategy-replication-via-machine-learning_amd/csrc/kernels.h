@@ -29,11 +29,16 @@ void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float
 void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const void* tape, void* hds, void* ttape, int B,
                        int Tn, int K, int H, int act, hipStream_t s);
 // W / dX non-null: the input gradient dX = dZ W^T (K columns) is produced by the same launch
+// head_d / head_dd + hw: dH (dHdot) = d[b] * hw[t H + h] generated in-kernel (Flatten -> Dense(1) head
+// adjoint; needs lstm2_head_fusion()); otherwise dH / dHd tensors (nullptr = zeros)
+bool lstm2_head_fusion();
 void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, const float* W, void* dX, int K,
-                      int B, int Tn, int H, int act, hipStream_t s);
+                      int B, int Tn, int H, int act, hipStream_t s, const void* head_d = nullptr,
+                      const float* hw = nullptr);
 void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const void* ttape, const float* U, void* dZ,
                        void* dZd, const float* W, void* dX, void* dXd, int K, int B, int Tn, int H, int act,
-                       hipStream_t s);
+                       hipStream_t s, const void* head_d = nullptr, const void* head_dd = nullptr,
+                       const float* hw = nullptr);
 
 // ---- gemm.hip ----
 // C[M,N] = act(A[M,K] . op(W) + bias);  op(W) = W (K,N) or W^T when w_trans (W stored (N,K)).

@@ -233,6 +233,64 @@ struct Tile8 {
     }
   }
 };
+// Source of the dH (dHdot) tiles of the reverse kernels, moved by NT threads in 8-byte chunks:
+// GEN = false: a row-major (B, T, W) tensor (`rs` = its tile descriptor);
+// GEN = true: the outer product d[b] * w[t W + h] of a Flatten -> Dense(1) critic head, generated
+// in-kernel (`rs` = descriptor over the tile's rows of d (B, 1), `rw` over w (T W floats)), so the
+// head's (B, T, W) input adjoint is never written to HBM nor read back.  The product is rounded
+// exactly as the skinny dgrad kernel rounds it (bf16(float(d) * w)).
+template <int W, int NT, bool GEN>
+struct TileSrc {
+  static constexpr int CPR = W / 4, NJ = (32 * CPR + NT - 1) / NT;
+  static_assert(W % 4 == 0, "8-byte chunks");
+  v2i v[GEN ? 1 : NJ];
+  uint32_t d[GEN ? NJ : 1];
+  float4 wv[GEN ? NJ : 1];
+  __device__ __forceinline__ void load(rsrc_t rs, rsrc_t rw, int Tn, int t, bool on, int tid) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int e = tid + NT * j;
+      const int r = e / CPR, c = e - r * CPR;
+      const bool ok = on && r < 32;
+      if constexpr (!GEN) {
+        v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, ok ? (r * Tn * W + 4 * c) * 2 : kOOB, t * W * 2, 0);
+      } else {
+        d[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, ok ? r * 2 : kOOB, 0, 0);
+        wv[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, ok ? (t * W + 4 * c) * 4 : kOOB, 0, 0));
+      }
+    }
+  }
+  __device__ __forceinline__ void to_lds(bf16_t* buf, int LD, int tid) const {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int e = tid + NT * j;
+      const int r = e / CPR, c = e - r * CPR;
+      if (r < 32) {
+        v2i o;
+        if constexpr (!GEN) {
+          o = v[j];
+        } else {
+          const float dv = __uint_as_float(d[j] << 16);
+          o = v2i{(int)pk2(dv * wv[j].x, dv * wv[j].y), (int)pk2(dv * wv[j].z, dv * wv[j].w)};
+        }
+        *reinterpret_cast<v2i*>(buf + r * LD + 4 * c) = o;
+      }
+    }
+  }
+};
+// tile descriptors of a dH source: (tensor tile, unused) or (rows of d, all of w)
+template <int W, bool GEN>
+__device__ __forceinline__ void head_rsrc(rsrc_t& rs, rsrc_t& rw, const bf16_t* dH, const bf16_t* hd, const float* hw,
+                                          int row0, int B, int Tn) {
+  if constexpr (GEN) {
+    rs = tile_rsrc(hd, row0, B, 1, 1);
+    rw = make_rsrc(hw, hw ? Tn * W * 4 : 0);
+  } else {
+    rs = tile_rsrc(dH, row0, B, Tn, W);
+    rw = make_rsrc(nullptr, 0);
+  }
+}
+
 template <int W>
 __device__ __forceinline__ void tile8_store(const bf16_t* buf, int LD, rsrc_t rd, int Tn, int t, bool on, int ltid) {
   constexpr int CPR = W / 4, NJ = (32 * CPR + 255) / 256;
@@ -675,10 +733,11 @@ lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
 // (their waits never cover a store).  The two roles run separate loops with the same barrier
 // sequence (3 per row block + 1 per step).
 // ==========================================================================================
-template <int H, int ACT, bool DX, bool ST = false>
+template <int H, int ACT, bool DX, bool GEN = false, bool ST = false>
 __global__ void __launch_bounds__(512)
 lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape, const float* __restrict__ U,
-                 bf16_t* __restrict__ dZ, const float* __restrict__ W, bf16_t* __restrict__ dX, int B, int Tn, int K) {
+                 bf16_t* __restrict__ dZ, const float* __restrict__ W, bf16_t* __restrict__ dX, int B, int Tn, int K,
+                 const bf16_t* __restrict__ hd, const float* __restrict__ hw) {
   constexpr int act = ACT;
   // diagnostic phase timers (ST: HFREP_LSTM_DBG & 128): recurrence waves 0 prefetch issue,
   // 1 MFMA, 2 gate math, 3 barrier; data waves 4 dH load issue, 5 dz tile stores, 6 dX MFMA +
@@ -777,15 +836,17 @@ lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
     for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
       const int row0 = rb * 32;
       const int nr = min(32, B - row0);
-      const rsrc_t rdh = tile_rsrc(dH, row0, B, Tn, H), rz = tile_rsrc(dZ, row0, B, Tn, G);
+      const rsrc_t rz = tile_rsrc(dZ, row0, B, Tn, G);
       const rsrc_t rdx = tile_rsrc(DX ? dX : nullptr, row0, B, Tn, DX ? K : 1);
-      Tile8<H> d0, d1;  // dH_{t-1}, dH_{t-2} in flight (two steps of prefetch)
-      d0.load(rdh, Tn, Tn - 1, true, ltid);
-      d1.load(rdh, Tn, Tn - 2, Tn > 1, ltid);
+      rsrc_t rdh, rhw;
+      head_rsrc<H, GEN>(rdh, rhw, dH, hd, hw, row0, B, Tn);
+      TileSrc<H, 256, GEN> d0, d1;  // dH_{t-1}, dH_{t-2} in flight (two steps of prefetch)
+      d0.load(rdh, rhw, Tn, Tn - 1, true, ltid);
+      d1.load(rdh, rhw, Tn, Tn - 2, Tn > 1, ltid);
       __syncthreads();  // (A)
       d0.to_lds(dhb + ((Tn - 1) & 1) * 32 * LH, LH, ltid);
       d0 = d1;
-      d1.load(rdh, Tn, Tn - 3, Tn > 2, ltid);
+      d1.load(rdh, rhw, Tn, Tn - 3, Tn > 2, ltid);
       __syncthreads();  // (B)
       for (int t = Tn - 1; t >= 0; --t) {
         const bf16_t* zprev = zb + ((t + 1) & 1) * 32 * LG;  // dz_{t+1}, final since the last barrier
@@ -804,7 +865,7 @@ lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
         }
         if (t > 0) d0.to_lds(dhb + ((t - 1) & 1) * 32 * LH, LH, ltid);  // dH_{t-1} for the next step
         d0 = d1;
-        d1.load(rdh, Tn, t - 3, t > 2, ltid);
+        d1.load(rdh, rhw, Tn, t - 3, t > 2, ltid);
         HFREP_STAMP(6)
         lds_barrier();  // step hand-off
         HFREP_STAMP(7)
@@ -1117,12 +1178,13 @@ struct Tb4Geo {
   static constexpr size_t smem = (size_t)(4 * 32 * LG + 4 * 32 * LH) * 2;
 };
 
-template <int H, int ACT, bool DX>
+template <int H, int ACT, bool DX, bool GEN = false>
 __global__ void __launch_bounds__(512)
 lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd, const bf16_t* __restrict__ tape,
                   const bf16_t* __restrict__ ttape, const float* __restrict__ U, bf16_t* __restrict__ dZ,
                   bf16_t* __restrict__ dZd, const float* __restrict__ W, bf16_t* __restrict__ dX,
-                  bf16_t* __restrict__ dXd, int B, int Tn, int K) {
+                  bf16_t* __restrict__ dXd, int B, int Tn, int K, const bf16_t* __restrict__ hd,
+                  const bf16_t* __restrict__ hdd, const float* __restrict__ hw) {
   constexpr int act = ACT;
   using Geo = Tb4Geo<H>;
   constexpr int G = Geo::G, NK = Geo::NK, LG = Geo::LG, LH = Geo::LH;
@@ -1296,11 +1358,13 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
     // ---------------- data wave ----------------
     for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
       const int row0 = rb * 32;
-      const rsrc_t rdh = tile_rsrc(dH, row0, B, Tn, H), rdhd = tile_rsrc(dHd, row0, B, Tn, H);
       const rsrc_t rz = tile_rsrc(dZ, row0, B, Tn, G), rzd = tile_rsrc(dZd, row0, B, Tn, G);
-      Tile8w<H> a, ad;
-      a.load(rdh, Tn, Tn - 1, true, lane);
-      ad.load(rdhd, Tn, Tn - 1, true, lane);
+      rsrc_t rdh, rdhd, rhw;
+      head_rsrc<H, GEN>(rdh, rhw, dH, hd, hw, row0, B, Tn);
+      head_rsrc<H, GEN>(rdhd, rhw, dHd, hdd, hw, row0, B, Tn);
+      TileSrc<H, 64, GEN> a, ad;
+      a.load(rdh, rhw, Tn, Tn - 1, true, lane);
+      ad.load(rdhd, rhw, Tn, Tn - 1, true, lane);
       __syncthreads();  // (A)
       a.to_lds(dhb + ((Tn - 1) & 1) * 32 * LH, LH, lane);
       ad.to_lds(dhdb + ((Tn - 1) & 1) * 32 * LH, LH, lane);
@@ -1308,8 +1372,8 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
       for (int t = Tn - 1; t >= 0; --t) {
         const int nb = (t + 1) & 1;
         const bool pv = t > 0, live = t < Tn - 1;
-        a.load(rdh, Tn, t - 1, pv, lane);  // loads first: their wait covers no store of this step
-        ad.load(rdhd, Tn, t - 1, pv, lane);
+        a.load(rdh, rhw, Tn, t - 1, pv, lane);  // loads first: their wait covers no store of this step
+        ad.load(rdhd, rhw, Tn, t - 1, pv, lane);
         tile16_store_w<G>(zb + nb * 32 * LG, LG, rz, Tn, t + 1, live, lane);
         tile16_store_w<G>(zdb + nb * 32 * LG, LG, rzd, Tn, t + 1, live, lane);
         if (pv) {
@@ -1782,12 +1846,14 @@ void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const voi
   else HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 0, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
 }
 
-#define HFREP_BWD3_LAUNCH(DXV, ...)                                                            \
+#define HFREP_BWD3_ACT(DXV, GV, ...)                                                           \
   switch (act) {                                                                                 \
-    case 0: launch(lstm_bwd3_kernel<100, 0, DXV>, __VA_ARGS__); break;                           \
-    case 1: launch(lstm_bwd3_kernel<100, 1, DXV>, __VA_ARGS__); break;                           \
-    default: launch(lstm_bwd3_kernel<100, 2, DXV>, __VA_ARGS__); break;                          \
+    case 0: launch(lstm_bwd3_kernel<100, 0, DXV, GV>, __VA_ARGS__); break;                       \
+    case 1: launch(lstm_bwd3_kernel<100, 1, DXV, GV>, __VA_ARGS__); break;                       \
+    default: launch(lstm_bwd3_kernel<100, 2, DXV, GV>, __VA_ARGS__); break;                      \
   }
+#define HFREP_BWD3_LAUNCH(DXV, ...)                                                            \
+  if (hw) HFREP_BWD3_ACT(DXV, true, __VA_ARGS__) else HFREP_BWD3_ACT(DXV, false, __VA_ARGS__)
 
 #define HFREP_BWD_LAUNCH(KERNEL, TL, DXV, ...)                                                  \
   switch (act) {                                                                                 \
@@ -1796,6 +1862,7 @@ void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const voi
     default: launch(KERNEL<100, 2, TL, DXV>, __VA_ARGS__); break;                                \
   }
 
+static int lstm_tbwd_version();
 static int lstm_bwd_version() {  // HFREP_LSTM_BWD=2: the single-role v2 BPTT (A/B only)
   static int v = 0;
   if (!v) {
@@ -1805,21 +1872,26 @@ static int lstm_bwd_version() {  // HFREP_LSTM_BWD=2: the single-role v2 BPTT (A
   return v;
 }
 
+bool lstm2_head_fusion() { return lstm_bwd_version() == 3 && lstm_tbwd_version() == 4; }
+
 void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, const float* W, void* dX, int K,
-                      int B, int Tn, int H, int act, hipStream_t s) {
+                      int B, int Tn, int H, int act, hipStream_t s, const void* head_d, const float* hw) {
   const bf16_t* dh = (const bf16_t*)dH;
   const bf16_t* tp = (const bf16_t*)tape;
+  const bf16_t* hd = (const bf16_t*)head_d;
   if (lstm_bwd_version() == 3) {
     const int g = persistent_grid(B, 1);
     const size_t sm = bwd_smem(H, 1);
-    if (dX && act == 2 && (lstm_dbg() & 128)) {  // diagnostic phase-timer build
-      launch(lstm_bwd3_kernel<100, 2, true, true>, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn, K);
+    if (dX && act == 2 && !hw && (lstm_dbg() & 128)) {  // diagnostic phase-timer build
+      launch(lstm_bwd3_kernel<100, 2, true, false, true>, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn,
+             K, hd, hw);
       return;
     }
     if (dX)
-      HFREP_BWD3_LAUNCH(true, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn, K)
+      HFREP_BWD3_LAUNCH(true, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn, K, hd, hw)
     else
-      HFREP_BWD3_LAUNCH(false, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, (const float*)nullptr, (bf16_t*)nullptr, B, Tn, 0)
+      HFREP_BWD3_LAUNCH(false, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, (const float*)nullptr, (bf16_t*)nullptr, B, Tn, 0,
+                        hd, hw)
     return;
   }
   if (dX)  // fused input gradient: U^T and W^T fragments in registers -> one row tile per workgroup
@@ -1838,26 +1910,31 @@ static int lstm_tbwd_version() {  // HFREP_LSTM_TBWD=2: the v2 tangent reverse (
   return v;
 }
 
-#define HFREP_TBWD4_LAUNCH(DXV, ...)                                                           \
+#define HFREP_TBWD4_ACT(DXV, GV, ...)                                                          \
   switch (act) {                                                                                 \
-    case 0: launch(lstm_tbwd4_kernel<100, 0, DXV>, __VA_ARGS__); break;                          \
-    case 1: launch(lstm_tbwd4_kernel<100, 1, DXV>, __VA_ARGS__); break;                          \
-    default: launch(lstm_tbwd4_kernel<100, 2, DXV>, __VA_ARGS__); break;                         \
+    case 0: launch(lstm_tbwd4_kernel<100, 0, DXV, GV>, __VA_ARGS__); break;                      \
+    case 1: launch(lstm_tbwd4_kernel<100, 1, DXV, GV>, __VA_ARGS__); break;                      \
+    default: launch(lstm_tbwd4_kernel<100, 2, DXV, GV>, __VA_ARGS__); break;                     \
   }
+#define HFREP_TBWD4_LAUNCH(DXV, ...)                                                           \
+  if (hw) HFREP_TBWD4_ACT(DXV, true, __VA_ARGS__) else HFREP_TBWD4_ACT(DXV, false, __VA_ARGS__)
 
 void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const void* ttape, const float* U, void* dZ,
                        void* dZd, const float* W, void* dX, void* dXd, int K, int B, int Tn, int H, int act,
-                       hipStream_t s) {
+                       hipStream_t s, const void* head_d, const void* head_dd, const float* hw) {
+  const bf16_t* hd = (const bf16_t*)head_d;
+  const bf16_t* hdd = (const bf16_t*)head_dd;
   if (lstm_tbwd_version() == 4) {
     const int g = persistent_grid(B, 1);
     const size_t sm = Tb4Geo<100>::smem;
     if (dX)
       HFREP_TBWD4_LAUNCH(true, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
-                         (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, W, (bf16_t*)dX, (bf16_t*)dXd, B, Tn, K)
+                         (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, W, (bf16_t*)dX, (bf16_t*)dXd, B, Tn, K, hd,
+                         hdd, hw)
     else
       HFREP_TBWD4_LAUNCH(false, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
                          (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, (const float*)nullptr, (bf16_t*)nullptr,
-                         (bf16_t*)nullptr, B, Tn, 0)
+                         (bf16_t*)nullptr, B, Tn, 0, hd, hdd, hw)
     return;
   }
   if (dX)

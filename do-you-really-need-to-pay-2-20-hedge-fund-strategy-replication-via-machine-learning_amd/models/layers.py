@@ -158,11 +158,18 @@ class Dense(Layer):
         y = Fn.linear(x, self.p("kernel"), self.p("bias") if self.use_bias else None, self.act_code)
         return y, ({"x": x, "y": y} if save else None)
 
+    def _dgrad(self, dz):
+        # a Dense(1) head hands its input adjoint on as a lazy outer product (OuterAdjoint): the
+        # LSTM reverse kernels generate it in-kernel, anything else materialises it
+        if self.units == 1 and dz.dim() == 2 and Fn.outer_adjoint_ok(dz):  # (B, 1): a Flatten head
+            return Fn.OuterAdjoint(dz, self.p("kernel"))
+        return Fn.linear_dgrad(dz, self.p("kernel"))
+
     def ebwd(self, ctx, dy, need_dx, wgrad=True):
         dz = Fn.act_backward(dy, ctx["y"], self.act_code)
         if wgrad:
             Fn.linear_wgrad_(ctx["x"], dz, self.g("kernel"), self.g("bias") if self.use_bias else None)
-        return Fn.linear_dgrad(dz, self.p("kernel")) if need_dx else None
+        return self._dgrad(dz) if need_dx else None
 
     def etfwd(self, ctx, xd):
         zd = Fn.linear(xd, self.p("kernel"), None, 0)
@@ -176,11 +183,14 @@ class Dense(Layer):
         Fn.linear_wgrad_(tctx["xd"], dzd, self.g("kernel"), None)
         if not need_dx:
             return None, None
-        return Fn.linear_dgrad(dz, self.p("kernel")), Fn.linear_dgrad(dzd, self.p("kernel"))
+        # dy is None (no primal seed) with a linear head: dz == 0, so dx is the zero adjoint (None)
+        dx = None if (dy is None and self.act_code in (0, 3, 4)) else self._dgrad(dz)
+        return dx, self._dgrad(dzd)
 
 
 class LSTM(Layer):
     kind = "lstm"
+    accepts_outer = True  # Fn.lstm_layer_bwd / _tbwd consume OuterAdjoint seeds
 
     def __init__(self, units: int, activation="tanh", return_sequences: bool = True):
         super().__init__()
@@ -304,6 +314,7 @@ class LeakyReLU(Layer):
 
 class Flatten(Layer):
     kind = "flatten"
+    accepts_outer = True  # reshape of a lazy OuterAdjoint stays lazy
 
     def build(self, in_shape):
         self.in_shape = tuple(in_shape)
@@ -530,14 +541,21 @@ class Sequential(torch.nn.Module):
     def predict(self, x):
         return self.efwd(x, save=False)[0]
 
+    @staticmethod
+    def _adj(layer, dy):
+        if isinstance(dy, Fn.OuterAdjoint) and not getattr(layer, "accepts_outer", False):
+            return dy.materialize()
+        return dy
+
     def ebwd(self, tape, dy, need_dx: bool = False, wgrad: bool = True, hook=None):
         """Reverse pass; ``hook(i)`` runs after layer i (its gradients are then final)."""
         for i in range(len(self.layers) - 1, -1, -1):
             need = need_dx or i > 0
-            dy = self.layers[i].ebwd(tape[i], dy, need, wgrad)
+            layer = self.layers[i]
+            dy = layer.ebwd(tape[i], self._adj(layer, dy), need, wgrad)
             if hook is not None:
                 hook(i)
-        return dy
+        return Fn._mat(dy)
 
     def etfwd(self, tape, xd):
         ttape = []
@@ -549,10 +567,11 @@ class Sequential(torch.nn.Module):
     def etbwd(self, tape, ttape, dy, dyd, need_dx: bool = False, hook=None):
         for i in range(len(self.layers) - 1, -1, -1):
             need = need_dx or i > 0
-            dy, dyd = self.layers[i].etbwd(tape[i], ttape[i], dy, dyd, need)
+            layer = self.layers[i]
+            dy, dyd = layer.etbwd(tape[i], ttape[i], self._adj(layer, dy), self._adj(layer, dyd), need)
             if hook is not None:
                 hook(i)
-        return dy, dyd
+        return Fn._mat(dy), Fn._mat(dyd)
 
     def grad_buckets(self, n: int = 2) -> list[tuple[int, int, int]]:
         """Split the flat gradient buffer at layer boundaries into <= n buckets of similar size.

@@ -226,16 +226,48 @@ def lstm_layer_fwd(x, W, b, U, act: int, save: bool):
     return hs, ((gates, cs) if save else None)
 
 
+class OuterAdjoint:
+    """Lazy input adjoint of a linear Dense(1) head: dX[b, j] = d[b, 0] * w[j, 0], viewed with
+    ``shape`` (after Flatten: (B, T, H)).  The bf16 LSTM reverse kernels generate it inside the
+    kernel (csrc/lstm2.hip TileSrc), so the (B, T*H) head adjoint never exists in HBM; every other
+    consumer calls :meth:`materialize` (the skinny dgrad kernel, same rounding)."""
+
+    def __init__(self, d: torch.Tensor, w: torch.Tensor, shape=None):
+        self.d, self.w = d, w
+        self.shape = tuple(shape) if shape is not None else (d.shape[0], w.shape[0])
+
+    def reshape(self, *shape):
+        shape = tuple(shape[0]) if len(shape) == 1 and not isinstance(shape[0], int) else tuple(shape)
+        return OuterAdjoint(self.d, self.w, shape)
+
+    def materialize(self) -> torch.Tensor:
+        return linear_dgrad(self.d, self.w).reshape(self.shape)
+
+
+def outer_adjoint_ok(dz: torch.Tensor) -> bool:
+    """Whether a Dense(1) head may hand its input adjoint on lazily (bf16 on the native path)."""
+    return dz.dtype == torch.bfloat16 and _nat(dz) and not _native.fallback_allowed()
+
+
+def _mat(a):
+    return a.materialize() if isinstance(a, OuterAdjoint) else a
+
+
 def lstm_layer_bwd(dH, tape, U, act: int, W=None, need_dz: bool = True):
     """dZ = dL/d(x W + b + h U) for every step; with ``W`` also the input gradient dX = dZ W^T,
     returned as ``(dZ, dX)`` (the v2 kernel produces it in the same launch, csrc/lstm2.hip).
     ``need_dz=False`` (only dX wanted, e.g. the gradient penalty's dD/dx) lets the v2 kernel skip
     writing dZ to HBM; the returned dZ is then None."""
     if isinstance(tape, torch.Tensor):
-        dZ, dX = _ops().lstm2_bwd(dH.contiguous(), tape, U, int(act), W, bool(need_dz or W is None))
+        nd = bool(need_dz or W is None)
+        if isinstance(dH, OuterAdjoint):  # head adjoint generated in-kernel
+            dZ, dX = _ops().lstm2_bwd(None, tape, U, int(act), W, nd, dH.d.contiguous(), dH.w.reshape(-1).contiguous())
+        else:
+            dZ, dX = _ops().lstm2_bwd(dH.contiguous(), tape, U, int(act), W, nd)
         if W is not None and not need_dz:
             dZ = None
         return dZ if W is None else (dZ, dX)
+    dH = _mat(dH)
     gates, cs = tape
     dZ = lstm_seq_bwd(dH, gates, cs, U, act)
     return dZ if W is None else (dZ, linear_dgrad(dZ, W))
@@ -272,9 +304,18 @@ def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None, impl: int = 
 def lstm_layer_tbwd(dH, dHd, tape, ttape, U, act: int, W=None):
     """(dZ, dZd) of the reverse-over-tangent pass; with ``W`` also (dX, dXd) = (dZ W^T, dZd W^T)."""
     if isinstance(tape, torch.Tensor):
-        dZ, dZd, dX, dXd = _ops().lstm2_tbwd(None if dH is None else dH.contiguous(), dHd.contiguous(), tape, ttape,
-                                             U, int(act), W)
+        heads = [a for a in (dH, dHd) if isinstance(a, OuterAdjoint)]
+        if heads and all(a is None or (isinstance(a, OuterAdjoint) and a.w is heads[0].w) for a in (dH, dHd)):
+            w = heads[0].w.reshape(-1).contiguous()
+            dZ, dZd, dX, dXd = _ops().lstm2_tbwd(None, None, tape, ttape, U, int(act), W,
+                                                 None if dH is None else dH.d.contiguous(),
+                                                 None if dHd is None else dHd.d.contiguous(), w)
+        else:
+            dH, dHd = _mat(dH), _mat(dHd)
+            dZ, dZd, dX, dXd = _ops().lstm2_tbwd(None if dH is None else dH.contiguous(), dHd.contiguous(), tape,
+                                                 ttape, U, int(act), W)
         return (dZ, dZd) if W is None else (dZ, dZd, dX, dXd)
+    dH, dHd = _mat(dH), _mat(dHd)
     gates, cs = tape
     zds, cds = ttape
     if dH is None:

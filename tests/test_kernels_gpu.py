@@ -489,3 +489,36 @@ def test_lstm2_persistent_multi_pass(cuda):
     _close(dZ2, rz, torch.bfloat16)
     _close(dZd2, rzd, torch.bfloat16)
     _close(dXd2, rzd @ W.double().t(), torch.bfloat16, scale=(rzd.abs() @ W.double().abs().t()).max().item())
+
+
+def test_lstm2_head_adjoint_in_kernel(cuda):
+    """Flatten -> Dense(1) head adjoint generated inside the reverse kernels == the materialised
+    outer product (bitwise: same bf16 rounding as the skinny dgrad kernel)."""
+    from hfrep.ops import functional as Fn
+
+    H, T, K, act = 100, 24, 100, 2
+    B = 97
+    g = torch.Generator().manual_seed(62)
+    x = (torch.randn(B, T, K, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    W = (torch.randn(K, 4 * H, generator=g) * K ** -0.5).to(cuda)
+    U = (torch.randn(H, 4 * H, generator=g) * H ** -0.5).to(cuda)
+    b = torch.zeros(4 * H, device=cuda)
+    _, tape = Fn.lstm_layer_fwd(x, W, b, U, act, True)
+    xd = (torch.randn(B, T, K, generator=g) * 0.3).to(torch.bfloat16).to(cuda)
+    _, ttape = Fn.lstm_layer_tfwd(xd, W, tape, U, act)
+    w = (torch.randn(T * H, 1, generator=g) * 0.05).to(cuda)
+    d = torch.randn(B, 1, generator=g).to(torch.bfloat16).to(cuda)
+    dd = torch.randn(B, 1, generator=g).to(torch.bfloat16).to(cuda)
+    oa, oad = Fn.OuterAdjoint(d, w, (B, T, H)), Fn.OuterAdjoint(dd, w, (B, T, H))
+    dHm, dHdm = oa.materialize(), oad.materialize()
+    assert torch.equal(dHm, Fn.linear_dgrad(d, w).reshape(B, T, H))
+    for Wx in (None, W):
+        r1 = Fn.lstm_layer_bwd(oa, tape, U, act, W=Wx)
+        r2 = Fn.lstm_layer_bwd(dHm, tape, U, act, W=Wx)
+        for a, c in zip(r1 if Wx is not None else (r1,), r2 if Wx is not None else (r2,)):
+            assert torch.equal(a, c)
+        for seeds, mats in (((None, oad), (None, dHdm)), ((oa, oad), (dHm, dHdm))):
+            t1 = Fn.lstm_layer_tbwd(seeds[0], seeds[1], tape, ttape, U, act, W=Wx)
+            t2 = Fn.lstm_layer_tbwd(mats[0], mats[1], tape, ttape, U, act, W=Wx)
+            for a, c in zip(t1, t2):
+                assert torch.equal(a, c)
