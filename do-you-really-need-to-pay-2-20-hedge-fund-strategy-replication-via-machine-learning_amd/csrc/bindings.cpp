@@ -47,6 +47,9 @@ Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act) {
   if (dt_of(x) == hfrep::DT_BF16 && hfrep::skinny_supported(K, N))
     hfrep::launch_skinny_fwd(x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
                              y.data_ptr(), M, K, N, (int)act, cur_stream(x));
+  else if (dt_of(x) == hfrep::DT_BF16 && hfrep::narrow_supported(K, N))
+    hfrep::launch_narrow_fwd(x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
+                             y.data_ptr(), M, K, N, (int)act, cur_stream(x));
   else if (dt_of(x) == hfrep::DT_BF16 && N > 64)
     hfrep::launch_linear2(x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
                           y.data_ptr(), M, N, K, 0, (int)act, cur_stream(x));

@@ -195,9 +195,87 @@ void launch_linear(int dt, const void* A, const float* W, const float* bias, voi
                        K, w_trans, act);
 }
 
+// narrow weight gradient (bf16, K % 4 == 0, K + 1 <= 128, N <= 32, no time shift: the generator's
+// output Dense(F)): one 32-wide column block, 4 waves x 32 rows of C = [X | 1]^T D.  The generic
+// kernel above stages both operands with one 2-byte load + div/mod per element and a 64-wide N
+// tile (half of it padding for N = 32): 425 us per (393k x 100)^T (393k x 32) call.  Here rows
+// are staged with 8-byte buffer loads (rows past the split read zeros) and transposed into LDS.
+typedef int v2i __attribute__((ext_vector_type(2)));
+__global__ void __launch_bounds__(256)
+narrow_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ D, float* __restrict__ slab, int M,
+                    int K, int N, int has_bias, int rows_per_split) {
+  using P = MF<bf16_t>;
+  constexpr int LK = 32 + 8;
+  __shared__ __attribute__((aligned(16))) bf16_t As[128 * LK];  // [i][m]: X^T chunk, row K = ones (bias)
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[32 * LK];   // [j][m]: D^T chunk
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int z = blockIdx.x;
+  const int mb = z * rows_per_split, me = min(M, mb + rows_per_split);
+  for (int i = tid; i < 128 * LK; i += 256) As[i] = 0;
+  for (int i = tid; i < 32 * LK; i += 256) Bs[i] = 0;
+  const int K4 = K / 4, N4 = (N + 3) / 4;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X + (size_t)mb * K), 0,
+                                                                      (me - mb) * K * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(D + (size_t)mb * N), 0,
+                                                                      (me - mb) * N * 2, 0x00020000);
+  f32x16 acc = zero16();
+  __syncthreads();
+  for (int m0 = 0; m0 < me - mb; m0 += 32) {
+    for (int e = tid; e < 32 * K4; e += 256) {
+      const int r = e / K4, c = e - r * K4;
+      const v2i v = __builtin_amdgcn_raw_buffer_load_b64(rx, ((m0 + r) * K + 4 * c) * 2, 0, 0);  // OOB rows -> 0
+      const uint32_t lo = (uint32_t)v[0], hi = (uint32_t)v[1];
+      As[(4 * c + 0) * LK + r] = (bf16_t)(lo & 0xffffu);
+      As[(4 * c + 1) * LK + r] = (bf16_t)(lo >> 16);
+      As[(4 * c + 2) * LK + r] = (bf16_t)(hi & 0xffffu);
+      As[(4 * c + 3) * LK + r] = (bf16_t)(hi >> 16);
+    }
+    if (has_bias && tid < 32) As[K * LK + tid] = (m0 + tid < me - mb) ? (bf16_t)0x3f80 : (bf16_t)0;  // 1.0
+    for (int e = tid; e < 32 * N4; e += 256) {
+      const int r = e / N4, c = e - r * N4;
+      const bool ok = 4 * c + 3 < N;  // (N % 4 != 0: the last group element-wise)
+      if (ok) {
+        const v2i v = __builtin_amdgcn_raw_buffer_load_b64(rd, ((m0 + r) * N + 4 * c) * 2, 0, 0);
+        const uint32_t lo = (uint32_t)v[0], hi = (uint32_t)v[1];
+        Bs[(4 * c + 0) * LK + r] = (bf16_t)(lo & 0xffffu);
+        Bs[(4 * c + 1) * LK + r] = (bf16_t)(lo >> 16);
+        Bs[(4 * c + 2) * LK + r] = (bf16_t)(hi & 0xffffu);
+        Bs[(4 * c + 3) * LK + r] = (bf16_t)(hi >> 16);
+      } else {
+        for (int q = 0; q < 4 && 4 * c + q < N; ++q)
+          Bs[(4 * c + q) * LK + r] = (bf16_t)__builtin_amdgcn_raw_buffer_load_b16(rd, ((m0 + r) * N + 4 * c + q) * 2, 0, 0);
+      }
+    }
+    __syncthreads();
+    const bf16_t* arow = As + (w * 32 + (lane & 31)) * LK;
+    const bf16_t* brow = Bs + (lane & 31) * LK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) acc = P::mma(P::lda(arow, ks, lane), P::lda(brow, ks, lane), acc);
+    __syncthreads();
+  }
+  const int Kr = K + has_bias;
+  float* out = slab + (size_t)z * Kr * N;
+  const int col = lane & 31;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = w * 32 + acc32_row(r, lane);
+    if (row < Kr && col < N) out[(size_t)row * N + col] = acc[r];
+  }
+}
+
 void launch_wgrad(int dt, const void* X, const void* D, float* gW, float* gb, int M, int K, int N, int shiftT,
                   float* ws, hipStream_t s) {
   if (M <= 0) return;
+  if (dt == DT_BF16 && shiftT == 0 && K % 4 == 0 && K + 1 <= 128 && N <= 32) {
+    const int splits = wgrad_splits(M, K, N);
+    const int rps = ((M + splits - 1) / splits + 31) / 32 * 32;
+    const int z = (M + rps - 1) / rps;
+    hipLaunchKernelGGL(narrow_wgrad_kernel, dim3(z), dim3(256), 0, s, (const bf16_t*)X, (const bf16_t*)D, ws, M, K, N,
+                       gb != nullptr ? 1 : 0, rps);
+    const int blocks = (int)std::min<int64_t>(((int64_t)(K + 1) * N + 255) / 256, 1024);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, gW, gb, z, K, N, gb != nullptr ? 1 : 0);
+    return;
+  }
   const int has_bias = gb != nullptr;
   const int Kr = K + has_bias;
   const int splits = wgrad_splits(M, K, N);

@@ -70,6 +70,9 @@ bool launch_lstm_wgrad3(const void* X0, const void* H0, const void* D0, const vo
 
 // ---- skinny.hip (bf16, N <= 4 output columns, K % 8 == 0: the Flatten -> Dense(1) critic head) ----
 bool skinny_supported(int K, int N);
+bool narrow_supported(int K, int N);  // 4 < N <= 64, K <= 128 (bf16 forward only)
+void launch_narrow_fwd(const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
+                       hipStream_t s);
 void launch_skinny_fwd(const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
                        hipStream_t s);
 size_t skinny_wgrad_workspace_floats(int M, int K, int N);

@@ -13,6 +13,9 @@
 //   skinny_dgrad dx[m,k]  = sum_n d[m,n] W[k,n]              one 16-byte output chunk per thread
 #include "common.h"
 #include "kernels.h"
+#include "mfma.h"
+
+#include <algorithm>
 
 namespace hfrep {
 
@@ -192,6 +195,83 @@ __global__ void __launch_bounds__(256) skinny_dgrad_kernel(const bf16_t* __restr
     }
     *reinterpret_cast<uint4*>(dx + m * K + 8 * c) = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]),
                                                                 pack2(o[4], o[5]), pack2(o[6], o[7]));
+  }
+}
+
+// ------------------------------------------------------------------------------------ narrow Dense
+// y = act(x W + b) for 4 < N <= 32, K <= 128, bf16 (the generator's output Dense(F), F = 32..36 ->
+// N <= 32 covers F = 32; 33..64 use two column tiles).  The generic tile GEMM staged x through LDS
+// for a 128-wide N tile and ran at ~1.1 TB/s (1.55 ms per (6.3M x 100) x (100 x 32) call).  Here a
+// wave owns one 32-column tile with W as register fragments (ceil(K/16) x 4 VGPRs) and streams
+// 32-row tiles (grid-stride) straight from HBM into MFMA A fragments (one 16-byte buffer load
+// per k-step per lane, rows past M read zeros, k >= K columns masked).
+template <int KS>
+__global__ void __launch_bounds__(256) narrow_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W,
+                                                         const float* __restrict__ bias, bf16_t* __restrict__ y, int M,
+                                                         int K, int N, int act) {
+  using P = MF<bf16_t>;
+  const int lane = threadIdx.x & 63;
+  const int col0 = blockIdx.y * 32, col = col0 + (lane & 31);
+  const int kh = 8 * (lane >> 5);
+  typename P::frag wb[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * ks + kh + j;
+      const float v = W[(size_t)min(k, K - 1) * N + min(col, N - 1)];
+      wb[ks][j] = (short)f2bf((k < K && col < N) ? v : 0.f);
+    }
+  const float bv = (bias && col < N) ? bias[col] : 0.f;
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x), 0, (int)std::min<int64_t>((int64_t)M * K * 2, 0x7fff0000), 0x00020000);
+  const int ntiles = (M + 31) / 32;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  for (int tile = wid; tile < ntiles; tile += nw) {
+    const int row = tile * 32 + (lane & 31);
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k0 = 16 * ks + kh;
+      const bool ok = row < M && k0 < K;
+      bf16x8 a = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                rx, ok ? (int)(((int64_t)row * K + k0) * 2) : 0x7fff0000, 0, 0));
+      if (16 * ks + 16 > K) {  // the k-step that crosses K: zero the columns past it (they belong to the next row)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (k0 + j >= K) a[j] = 0;
+      }
+      acc = P::mma(a, wb[ks], acc);
+    }
+    if (col < N) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = tile * 32 + acc32_row(r, lane);
+        if (rr < M) y[(size_t)rr * N + col] = f2bf(act_f(act, acc[r] + bv));
+      }
+    }
+  }
+}
+
+bool narrow_supported(int K, int N) { return N > 4 && N <= 64 && K >= 1 && K <= 128; }
+
+void launch_narrow_fwd(const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
+                       hipStream_t s) {
+  const int ntiles = (M + 31) / 32;
+  const int bx = std::max(1, std::min((ntiles + 3) / 4, device_cu_count() * 8));
+  const dim3 grid(bx, (N + 31) / 32);
+  const int ks = (K + 15) / 16;
+  const bf16_t* xp = (const bf16_t*)x;
+  bf16_t* yp = (bf16_t*)y;
+  switch (ks) {
+    case 1: hipLaunchKernelGGL(narrow_fwd_kernel<1>, grid, dim3(256), 0, s, xp, W, b, yp, M, K, N, act); break;
+    case 2: hipLaunchKernelGGL(narrow_fwd_kernel<2>, grid, dim3(256), 0, s, xp, W, b, yp, M, K, N, act); break;
+    case 3: hipLaunchKernelGGL(narrow_fwd_kernel<3>, grid, dim3(256), 0, s, xp, W, b, yp, M, K, N, act); break;
+    case 4: hipLaunchKernelGGL(narrow_fwd_kernel<4>, grid, dim3(256), 0, s, xp, W, b, yp, M, K, N, act); break;
+    case 5: hipLaunchKernelGGL(narrow_fwd_kernel<5>, grid, dim3(256), 0, s, xp, W, b, yp, M, K, N, act); break;
+    case 6: hipLaunchKernelGGL(narrow_fwd_kernel<6>, grid, dim3(256), 0, s, xp, W, b, yp, M, K, N, act); break;
+    case 7: hipLaunchKernelGGL(narrow_fwd_kernel<7>, grid, dim3(256), 0, s, xp, W, b, yp, M, K, N, act); break;
+    default: hipLaunchKernelGGL(narrow_fwd_kernel<8>, grid, dim3(256), 0, s, xp, W, b, yp, M, K, N, act); break;
   }
 }
 

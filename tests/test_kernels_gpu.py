@@ -33,7 +33,8 @@ def _ops():
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,K,N,act", [(1000, 32, 400, 0), (777, 100, 400, 0), (300, 35, 100, 1), (64, 2400, 1, 0),
-                                       (257, 100, 35, 3), (40, 100, 100, 2)])
+                                       (257, 100, 35, 3), (40, 100, 100, 2), (70001, 100, 32, 0), (333, 36, 36, 1),
+                                       (129, 22, 7, 3)])
 def test_linear(cuda, dt, M, K, N, act):
     g = torch.Generator().manual_seed(0)
     x = torch.randn(M, K, generator=g) * 0.5
@@ -55,7 +56,8 @@ def test_linear_dgrad(cuda, dt, M, N, K):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("M,K,N,shift", [(5000, 100, 400, 0), (4800, 100, 400, 24), (96, 32, 400, 0), (64, 2400, 1, 0)])
+@pytest.mark.parametrize("M,K,N,shift", [(5000, 100, 400, 0), (4800, 100, 400, 24), (96, 32, 400, 0), (64, 2400, 1, 0),
+                                         (70001, 100, 32, 0), (777, 32, 20, 0), (300, 36, 7, 0)])
 def test_wgrad(cuda, dt, M, K, N, shift):
     g = torch.Generator().manual_seed(2)
     x = torch.randn(M, K, generator=g)
