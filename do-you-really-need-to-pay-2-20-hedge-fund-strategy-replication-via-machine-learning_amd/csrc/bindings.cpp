@@ -12,6 +12,10 @@
 
 #include "kernels.h"
 
+#include <atomic>
+#include <cmath>
+#include <cstdlib>
+
 namespace {
 
 using at::Tensor;
@@ -36,6 +40,26 @@ inline void same_dt(const Tensor& a, const Tensor& b) {
 }
 inline const void* ptr_or_null(const optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
 
+// Debug poison mode (HFREP_POISON=1 or set_debug_poison(True)): every op output / workspace is
+// allocated filled with NaN instead of uninitialised, so an element a kernel fails to write shows
+// up as a non-finite loss or gradient (tests/test_gpu_runtime.py).  Off by default (it costs a
+// fill per output).  Tapes are exempt: their padded unit lanes are unwritten by design and never
+// read.
+std::atomic<bool>& poison_flag() {
+  static std::atomic<bool> f{[] {
+    const char* e = getenv("HFREP_POISON");
+    return e && e[0] == '1';
+  }()};
+  return f;
+}
+inline Tensor out_empty(at::IntArrayRef sizes, const at::TensorOptions& o) {
+  return poison_flag().load(std::memory_order_relaxed) ? at::full(sizes, NAN, o) : at::empty(sizes, o);
+}
+inline Tensor out_empty_like(const Tensor& t) {
+  return poison_flag().load(std::memory_order_relaxed) ? at::full_like(t, NAN) : at::empty_like(t);
+}
+bool set_debug_poison(bool on) { return poison_flag().exchange(on); }
+
 // ------------------------------------------------------------------------------------ GEMM
 Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act) {
   CHECK_GPU(x); CHECK_F32(W);
@@ -43,7 +67,7 @@ Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act) {
   if (b.has_value()) { CHECK_F32(*b); TORCH_CHECK(b->numel() == W.size(1), "linear: bias size"); }
   GUARD(x);
   const int M = x.size(0), K = x.size(1), N = W.size(1);
-  Tensor y = at::empty({M, N}, x.options());
+  Tensor y = out_empty({M, N}, x.options());
   if (dt_of(x) == hfrep::DT_BF16 && hfrep::skinny_supported(K, N))
     hfrep::launch_skinny_fwd(x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
                              y.data_ptr(), M, K, N, (int)act, cur_stream(x));
@@ -64,7 +88,7 @@ Tensor linear_dgrad(Tensor dz, Tensor W) {
   TORCH_CHECK(dz.dim() == 2 && W.dim() == 2 && dz.size(1) == W.size(1), "linear_dgrad: shape mismatch");
   GUARD(dz);
   const int M = dz.size(0), K = dz.size(1), N = W.size(0);
-  Tensor dx = at::empty({M, N}, dz.options());
+  Tensor dx = out_empty({M, N}, dz.options());
   // dx = dz . W^T : W stored (N, K) row-major -> w_trans
   if (dt_of(dz) == hfrep::DT_BF16 && hfrep::skinny_supported(N, K))
     hfrep::launch_skinny_dgrad(dz.data_ptr(), W.data_ptr<float>(), dx.data_ptr(), M, N, K, cur_stream(dz));
@@ -85,13 +109,13 @@ void linear_wgrad_(Tensor x, Tensor dz, Tensor gW, optional<Tensor> gb, int64_t 
   GUARD(x);
   const int M = x.size(0), K = x.size(1), N = dz.size(1);
   if (dt_of(x) == hfrep::DT_BF16 && shiftT == 0 && hfrep::skinny_supported(K, N)) {
-    Tensor ws = at::empty({(int64_t)hfrep::skinny_wgrad_workspace_floats(M, K, N)}, x.options().dtype(at::kFloat));
+    Tensor ws = out_empty({(int64_t)hfrep::skinny_wgrad_workspace_floats(M, K, N)}, x.options().dtype(at::kFloat));
     hfrep::launch_skinny_wgrad(x.data_ptr(), dz.data_ptr(), gW.data_ptr<float>(),
                                gb.has_value() ? gb->data_ptr<float>() : nullptr, M, K, N, ws.data_ptr<float>(),
                                cur_stream(x));
     return;
   }
-  Tensor ws = at::empty({(int64_t)hfrep::wgrad_workspace_floats(M, K, N)}, x.options().dtype(at::kFloat));
+  Tensor ws = out_empty({(int64_t)hfrep::wgrad_workspace_floats(M, K, N)}, x.options().dtype(at::kFloat));
   hfrep::launch_wgrad(dt_of(x), x.data_ptr(), dz.data_ptr(), gW.data_ptr<float>(),
                       gb.has_value() ? gb->data_ptr<float>() : nullptr, M, K, N, (int)shiftT, ws.data_ptr<float>(),
                       cur_stream(x));
@@ -122,12 +146,12 @@ void lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<
   float* gbp = gb.has_value() ? gb->data_ptr<float>() : nullptr;
   // impl: 0 = auto (LDS-DMA streaming v3 where supported), 2 = force v2 (tests / A-B)
   if (impl != 2 && hfrep::lstm_wgrad3_supported(M, K, Hd, N)) {
-    Tensor ws = at::empty({(int64_t)hfrep::lstm_wgrad3_workspace_floats(K, Hd, N)}, x.options().dtype(at::kFloat));
+    Tensor ws = out_empty({(int64_t)hfrep::lstm_wgrad3_workspace_floats(K, Hd, N)}, x.options().dtype(at::kFloat));
     if (hfrep::launch_lstm_wgrad3(x.data_ptr(), hs.data_ptr(), dZ.data_ptr(), X1, H1, D1, gW.data_ptr<float>(),
                                   gU.data_ptr<float>(), gbp, M, K, Hd, N, Tn, ws.data_ptr<float>(), cur_stream(x)))
       return;
   }
-  Tensor ws = at::empty({(int64_t)hfrep::lstm_wgrad2_workspace_floats(M, K, Hd, N)}, x.options().dtype(at::kFloat));
+  Tensor ws = out_empty({(int64_t)hfrep::lstm_wgrad2_workspace_floats(M, K, Hd, N)}, x.options().dtype(at::kFloat));
   hfrep::launch_lstm_wgrad2(x.data_ptr(), hs.data_ptr(), dZ.data_ptr(), tangent ? xd->data_ptr() : nullptr,
                             tangent ? hds->data_ptr() : nullptr, tangent ? dZd->data_ptr() : nullptr,
                             gW.data_ptr<float>(), gU.data_ptr<float>(), gb.has_value() ? gb->data_ptr<float>() : nullptr,
@@ -137,7 +161,7 @@ void lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<
 // ------------------------------------------------------------------------------------ elementwise
 Tensor act_fwd(Tensor x, int64_t act) {
   CHECK_GPU(x); GUARD(x);
-  Tensor y = at::empty_like(x);
+  Tensor y = out_empty_like(x);
   hfrep::launch_act_fwd(dt_of(x), x.data_ptr(), y.data_ptr(), x.numel(), (int)act, cur_stream(x));
   return y;
 }
@@ -145,7 +169,7 @@ Tensor act_bwd(Tensor dy, Tensor y, int64_t act) {
   CHECK_GPU(dy); CHECK_GPU(y); same_dt(dy, y);
   TORCH_CHECK(dy.numel() == y.numel(), "act_bwd: size");
   GUARD(dy);
-  Tensor dx = at::empty_like(dy);
+  Tensor dx = out_empty_like(dy);
   hfrep::launch_act_bwd(dt_of(dy), dy.data_ptr(), y.data_ptr(), dx.data_ptr(), dy.numel(), (int)act, cur_stream(dy));
   return dx;
 }
@@ -153,7 +177,7 @@ Tensor act_tangent_bwd(Tensor dyd, Tensor y, Tensor zd, int64_t act) {
   CHECK_GPU(dyd); CHECK_GPU(y); CHECK_GPU(zd); same_dt(dyd, y); same_dt(dyd, zd);
   TORCH_CHECK(dyd.numel() == y.numel() && y.numel() == zd.numel(), "act_tangent_bwd: size");
   GUARD(dyd);
-  Tensor out = at::empty_like(dyd);
+  Tensor out = out_empty_like(dyd);
   hfrep::launch_act_tangent_bwd(dt_of(dyd), dyd.data_ptr(), y.data_ptr(), zd.data_ptr(), out.data_ptr(), dyd.numel(),
                                 (int)act, cur_stream(dyd));
   return out;
@@ -171,9 +195,9 @@ std::tuple<Tensor, Tensor, Tensor> lstm_fwd(Tensor zx, Tensor U, int64_t act, bo
   const int B = zx.size(0), Tn = zx.size(1), H = zx.size(2) / 4;
   check_lstm_U(U, H);
   GUARD(zx);
-  Tensor hs = at::empty({B, Tn, H}, zx.options());
-  Tensor gates = save ? at::empty({B, Tn, 4 * H}, zx.options()) : at::empty({0}, zx.options());
-  Tensor cs = save ? at::empty({B, Tn, H}, zx.options()) : at::empty({0}, zx.options());
+  Tensor hs = out_empty({B, Tn, H}, zx.options());
+  Tensor gates = save ? out_empty({B, Tn, 4 * H}, zx.options()) : out_empty({0}, zx.options());
+  Tensor cs = save ? out_empty({B, Tn, H}, zx.options()) : out_empty({0}, zx.options());
   const bool ok = hfrep::launch_lstm_fwd(dt_of(zx), zx.data_ptr(), U.data_ptr<float>(), hs.data_ptr(),
                                          save ? gates.data_ptr() : nullptr, save ? cs.data_ptr() : nullptr, B, Tn, H,
                                          (int)act, cur_stream(zx));
@@ -187,7 +211,7 @@ Tensor lstm_bwd(Tensor dH, Tensor gates, Tensor cs, Tensor U, int64_t act) {
   TORCH_CHECK(dH.sizes() == cs.sizes() && cs.size(2) == H, "lstm_bwd: shapes");
   check_lstm_U(U, H);
   GUARD(dH);
-  Tensor dZ = at::empty_like(gates);
+  Tensor dZ = out_empty_like(gates);
   const bool ok = hfrep::launch_lstm_bwd(dt_of(dH), dH.data_ptr(), gates.data_ptr(), cs.data_ptr(),
                                          U.data_ptr<float>(), dZ.data_ptr(), B, Tn, H, (int)act, cur_stream(dH));
   TORCH_CHECK(ok, "lstm_bwd: hidden size ", H, " not instantiated");
@@ -200,9 +224,9 @@ std::tuple<Tensor, Tensor, Tensor> lstm_tfwd(Tensor dzx, Tensor gates, Tensor cs
   const int B = gates.size(0), Tn = gates.size(1), H = gates.size(2) / 4;
   check_lstm_U(U, H);
   GUARD(dzx);
-  Tensor hds = at::empty({B, Tn, H}, dzx.options());
-  Tensor zds = at::empty_like(gates);
-  Tensor cds = at::empty({B, Tn, H}, dzx.options());
+  Tensor hds = out_empty({B, Tn, H}, dzx.options());
+  Tensor zds = out_empty_like(gates);
+  Tensor cds = out_empty({B, Tn, H}, dzx.options());
   const bool ok = hfrep::launch_lstm_tfwd(dt_of(dzx), dzx.data_ptr(), gates.data_ptr(), cs.data_ptr(),
                                           U.data_ptr<float>(), hds.data_ptr(), zds.data_ptr(), cds.data_ptr(), B, Tn,
                                           H, (int)act, cur_stream(dzx));
@@ -218,7 +242,7 @@ std::tuple<Tensor, Tensor> lstm_tbwd(optional<Tensor> dH, Tensor dHd, Tensor gat
   const int B = gates.size(0), Tn = gates.size(1), H = gates.size(2) / 4;
   check_lstm_U(U, H);
   GUARD(dHd);
-  Tensor dZ = at::empty_like(gates), dZd = at::empty_like(gates);
+  Tensor dZ = out_empty_like(gates), dZd = out_empty_like(gates);
   const bool ok = hfrep::launch_lstm_tbwd(dt_of(dHd), ptr_or_null(dH), dHd.data_ptr(), gates.data_ptr(),
                                           cs.data_ptr(), zds.data_ptr(), cds.data_ptr(), U.data_ptr<float>(),
                                           dZ.data_ptr(), dZd.data_ptr(), B, Tn, H, (int)act, cur_stream(dHd));
@@ -241,8 +265,8 @@ std::tuple<Tensor, Tensor> lstm2_fwd(Tensor x, Tensor W, optional<Tensor> b, Ten
   TORCH_CHECK(W.size(0) == K && W.size(1) == 4 * H, "W must be (K, 4H)");
   if (b.has_value()) { CHECK_F32(*b); TORCH_CHECK(b->numel() == 4 * H, "bias size"); }
   GUARD(x);
-  Tensor hs = at::empty({B, Tn, H}, x.options());
-  Tensor tape = at::empty({save ? (int64_t)hfrep::lstm2_tape_elems(B, Tn) : 0}, x.options());
+  Tensor hs = out_empty({B, Tn, H}, x.options());
+  Tensor tape = at::empty({save ? (int64_t)hfrep::lstm2_tape_elems(B, Tn) : 0}, x.options());  // (not poisoned: padded lanes)
   hfrep::launch_lstm2_fwd(x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
                           U.data_ptr<float>(), hs.data_ptr(), save ? tape.data_ptr() : nullptr, B, Tn, K, H, (int)act,
                           cur_stream(x));
@@ -294,8 +318,8 @@ std::tuple<Tensor, Tensor> lstm2_bwd(optional<Tensor> dH_, Tensor tape, Tensor U
   TORCH_CHECK(need_dz || K, "lstm2_bwd: nothing to compute (need_dz=False without W)");
   const bool gen = !dH_ && hfrep::lstm2_head_fusion();
   Tensor dH = dH_ ? *dH_ : (gen ? Tensor() : head_outer(*head_d, *head_w, B, Tn, H));
-  Tensor dZ = at::empty({need_dz ? B : 0, Tn, 4 * H}, tape.options());
-  Tensor dX = at::empty({K ? B : 0, Tn, K}, tape.options());
+  Tensor dZ = out_empty({need_dz ? B : 0, Tn, 4 * H}, tape.options());
+  Tensor dX = out_empty({K ? B : 0, Tn, K}, tape.options());
   hfrep::launch_lstm2_bwd(gen ? nullptr : dH.data_ptr(), tape.data_ptr(), U.data_ptr<float>(),
                           need_dz ? dZ.data_ptr() : nullptr, K ? W->data_ptr<float>() : nullptr,
                           K ? dX.data_ptr() : nullptr, K, B, Tn, H, (int)act, cur_stream(tape),
@@ -310,8 +334,8 @@ std::tuple<Tensor, Tensor> lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape
   TORCH_CHECK(W.size(0) == K && W.size(1) == 4 * H, "W must be (K, 4H)");
   TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstm2_tape_elems(B, Tn), "lstm2_tfwd: tape size");
   GUARD(xd);
-  Tensor hds = at::empty({B, Tn, H}, xd.options());
-  Tensor ttape = at::empty_like(tape);
+  Tensor hds = out_empty({B, Tn, H}, xd.options());
+  Tensor ttape = at::empty_like(tape);  // (not poisoned: padded lanes)
   hfrep::launch_lstm2_tfwd(xd.data_ptr(), W.data_ptr<float>(), U.data_ptr<float>(), tape.data_ptr(), hds.data_ptr(),
                            ttape.data_ptr(), B, Tn, K, H, (int)act, cur_stream(xd));
   return {hds, ttape};
@@ -350,8 +374,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm2_tbwd(optional<Tensor> dH, optio
   } else if (!head) {
     dHd = *dHd_;
   }
-  Tensor dZ = at::empty({B, Tn, 4 * H}, tape.options()), dZd = at::empty({B, Tn, 4 * H}, tape.options());
-  Tensor dX = at::empty({K ? B : 0, Tn, K}, tape.options()), dXd = at::empty({K ? B : 0, Tn, K}, tape.options());
+  Tensor dZ = out_empty({B, Tn, 4 * H}, tape.options()), dZd = out_empty({B, Tn, 4 * H}, tape.options());
+  Tensor dX = out_empty({K ? B : 0, Tn, K}, tape.options()), dXd = out_empty({K ? B : 0, Tn, K}, tape.options());
   hfrep::launch_lstm2_tbwd(gen ? nullptr : ptr_or_null(dHm), gen ? nullptr : dHd.data_ptr(), tape.data_ptr(),
                            ttape.data_ptr(), U.data_ptr<float>(), dZ.data_ptr(), dZd.data_ptr(),
                            K ? W->data_ptr<float>() : nullptr, K ? dX.data_ptr() : nullptr, K ? dXd.data_ptr() : nullptr,
@@ -370,10 +394,10 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(Tensor x, Tensor gamma, Tensor 
   TORCH_CHECK(D <= 256 && gamma.numel() == D && beta.numel() == D, "layernorm: D <= 256 and param sizes");
   GUARD(x);
   const int64_t rows = x.numel() / D;
-  Tensor y = at::empty_like(x), xhat = save ? at::empty_like(x) : at::empty({0}, x.options());
+  Tensor y = out_empty_like(x), xhat = save ? out_empty_like(x) : out_empty({0}, x.options());
   std::vector<int64_t> rs(x.sizes().begin(), x.sizes().end() - 1);
   rs.push_back(1);
-  Tensor rstd = save ? at::empty(rs, x.options().dtype(at::kFloat)) : at::empty({0}, x.options().dtype(at::kFloat));
+  Tensor rstd = save ? out_empty(rs, x.options().dtype(at::kFloat)) : out_empty({0}, x.options().dtype(at::kFloat));
   hfrep::launch_layernorm_fwd(dt_of(x), x.data_ptr(), gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
                               save ? xhat.data_ptr() : nullptr, save ? rstd.data_ptr<float>() : nullptr, rows, D,
                               (float)eps, (float)pre_lrelu, cur_stream(x));
@@ -389,9 +413,9 @@ Tensor layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, optiona
   if (ggamma.has_value()) { CHECK_F32(*ggamma); gg = ggamma->data_ptr<float>(); }
   if (gbeta.has_value()) { CHECK_F32(*gbeta); gbp = gbeta->data_ptr<float>(); }
   GUARD(dy);
-  Tensor dx = at::empty_like(dy);
+  Tensor dx = out_empty_like(dy);
   const int64_t rows = dy.numel() / D;
-  Tensor ws = at::empty({(gg || gbp) ? (int64_t)hfrep::layernorm_bwd_splits(rows) * 2 * D : 0},
+  Tensor ws = out_empty({(gg || gbp) ? (int64_t)hfrep::layernorm_bwd_splits(rows) * 2 * D : 0},
                         dy.options().dtype(at::kFloat));
   hfrep::launch_layernorm_bwd(dt_of(dy), dy.data_ptr(), xhat.data_ptr(), rstd.data_ptr<float>(),
                               gamma.data_ptr<float>(), dx.data_ptr(), gg, gbp, (gg || gbp) ? ws.data_ptr<float>() : nullptr,
@@ -405,7 +429,7 @@ Tensor im2col_causal(Tensor x, int64_t k, int64_t dil) {
   TORCH_CHECK(x.dim() == 3 && k >= 1 && dil >= 1, "im2col_causal: (B,T,C), k, dil");
   GUARD(x);
   const int B = x.size(0), Tn = x.size(1), C = x.size(2);
-  Tensor cols = at::empty({B, Tn, k * C}, x.options());
+  Tensor cols = out_empty({B, Tn, k * C}, x.options());
   hfrep::launch_im2col_causal(dt_of(x), x.data_ptr(), cols.data_ptr(), B, Tn, C, (int)k, (int)dil, cur_stream(x));
   return cols;
 }
@@ -414,7 +438,7 @@ Tensor col2im_causal(Tensor dcols, int64_t k, int64_t dil, int64_t C) {
   TORCH_CHECK(dcols.dim() == 3 && dcols.size(2) == k * C, "col2im_causal: (B,T,k*C)");
   GUARD(dcols);
   const int B = dcols.size(0), Tn = dcols.size(1);
-  Tensor dx = at::empty({B, Tn, C}, dcols.options());
+  Tensor dx = out_empty({B, Tn, C}, dcols.options());
   hfrep::launch_col2im_causal(dt_of(dcols), dcols.data_ptr(), dx.data_ptr(), B, Tn, (int)C, (int)k, (int)dil,
                               cur_stream(dcols));
   return dx;
@@ -425,9 +449,9 @@ std::tuple<Tensor, Tensor> gp_coef(Tensor g, double weight) {
   CHECK_GPU(g); GUARD(g);
   const int B = g.size(0);
   const int64_t D = g.numel() / B;
-  Tensor v = at::empty_like(g);
+  Tensor v = out_empty_like(g);
   Tensor pen = at::zeros({}, g.options().dtype(at::kFloat));
-  Tensor rowpen = at::empty({B}, g.options().dtype(at::kFloat));
+  Tensor rowpen = out_empty({B}, g.options().dtype(at::kFloat));
   hfrep::launch_gp_coef(dt_of(g), g.data_ptr(), v.data_ptr(), pen.data_ptr<float>(), rowpen.data_ptr<float>(), B, D,
                         (float)weight, cur_stream(g));
   return {pen, v};
@@ -437,7 +461,7 @@ Tensor interpolate(Tensor real, Tensor fake, Tensor alpha) {
   CHECK_GPU(real); CHECK_GPU(fake); same_dt(real, fake); CHECK_F32(alpha);
   TORCH_CHECK(real.sizes() == fake.sizes() && alpha.numel() == real.size(0), "interpolate: shapes");
   GUARD(real);
-  Tensor out = at::empty_like(real);
+  Tensor out = out_empty_like(real);
   const int B = real.size(0);
   hfrep::launch_interpolate(dt_of(real), real.data_ptr(), fake.data_ptr(), alpha.data_ptr<float>(), out.data_ptr(), B,
                             real.numel() / B, cur_stream(real));
@@ -459,7 +483,7 @@ Tensor sample_windows(Tensor data, int64_t batch, int64_t seed, Tensor ctr, at::
   GUARD(data);
   std::vector<int64_t> shape(data.sizes().begin(), data.sizes().end());
   shape[0] = batch;
-  Tensor out = at::empty(shape, data.options().dtype(out_dtype));
+  Tensor out = out_empty(shape, data.options().dtype(out_dtype));
   const int64_t N = data.size(0), D = data.numel() / N;
   hfrep::launch_sample_windows(dt_of(out), data.data_ptr<float>(), N, D, out.data_ptr(), (int)batch, (uint64_t)seed,
                                ctr.data_ptr<int64_t>(), cur_stream(data));
@@ -529,6 +553,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int act) -> (Tensor, Tensor)");
   m.def("lstm2_tbwd(Tensor? dH, Tensor? dHd, Tensor tape, Tensor ttape, Tensor U, int act, Tensor? W=None, "
         "Tensor? head_d=None, Tensor? head_dd=None, Tensor? head_w=None) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("set_debug_poison(bool on) -> bool", &set_debug_poison);  // no tensor inputs: catch-all kernel
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps, bool save=True, float pre_lrelu=-1.0) -> "
         "(Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, Tensor(a!)? ggamma, Tensor(b!)? gbeta) -> Tensor");

@@ -110,3 +110,28 @@ def test_dp_two_ranks_on_gpu_tensors(cuda):
         p.join(timeout=60)
     assert np.isfinite(res[0]).all()
     assert np.array_equal(res[0], res[1])
+
+
+@pytest.mark.parametrize("key", [("lstm", "wgan_gp"), ("lstm", "wgan"), ("lstm", "gan"), ("mlp", "wgan_gp"),
+                                 ("conv", "wgan_gp")])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_poisoned_outputs_all_written(cuda, key, dtype):
+    """Uninitialised-output detector (SURVEY.md §5 race/sanitizer row): with the debug poison mode
+    every op output and workspace starts as NaN, so any element a kernel leaves unwritten (a lost
+    row tile, a short store loop, a skipped padded column that is read later) turns the losses
+    or gradients non-finite.  Odd batch (37) and window (23) exercise the partial-tile paths."""
+    from hfrep.ops import _native
+
+    ops = _native.native()
+    prev = ops.set_debug_poison(True)
+    try:
+        tr = _trainer(cuda, dtype=dtype, key=key, B=37, T=23, F=32)
+        for _ in range(2):
+            tr.train_step()
+        torch.cuda.synchronize()
+        rec = tr.losses()
+        assert all(np.isfinite(v) for k, v in rec.items() if k != "iteration"), rec
+        for m in (tr.generator, tr.critic):
+            assert bool(torch.isfinite(m.flat).all()), m.model_name
+    finally:
+        ops.set_debug_poison(prev)
