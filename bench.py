@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--dataset-windows", type=int, default=8192)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (e.g. for rocprof)")
+    ap.add_argument("--trace-out", default="", help="after the timed steps: torch.profiler Chrome trace of "
+                    "--profile-steps (default 2) untimed steps with the trainer's phase ranges")
     args = ap.parse_args()
 
     import numpy as np
@@ -82,8 +84,13 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    for _ in range(args.profile_steps):
-        tr.train_step()
+    if args.trace_out and rank == 0:
+        from hfrep.utils.trace import profile_steps
+
+        print(profile_steps(tr.train_step, args.profile_steps or 2, args.trace_out), file=sys.stderr)
+    else:
+        for _ in range(args.profile_steps):
+            tr.train_step()
     torch.cuda.synchronize()
 
     ms = elapsed / args.steps * 1e3

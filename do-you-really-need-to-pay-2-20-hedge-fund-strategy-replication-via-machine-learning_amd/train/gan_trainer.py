@@ -32,6 +32,7 @@ from ..models import gan as zoo
 from ..ops import functional as Fn
 from ..ops import reference as R
 from ..utils.rng import DeviceRNG
+from ..utils.trace import trange
 from .optim import KerasOptimizer
 
 
@@ -127,13 +128,15 @@ class GANTrainer:
 
     def _sync(self, model):
         if self.grad_sync is not None:
-            if self.grad_sync.finish_() == 0:  # no overlapped buckets were launched
-                self.grad_sync.all_reduce_(model.flat.grad)
+            with trange("allreduce"):
+                if self.grad_sync.finish_() == 0:  # no overlapped buckets were launched
+                    self.grad_sync.all_reduce_(model.flat.grad)
 
     def _apply(self, model, clip=0.0):
         self._sync(model)
-        self.opt.apply(model.flat, clip=clip)
-        model.zero_grad()
+        with trange("optimizer"):
+            self.opt.apply(model.flat, clip=clip)
+            model.zero_grad()
 
     # ---- critic losses --------------------------------------------------------------------
     def _bce_step(self, x, label: float):
@@ -159,8 +162,9 @@ class GANTrainer:
         return loss
 
     def _gp_step(self, real, noise):
-        fake = self.generator.predict(noise)
-        alpha = self.rng.uniform((real.shape[0],))
+        with trange("critic/generate"):
+            fake = self.generator.predict(noise)
+            alpha = self.rng.uniform((real.shape[0],))
         out = self.critic_gp_grads(real, fake, alpha)
         self._apply(self.critic)
         return out
@@ -171,19 +175,22 @@ class GANTrainer:
         B = real.shape[0]
         xh = Fn.interpolate(real, fake, alpha)
         # W terms on [real; fake]
-        xrf = torch.cat([real, fake], 0)
-        s, tape = C.efwd(xrf, save=True)
-        ds = torch.empty_like(s)
-        ds[:B] = -1.0 / B
-        ds[B:] = 1.0 / B
-        C.ebwd(tape, ds)
+        with trange("critic/w_terms"):
+            xrf = torch.cat([real, fake], 0)
+            s, tape = C.efwd(xrf, save=True)
+            ds = torch.empty_like(s)
+            ds[:B] = -1.0 / B
+            ds[B:] = 1.0 / B
+            C.ebwd(tape, ds)
         # gradient penalty: g = dD/dx_hat (input gradient only), v = dGP/dg, then the
         # theta-gradient of <v, g> as reverse-over-tangent
-        sh, tape_h = C.efwd(xh, save=True)
-        g = C.ebwd(tape_h, torch.ones_like(sh), need_dx=True, wgrad=False)
-        pen, v = Fn.gp_coef(g, self.gp_weight)
-        sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
-        C.etbwd(tape_h, ttape, None, torch.ones_like(sd), hook=self._hook(C))
+        with trange("critic/gp_input_grad"):
+            sh, tape_h = C.efwd(xh, save=True)
+            g = C.ebwd(tape_h, torch.ones_like(sh), need_dx=True, wgrad=False)
+            pen, v = Fn.gp_coef(g, self.gp_weight)
+        with trange("critic/gp_second_order"):
+            sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
+            C.etbwd(tape_h, ttape, None, torch.ones_like(sd), hook=self._hook(C))
         sf = s.to(self._acc)
         w_real = -sf[:B].mean()
         w_fake = sf[B:].mean()
@@ -191,7 +198,8 @@ class GANTrainer:
 
     # ---- generator ------------------------------------------------------------------------
     def _generator_step(self, noise):
-        loss = self.generator_grads(noise)
+        with trange("generator"):
+            loss = self.generator_grads(noise)
         self._apply(self.generator)
         return loss
 
@@ -237,7 +245,8 @@ class GANTrainer:
             self._g_acc = self._generator_step(noise).reshape(1)
         else:
             for _ in range(self.n_critic):
-                real, noise = self._batch(B)
+                with trange("critic/sample"):
+                    real, noise = self._batch(B)
                 self._d_acc = self._gp_step(real, noise)
             self._g_acc = self._generator_step(noise).reshape(1)
         self.iteration += 1

@@ -105,3 +105,29 @@ def test_cli_train_generate_eval(tmp_path):
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stdout)
     assert set(res) == {"wasserstein", "lp_dist"} and all(np.isfinite(v) for v in res.values())
+
+
+def test_trace_ranges_and_profile(tmp_path):
+    """Phase ranges (utils/trace.py): no-op unless enabled; profile_steps exports a Chrome trace
+    whose events include the trainer's phase names."""
+    import json
+
+    import numpy as np
+    import torch
+
+    from hfrep.train.gan_trainer import GANConfig, GANTrainer
+    from hfrep.utils import trace
+
+    with trace.trange("nothing"):  # disabled: plain pass-through
+        pass
+    ds = np.random.RandomState(0).rand(64, 12, 8).astype(np.float32)
+    tr = GANTrainer(GANConfig(arch="lstm", loss="wgan_gp", window=12, features=8, batch_size=4, dtype="float64"), ds,
+                    param_dtype=torch.float64)
+    out = tmp_path / "trace.json"
+    table = trace.profile_steps(tr.train_step, 1, str(out))
+    names = {e.get("name") for e in json.loads(out.read_text())["traceEvents"]}
+    for phase in ("critic/sample", "critic/w_terms", "critic/gp_input_grad", "critic/gp_second_order", "optimizer",
+                  "generator"):
+        assert phase in names, phase
+    assert "critic/w_terms" in table
+    assert not trace.enabled()
