@@ -1092,6 +1092,18 @@ lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 // 32x32 layout written by lstm_fwd2 / lstm_tfwd2: a 16x16 accumulator lane's four rows of one
 // 16-row block are four contiguous values of one 32x32 lane's slot half (one 8-byte load).
 // ==========================================================================================
+// a K extent as full 32-wide k-steps plus at most one 16-wide tail step (v_mfma_f32_16x16x16_bf16):
+// K = 100 -> 3 x 32 + 16 = 112 instead of 128 (fewer fragment registers and MFMAs)
+template <int KD>
+struct KSplit {
+  static constexpr bool TAIL = KD > 0 && (KD % 32) != 0 && (KD % 32) <= 16;
+  static constexpr int NF = KD > 0 ? (TAIL ? KD / 32 : (KD + 31) / 32) : 4;  // (KD = 0: runtime K <= 128)
+  static constexpr int KP = 32 * NF + (TAIL ? 16 : 0);
+};
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mma16k16(const bf16x4& a, const bf16x4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
 struct Slot8 {  // 8 bf16 of one 16x16-layout lane: block m = 0, 1 (rows 16 m + 4 (lane >> 4) + i)
   uint2 m0, m1;
   __device__ __forceinline__ float get(int m, int i) const {
@@ -1172,7 +1184,9 @@ struct Tile8w {
 
 template <int H>
 struct Tb4Geo {
-  static constexpr int G = 4 * H, NK = (G + 31) / 32, LG = NK * 32 + 8, LH = ((H + 3) / 4) * 4 + 4;
+  // the gate axis as full 32-wide k-steps + a 16-wide tail: G = 400 -> 12 x 32 + 16, no padding
+  static constexpr int G = 4 * H, NK = KSplit<G>::NF, KP = KSplit<G>::KP, LG = KP + 8, LH = ((H + 3) / 4) * 4 + 4;
+  static constexpr bool TAIL = KSplit<G>::TAIL;
   static constexpr int NCW = (H + 15) / 16;  // compute waves
   static_assert(NCW <= 7, "tbwd4: H <= 112 (7 compute waves + 1 data wave)");
   static constexpr size_t smem = (size_t)(4 * 32 * LG + 4 * 32 * LH) * 2;
@@ -1187,7 +1201,8 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
                   const bf16_t* __restrict__ hdd, const float* __restrict__ hw) {
   constexpr int act = ACT;
   using Geo = Tb4Geo<H>;
-  constexpr int G = Geo::G, NK = Geo::NK, LG = Geo::LG, LH = Geo::LH;
+  constexpr int G = Geo::G, NK = Geo::NK, KP = Geo::KP, LG = Geo::LG, LH = Geo::LH;
+  constexpr bool TAIL = Geo::TAIL;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* zb = reinterpret_cast<bf16_t*>(smem);  // [2][32][LG]  dz_t
   bf16_t* zdb = zb + 2 * 32 * LG;                 // [2][32][LG]  dzdot_t
@@ -1195,12 +1210,14 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
   bf16_t* dhdb = dhb + 2 * 32 * LH;               // [2][32][LH]  dHdot_t
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nrb = (B + 31) / 32;
-  // the K padding columns [G, 32 NK) of the dz tiles are read by the last MFMA k-step: zero them
+  // K padding columns [G, KP) of the dz tiles (if any) are read by the last MFMA k-step: zero them
   // once (nothing writes them afterwards; garbage there could be a NaN times a zero fragment)
-  for (int i = threadIdx.x; i < 4 * 32 * (32 * NK - G); i += 512) {
-    const int buf = i / (32 * (32 * NK - G)), rem = i - buf * 32 * (32 * NK - G);
-    const int r = rem / (32 * NK - G), c = G + rem - r * (32 * NK - G);
-    zb[buf * 32 * LG + r * LG + c] = 0;  // buf 0..3 spans zb[0..1] and zdb[0..1]
+  if constexpr (KP > G) {
+    for (int i = threadIdx.x; i < 4 * 32 * (KP - G); i += 512) {
+      const int buf = i / (32 * (KP - G)), rem = i - buf * 32 * (KP - G);
+      const int r = rem / (KP - G), c = G + rem - r * (KP - G);
+      zb[buf * 32 * LG + r * LG + c] = 0;  // buf 0..3 spans zb[0..1] and zdb[0..1]
+    }
   }
 
   if (wave < Geo::NCW) {
@@ -1210,6 +1227,7 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
     const int wt32 = __builtin_amdgcn_readfirstlane(wave >> 1);  // the 32x32 tape wave holding unit c
     const int lo8 = (32 * (g4 & 1) + (c & 31)) * 8 + 4 * (g4 >> 1);
     bf16x8 ut[NK];
+    bf16x4 ut4;  // 16-wide tail step (4 values per lane: k = 32 NK + 4 (lane >> 4) + j)
 #pragma unroll
     for (int ks = 0; ks < NK; ++ks)
 #pragma unroll
@@ -1218,8 +1236,14 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
         const float v = U[(size_t)(uok ? c : H - 1) * G + min(k, G - 1)];
         ut[ks][j] = (short)f2bf((uok && k < G) ? v : 0.f);
       }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 32 * NK + 4 * g4 + j;
+      ut4[j] = (short)f2bf((TAIL && uok && k < G) ? U[(size_t)(uok ? c : H - 1) * G + min(k, G - 1)] : 0.f);
+    }
     const bool xw = DX && 16 * wave < K;  // this wave owns input columns (wave-uniform)
     bf16x8 wt[DX ? NK : 1];
+    bf16x4 wt4;
     if constexpr (DX) {
 #pragma unroll
       for (int ks = 0; ks < NK; ++ks)
@@ -1229,6 +1253,11 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
           const float v = W[(size_t)min(c, K - 1) * G + min(k, G - 1)];
           wt[ks][j] = (short)f2bf((c < K && k < G) ? v : 0.f);
         }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 32 * NK + 4 * g4 + j;
+        wt4[j] = (short)f2bf((TAIL && c < K && k < G) ? W[(size_t)min(c, K - 1) * G + min(k, G - 1)] : 0.f);
+      }
     }
     for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
       const int row0 = rb * 32, nr = min(32, B - row0);
@@ -1261,8 +1290,10 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
         if (live) {
 #pragma unroll
           for (int m = 0; m < 2; ++m) {
-            const bf16_t* arow = zb + nb * 32 * LG + (16 * m + (lane & 15)) * LG + 8 * g4;
-            const bf16_t* drow = zdb + nb * 32 * LG + (16 * m + (lane & 15)) * LG + 8 * g4;
+            const bf16_t* rowz = zb + nb * 32 * LG + (16 * m + (lane & 15)) * LG;
+            const bf16_t* rowd = zdb + nb * 32 * LG + (16 * m + (lane & 15)) * LG;
+            const bf16_t* arow = rowz + 8 * g4;
+            const bf16_t* drow = rowd + 8 * g4;
             if (xw) {
 #pragma unroll
               for (int ks = 0; ks < NK; ++ks) {
@@ -1275,11 +1306,25 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
                   axd[m] = mma16(ad, wt[ks], axd[m]);
                 }
               }
+              if constexpr (TAIL) {
+                const bf16x4 a = *reinterpret_cast<const bf16x4*>(rowz + 32 * NK + 4 * g4);
+                const bf16x4 ad = *reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4);
+                ah[m] = mma16k16(a, ut4, ah[m]);
+                ahd[m] = mma16k16(ad, ut4, ahd[m]);
+                if constexpr (DX) {
+                  ax[m] = mma16k16(a, wt4, ax[m]);
+                  axd[m] = mma16k16(ad, wt4, axd[m]);
+                }
+              }
             } else {
 #pragma unroll
               for (int ks = 0; ks < NK; ++ks) {
                 ah[m] = mma16(*reinterpret_cast<const bf16x8*>(arow + 32 * ks), ut[ks], ah[m]);
                 ahd[m] = mma16(*reinterpret_cast<const bf16x8*>(drow + 32 * ks), ut[ks], ahd[m]);
+              }
+              if constexpr (TAIL) {
+                ah[m] = mma16k16(*reinterpret_cast<const bf16x4*>(rowz + 32 * NK + 4 * g4), ut4, ah[m]);
+                ahd[m] = mma16k16(*reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4), ut4, ahd[m]);
               }
             }
           }
@@ -1340,12 +1385,16 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
         for (int m = 0; m < 2; ++m) {
           ax[m] = f32x4{0.f, 0.f, 0.f, 0.f}; axd[m] = ax[m];
           if (xw) {
-            const bf16_t* arow = zb + (16 * m + (lane & 15)) * LG + 8 * g4;
-            const bf16_t* drow = zdb + (16 * m + (lane & 15)) * LG + 8 * g4;
+            const bf16_t* rowz = zb + (16 * m + (lane & 15)) * LG;
+            const bf16_t* rowd = zdb + (16 * m + (lane & 15)) * LG;
 #pragma unroll
             for (int ks = 0; ks < NK; ++ks) {
-              ax[m] = mma16(*reinterpret_cast<const bf16x8*>(arow + 32 * ks), wt[ks], ax[m]);
-              axd[m] = mma16(*reinterpret_cast<const bf16x8*>(drow + 32 * ks), wt[ks], axd[m]);
+              ax[m] = mma16(*reinterpret_cast<const bf16x8*>(rowz + 8 * g4 + 32 * ks), wt[ks], ax[m]);
+              axd[m] = mma16(*reinterpret_cast<const bf16x8*>(rowd + 8 * g4 + 32 * ks), wt[ks], axd[m]);
+            }
+            if constexpr (TAIL) {
+              ax[m] = mma16k16(*reinterpret_cast<const bf16x4*>(rowz + 32 * NK + 4 * g4), wt4, ax[m]);
+              axd[m] = mma16k16(*reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4), wt4, axd[m]);
             }
           }
         }
@@ -1411,18 +1460,6 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 // TAN = false: z = x W + h U + b, tape = gate activations + cell.  TAN = true: zdot = xdot W +
 // hdot U at the taped primal point, tape = tangent pre-activations + cell tangent.
 // ==========================================================================================
-// a K extent as full 32-wide k-steps plus at most one 16-wide tail step (v_mfma_f32_16x16x16_bf16):
-// K = 100 -> 3 x 32 + 16 = 112 instead of 128 (fewer fragment registers and MFMAs)
-template <int KD>
-struct KSplit {
-  static constexpr bool TAIL = KD > 0 && (KD % 32) != 0 && (KD % 32) <= 16;
-  static constexpr int NF = KD > 0 ? (TAIL ? KD / 32 : (KD + 31) / 32) : 4;  // (KD = 0: runtime K <= 128)
-  static constexpr int KP = 32 * NF + (TAIL ? 16 : 0);
-};
-typedef short bf16x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ f32x4 mma16k16(const bf16x4& a, const bf16x4& b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
-}
 template <int H, int KX>
 struct Fw4Geo {
   static constexpr int G = 4 * H, KPH = KSplit<H>::KP, LH = KPH + 8;

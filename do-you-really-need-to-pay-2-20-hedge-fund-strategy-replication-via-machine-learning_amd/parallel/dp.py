@@ -2,9 +2,12 @@
 
 The reference has no parallelism at all.  Here every rank runs the full GAN
 step on its own per-GPU batch (rank-seeded Philox streams), and each model's gradients — ONE
-flat fp32 buffer per model, ~0.55 MB for the LSTM critic — are averaged with a single
-all-reduce before the fused optimizer launch.  At this message size the ring is latency-bound
-(SURVEY §2.4), so there is exactly one bucket per model per step: no per-parameter collectives.
+flat fp32 buffer per model, ~0.55 MB for the LSTM critic — are averaged before the fused
+optimizer launch.  At this message size the ring is latency-bound, so the buffer
+is cut into just two buckets at layer boundaries (``Sequential.grad_buckets``): each is
+all-reduced asynchronously from the reverse pass as soon as its layers are final (the reduction
+of the last layers overlaps the backward of the first ones), and :meth:`GradSync.finish_` joins
+them before the optimizer.  No per-parameter collectives.
 
 ``torch.distributed`` with backend ``nccl`` is RCCL on ROCm; ``gloo`` is used for CPU tests.
 """
