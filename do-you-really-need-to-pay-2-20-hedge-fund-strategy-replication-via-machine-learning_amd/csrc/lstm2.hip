@@ -16,6 +16,18 @@
 //    and are streamed to/from HBM with coalesced 8-byte accesses by the whole workgroup.
 //
 // Contracts are identical to ops/reference.py (lstm_seq_*), with zx = x W + b folded in.
+//
+// File map (the production kernels are the v3 / v4 ones; v2 stays for A/B runs and as the
+// phase-timer build of the forward: HFREP_LSTM_FWD / _BWD / _TBWD = 2 select it):
+//   buffer descriptors, tile movers, tape slot I/O ........ shared device helpers
+//   lstm_fwd2 / lstm_tfwd2 / lstm_bwd2 / lstm_tbwd2 ........ v2: 32x32x16 MFMA, 32 units per wave
+//   lstm_bwd3 ............................................... BPTT: 4 recurrence + 4 data waves
+//   lstm_tbwd4 .............................................. tangent reverse: 16x16x32, 7 + 1 waves
+//   lstm_fwd4 ............................................... forward + tangent forward: 16x16x32
+//   host side ............................................... launchers, version switches
+// Every v3 / v4 kernel: one persistent workgroup per CU walking 32-row tiles, 2 waves per SIMD
+// (<= 256 VGPRs, no spills), row-major tiles moved HBM <-> LDS by the data waves, tapes in the
+// blocked 32x32-accumulator layout, buffer-descriptor (range-checked) global accesses.
 #include "common.h"
 #include "mfma.h"
 #include "kernels.h"
