@@ -69,6 +69,35 @@ __device__ __forceinline__ float act_f(int act, float x) {
     default: return x;
   }
 }
+// ---------------------------------------------------------------------------
+// Packed gate math for the recurrent step loops (VALU-issue bound: lstm_fwd4 spent ~1.8k VALU
+// issue cycles per wave per step against 1k of MFMA).  Pairs of values go through v_pk_add /
+// v_pk_mul / v_pk_fma_f32 (two fp32 lanes per instruction), and the pre-activations arrive
+// PRE-SCALED by the weights (W, U and b multiplied by -log2 e, or -2 log2 e for a tanh gate), so
+// a sigmoid is exp2 + add + rcp and a tanh is one more fma: no per-element scale, no abs /
+// copysign.  exp2 of a large argument is +inf and rcp(inf) = 0, so both saturate cleanly.
+// ---------------------------------------------------------------------------
+typedef float f2_t __attribute__((ext_vector_type(2)));
+constexpr float kLog2e = 1.4426950408889634f;
+__device__ __forceinline__ f2_t ex2_2(f2_t x) { return f2_t{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])}; }
+__device__ __forceinline__ f2_t rcp_2(f2_t x) { return f2_t{__builtin_amdgcn_rcpf(x[0]), __builtin_amdgcn_rcpf(x[1])}; }
+// sigmoid(z) from s = -log2(e) z
+__device__ __forceinline__ f2_t sig_s2(f2_t s) { return rcp_2(1.f + ex2_2(s)); }
+// tanh(z) from s = -2 log2(e) z
+__device__ __forceinline__ f2_t tanh_s2(f2_t s) { return 2.f * sig_s2(s) - 1.f; }
+// pre-scale of an activation's argument (1 for the piecewise-linear ones)
+template <int ACT>
+__device__ constexpr float act_prescale() {
+  return ACT == ACT_TANH ? -2.f * kLog2e : ACT == ACT_SIGMOID ? -kLog2e : 1.f;
+}
+// act(z) from the pre-scaled s = act_prescale<ACT>() z
+template <int ACT>
+__device__ __forceinline__ f2_t act_s2(f2_t s) {
+  if constexpr (ACT == ACT_TANH) return tanh_s2(s);
+  else if constexpr (ACT == ACT_SIGMOID) return sig_s2(s);
+  else return f2_t{act_f(ACT, s[0]), act_f(ACT, s[1])};
+}
+
 // derivative expressed through the activation OUTPUT y (all supported acts allow it)
 __device__ __forceinline__ float act_dy(int act, float y) {
   switch (act) {

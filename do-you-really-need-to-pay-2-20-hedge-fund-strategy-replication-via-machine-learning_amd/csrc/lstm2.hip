@@ -1472,58 +1472,83 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 // TAN = false: z = x W + h U + b, tape = gate activations + cell.  TAN = true: zdot = xdot W +
 // hdot U at the taped primal point, tape = tangent pre-activations + cell tangent.
 // ==========================================================================================
+// One step's tape image of a row block (NW2 x TAPE_SLOTS slots of 2 KiB, already in the global
+// blocked layout) LDS -> HBM by ONE wave: 16-byte lane stores, each wave instruction one contiguous
+// KiB.  The compute waves used to store their own 8-byte pieces (two 256-byte runs per instruction):
+// those stores ran at 4.8 TB/s against 6.1 for 16-byte ones (scripts/probes/store_probe.hip) and,
+// worse, stalled the compute waves at issue, so tape traffic and the recurrence did not overlap.
+// Lanes of padded units (unit >= H) get the out-of-range offset: no bytes written for them.
+constexpr int FW4_STAGE = NW2 * TAPE_SLOTS * SLOT_ELEMS;
+template <int H>
+__device__ __forceinline__ void tape_image_store(const bf16_t* img, rsrc_t rt, int t, bool on, int lane) {
+  constexpr int NCH = FW4_STAGE / 512, G = 5;  // 1 KiB chunks, stored in groups of G
+  static_assert(NCH % G == 0, "chunk groups");
+  const int base = t * FW4_STAGE * 2 + lane * 16;
+#pragma unroll
+  for (int g = 0; g < NCH; g += G) {
+    v4i d[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) d[j] = *reinterpret_cast<const v4i*>(img + (g + j) * 512 + lane * 8);
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int ch = g + j, w = ch / (TAPE_SLOTS * 2);
+      const bool ok = on && 32 * w + (lane & 31) < H;
+      // 16-byte store: the whole offset in voffset, soffset 0 (see the store-data hazard note)
+      __builtin_amdgcn_raw_buffer_store_b128(d[j], rt, ok ? base + ch * 1024 : kOOB, 0, 0);
+    }
+  }
+}
+
 template <int H, int KX>
 struct Fw4Geo {
   static constexpr int G = 4 * H, KPH = KSplit<H>::KP, LH = KPH + 8;
 };
-// x tile loader of the data wave: XJ chunks per lane (8-byte chunks if K % 4 == 0, else 2-byte)
-template <int KX>
-struct XTile {
+// x tile loader, split over the NP compute waves: part p moves chunks j = p, p + NP, ... of the
+// tile (8-byte chunks if K % 4 == 0, else 2-byte), i.e. one to three loads per lane per step.
+// The per-lane global / LDS offsets do not depend on the step: they are computed once per row
+// block (set), so the step loop holds no integer division and no lane-dependent branch (an
+// exec-masked form let the compiler sink the loads into divergent blocks and corrupt values of
+// the tangent forward).  Chunks past the tile load from kOOB (zeros) into an LDS trash word.
+template <int KX, int NP>
+struct XPart {
   static constexpr bool VEC = KX > 0 && KX % 4 == 0;
-  static constexpr int NJ = VEC ? (32 * (KX / 4) + 63) / 64 : (32 * (KX ? KX : 128) + 63) / 64;
-  uint32_t v[VEC ? 2 * NJ : (NJ + 1) / 2];
-  __device__ __forceinline__ void load(rsrc_t rx, int Tn, int t, bool on, int K, int lane) {
-    if constexpr (VEC) {
-      constexpr int K4 = KX / 4;
+  static constexpr int NJT = VEC ? (32 * (KX / 4) + 63) / 64 : (32 * (KX ? KX : 128) + 63) / 64;  // whole tile
+  static constexpr int NJ = (NJT + NP - 1) / NP;                                                  // this part
+  uint32_t v[VEC ? 2 * NJ : NJ];
+  int goff[NJ], loff[NJ];  // byte offset in the row tile at t = 0 (kOOB: none); LDS element offset (-1: trash)
+  __device__ __forceinline__ void set(int Tn, int K, int p, int lane) {
+    if constexpr (KX > 0) K = KX;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int e = lane + 64 * j;
-        const int r = e / K4, c = e - r * K4;
-        const v2i d = __builtin_amdgcn_raw_buffer_load_b64(rx, (on && r < 32) ? (r * Tn * KX + 4 * c) * 2 : kOOB,
-                                                           t * KX * 2, 0);
-        v[2 * j] = (uint32_t)d[0];
-        v[2 * j + 1] = (uint32_t)d[1];
-      }
-    } else {
-      if constexpr (KX > 0) K = KX;
+    for (int jj = 0; jj < NJ; ++jj) {
+      const int j = p + NP * jj, e = lane + 64 * j;
+      const int per = VEC ? K / 4 : K, w = VEC ? 4 : 1;
+      const int r = e / per, c = e - r * per;
+      const bool ok = j < NJT && r < 32;
+      goff[jj] = ok ? (r * Tn * K + w * c) * 2 : kOOB;
+      loff[jj] = ok ? (r << 16) | (w * c) : -1;
+    }
+  }
+  __device__ __forceinline__ void load(rsrc_t rx, int t, bool on, int K) {
+    if constexpr (KX > 0) K = KX;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int e = lane + 64 * j;
-        const int r = e / K, k = e - r * K;
-        const uint32_t d = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(
-            rx, (on && r < 32) ? (r * Tn * K + k) * 2 : kOOB, t * K * 2, 0);
-        if (j & 1) v[j >> 1] |= d << 16;
-        else v[j >> 1] = d;
+    for (int jj = 0; jj < NJ; ++jj) {
+      const int vo = on ? goff[jj] : kOOB;
+      if constexpr (VEC) {
+        const v2i d = __builtin_amdgcn_raw_buffer_load_b64(rx, vo, t * K * 2, 0);
+        v[2 * jj] = (uint32_t)d[0];
+        v[2 * jj + 1] = (uint32_t)d[1];
+      } else {
+        v[jj] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rx, vo, t * K * 2, 0);
       }
     }
   }
-  __device__ __forceinline__ void to_lds(bf16_t* xb, int LX, int K, int lane) const {
-    if constexpr (VEC) {
-      constexpr int K4 = KX / 4;
+  __device__ __forceinline__ void to_lds(bf16_t* xb, bf16_t* trash, int LX) const {
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int e = lane + 64 * j;
-        const int r = e / K4, c = e - r * K4;
-        if (r < 32) *reinterpret_cast<uint2*>(xb + r * LX + 4 * c) = make_uint2(v[2 * j], v[2 * j + 1]);
-      }
-    } else {
-      if constexpr (KX > 0) K = KX;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int e = lane + 64 * j;
-        const int r = e / K, k = e - r * K;
-        if (r < 32) xb[r * LX + k] = (bf16_t)((j & 1) ? (v[j >> 1] >> 16) : (v[j >> 1] & 0xffffu));
-      }
+    for (int jj = 0; jj < NJ; ++jj) {
+      const int lo = loff[jj];
+      bf16_t* dst = lo >= 0 ? xb + (lo >> 16) * LX + (lo & 0xffff) : trash;
+      if constexpr (VEC) *reinterpret_cast<uint2*>(dst) = make_uint2(v[2 * jj], v[2 * jj + 1]);
+      else *dst = (bf16_t)v[jj];
     }
   }
 };
@@ -1532,7 +1557,7 @@ template <int H, int ACT, int KX, bool TAPE, bool TAN>
 __global__ void __launch_bounds__(512)
 lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
                  const float* __restrict__ U, const bf16_t* __restrict__ ptape, bf16_t* __restrict__ hs,
-                 bf16_t* __restrict__ tape, int B, int Tn, int K_rt) {
+                 bf16_t* __restrict__ tape, int B, int Tn, int K_rt, int dbg) {
   constexpr int act = ACT;
   using Geo = Fw4Geo<H, KX>;
   using KS = KSplit<KX>;
@@ -1545,6 +1570,8 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* xb = reinterpret_cast<bf16_t*>(smem);  // [2][32][LX]
   bf16_t* hb = xb + 2 * 32 * LX;                  // [2][32][LH]
+  bf16_t* tsg = hb + 2 * 32 * LH;                 // TAPE: [2][NW2 x TAPE_SLOTS x SLOT_ELEMS] step images
+  bf16_t* trash = tsg + (TAPE ? 2 * FW4_STAGE : 0);  // 16 bytes nobody reads
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nrb = (B + 31) / 32;
   // K / H padding columns of both tile buffers stay zero (the data wave writes K columns, the
@@ -1564,15 +1591,18 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
     constexpr int NKXM = KS::NF, NKH = HS::NF;
     bf16x8 wf[4][NKXM], uf[4][NKH];
     bf16x4 wf4[4], uf4[4];
+    // forward: gate q's weights and bias are pre-scaled for the packed gate math (act_s2)
+    constexpr float SIG = act_prescale<ACT_SIGMOID>(), GSC = act_prescale<ACT>();
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      const float sc = TAN ? 1.f : (q == 2 ? GSC : SIG);
 #pragma unroll
       for (int ks = 0; ks < NKXM; ++ks)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int k = 32 * ks + 8 * g4 + j;
           const float v = W[(size_t)min(k, K - 1) * G + q * H + cc_];
-          wf[q][ks][j] = (short)f2bf((uok && k < K) ? v : 0.f);
+          wf[q][ks][j] = (short)f2bf((uok && k < K) ? v * sc : 0.f);
         }
 #pragma unroll
       for (int ks = 0; ks < NKH; ++ks)
@@ -1580,23 +1610,22 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
         for (int j = 0; j < 8; ++j) {
           const int k = 32 * ks + 8 * g4 + j;
           const float v = U[(size_t)min(k, H - 1) * G + q * H + cc_];
-          uf[q][ks][j] = (short)f2bf((uok && k < H) ? v : 0.f);
+          uf[q][ks][j] = (short)f2bf((uok && k < H) ? v * sc : 0.f);
         }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int kx = 32 * NKXM + 4 * g4 + j, kh = 32 * NKH + 4 * g4 + j;
         const float vx = W[(size_t)min(kx, K - 1) * G + q * H + cc_];
         const float vh = U[(size_t)min(kh, H - 1) * G + q * H + cc_];
-        wf4[q][j] = (short)f2bf((KS::TAIL && uok && kx < K) ? vx : 0.f);
-        uf4[q][j] = (short)f2bf((HS::TAIL && uok && kh < H) ? vh : 0.f);
+        wf4[q][j] = (short)f2bf((KS::TAIL && uok && kx < K) ? vx * sc : 0.f);
+        uf4[q][j] = (short)f2bf((HS::TAIL && uok && kh < H) ? vh * sc : 0.f);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
     float bq[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) bq[q] = (!TAN && uok && bias) ? bias[q * H + c] : 0.f;
+    for (int q = 0; q < 4; ++q) bq[q] = (!TAN && uok && bias) ? bias[q * H + c] * (q == 2 ? GSC : SIG) : 0.f;
     for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
-      const rsrc_t rt = tape_rsrc(TAPE ? tape : nullptr, rb, nrb, Tn);
       const rsrc_t rp = tape_rsrc(TAN ? ptape : nullptr, rb, nrb, Tn);
       float cs[8], cprev[8];
 #pragma unroll
@@ -1606,15 +1635,21 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 #pragma unroll
         for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = ld_slot8(rp, uok, lo8, tape_off(0, wt32) + s * SLOT_ELEMS);
       }
+      const rsrc_t rx = tile_rsrc(x, rb * 32, B, Tn, K);
+      XPart<KX, NCW> xp;
+      xp.set(Tn, K, wave, lane);
+      xp.load(rx, 0, true, K);
       __syncthreads();  // (A)
       // h_{-1} = 0: this wave's units of buffer 0
       if (uok)
         for (int r = 0; r < 32; r += 4) hb[(r + g4) * LH + c] = 0;
+      xp.to_lds(xb, trash, LX);
       __syncthreads();  // (B) x_0 staged, h_{-1} zeroed
       for (int t = 0; t < Tn; ++t) {
         const bf16_t* xcur = xb + (t & 1) * 32 * LX;
         const bf16_t* hcur = hb + (t & 1) * 32 * LH;
         bf16_t* hnext = hb + ((t + 1) & 1) * 32 * LH;
+        xp.load(rx, t + 1, t + 1 < Tn && !(dbg & 4), K);  // x_{t+1}: lands during this step
         if constexpr (TAN) {  // primal tape of the next step (loads only; no store precedes them)
 #pragma unroll
           for (int s = 0; s < TAPE_SLOTS; ++s)
@@ -1655,58 +1690,63 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
         for (int m = 0; m < 2; ++m) {
           uint32_t pk[TAPE_SLOTS][2];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int e = 4 * m + i, rr = 16 * m + 4 * g4 + i;
-            float v0, v1, v2, v3, v4, hv;
+          for (int p = 0; p < 2; ++p) {  // rows 16 m + 4 g4 + 2 p + {0, 1}: one packed pair
+            const int e = 4 * m + 2 * p, rr = 16 * m + 4 * g4 + 2 * p;
+            const f2_t a0 = {acc[0][m][2 * p], acc[0][m][2 * p + 1]}, a1 = {acc[1][m][2 * p], acc[1][m][2 * p + 1]};
+            const f2_t a2 = {acc[2][m][2 * p], acc[2][m][2 * p + 1]}, a3 = {acc[3][m][2 * p], acc[3][m][2 * p + 1]};
+            const f2_t cp = {cs[e], cs[e + 1]};
+            f2_t v0, v1, v2, v3, v4, hv;
             if constexpr (!TAN) {
-              const float ig = sigmoidf_(acc[0][m][i] + bq[0]), fg = sigmoidf_(acc[1][m][i] + bq[1]);
-              const float gg = act_f(act, acc[2][m][i] + bq[2]), og = sigmoidf_(acc[3][m][i] + bq[3]);
-              float cn = fg * cs[e] + ig * gg;
-              float h = og * act_f(act, cn);
-              if (!uok) { cn = 0.f; h = 0.f; }
-              cs[e] = cn;
+              // padded units (!uok): zero weights and bias give s = 0 in every gate; with a tanh cell
+              // that makes c and h exactly 0, otherwise h is masked (c is never stored for them)
+              const f2_t ig = sig_s2(a0 + bq[0]), fg = sig_s2(a1 + bq[1]);
+              const f2_t gg = act_s2<ACT>(a2 + bq[2]), og = sig_s2(a3 + bq[3]);
+              const f2_t cn = fg * cp + ig * gg;
+              f2_t h = og * act_s2<ACT>(GSC * cn);
+              if constexpr (ACT != ACT_TANH) h = uok ? h : f2_t{0.f, 0.f};
+              cs[e] = cn[0]; cs[e + 1] = cn[1];
               v0 = ig; v1 = fg; v2 = gg; v3 = og; v4 = cn; hv = h;
             } else {
-              const float ig = tg[0].get(m, i), fg = tg[1].get(m, i), gg = tg[2].get(m, i), og = tg[3].get(m, i);
-              const float cv = tg[4].get(m, i);
-              const float idot = ig * (1.f - ig) * acc[0][m][i];
-              const float fdot = fg * (1.f - fg) * acc[1][m][i];
-              const float gdot = act_dy(act, gg) * acc[2][m][i];
-              const float odot = og * (1.f - og) * acc[3][m][i];
-              float cdn = fdot * cprev[e] + fg * cs[e] + idot * gg + ig * gdot;
-              const float ca = act_f(act, cv);
-              float hd = odot * ca + og * act_dy(act, ca) * cdn;
-              if (!uok) { cdn = 0.f; hd = 0.f; }
-              cs[e] = cdn;
-              cprev[e] = cv;
-              v0 = acc[0][m][i]; v1 = acc[1][m][i]; v2 = acc[2][m][i]; v3 = acc[3][m][i]; v4 = cdn; hv = hd;
-            }
-            if (uok) hnext[rr * LH + c] = f2bf(hv);
-            if constexpr (TAPE) {
-              const int h2 = i >> 1;
-              if (i & 1) {
-                pk[0][h2] |= (uint32_t)f2bf(v0) << 16; pk[1][h2] |= (uint32_t)f2bf(v1) << 16;
-                pk[2][h2] |= (uint32_t)f2bf(v2) << 16; pk[3][h2] |= (uint32_t)f2bf(v3) << 16;
-                pk[4][h2] |= (uint32_t)f2bf(v4) << 16;
-              } else {
-                pk[0][h2] = f2bf(v0); pk[1][h2] = f2bf(v1); pk[2][h2] = f2bf(v2); pk[3][h2] = f2bf(v3);
-                pk[4][h2] = f2bf(v4);
+              f2_t hd2, cd2;
+#pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                const int i = 2 * p + u;
+                const float ig = tg[0].get(m, i), fg = tg[1].get(m, i), gg = tg[2].get(m, i), og = tg[3].get(m, i);
+                const float cv = tg[4].get(m, i);
+                const float idot = ig * (1.f - ig) * acc[0][m][i];
+                const float fdot = fg * (1.f - fg) * acc[1][m][i];
+                const float gdot = act_dy(act, gg) * acc[2][m][i];
+                const float odot = og * (1.f - og) * acc[3][m][i];
+                float cdn = fdot * cprev[e + u] + fg * cs[e + u] + idot * gg + ig * gdot;
+                const float ca = act_f(act, cv);
+                float hd = odot * ca + og * act_dy(act, ca) * cdn;
+                if (!uok) { cdn = 0.f; hd = 0.f; }
+                cs[e + u] = cdn;
+                cprev[e + u] = cv;
+                cd2[u] = cdn; hd2[u] = hd;
               }
+              v0 = a0; v1 = a1; v2 = a2; v3 = a3; v4 = cd2; hv = hd2;
+            }
+            // unconditional: padded unit columns (c in [H, 112)) receive the zeros they must hold
+            hnext[rr * LH + c] = f2bf(hv[0]);
+            hnext[(rr + 1) * LH + c] = f2bf(hv[1]);
+            if constexpr (TAPE) {
+              pk[0][p] = pk2bf(v0[0], v0[1]); pk[1][p] = pk2bf(v1[0], v1[1]); pk[2][p] = pk2bf(v2[0], v2[1]);
+              pk[3][p] = pk2bf(v3[0], v3[1]); pk[4][p] = pk2bf(v4[0], v4[1]);
             }
           }
-          if constexpr (TAPE) {
-            const int v = uok ? lo8 * 2 : kOOB;
+          if constexpr (TAPE) {  // into this step's image; the data wave streams it out next step
+            bf16_t* img = tsg + (t & 1) * FW4_STAGE + tape_off(0, wt32) + m * SLOT_HALF + lo8;
 #pragma unroll
-            for (int s = 0; s < TAPE_SLOTS; ++s) {
-              const v2i d = {(int)pk[s][0], (int)pk[s][1]};
-              __builtin_amdgcn_raw_buffer_store_b64(d, rt, v, (tape_off(t, wt32) + s * SLOT_ELEMS + m * SLOT_HALF) * 2, 0);
-            }
+            for (int s = 0; s < TAPE_SLOTS; ++s)
+              *reinterpret_cast<v2i*>(img + s * SLOT_ELEMS) = v2i{(int)pk[s][0], (int)pk[s][1]};
           }
         }
         if constexpr (TAN) {
 #pragma unroll
           for (int s = 0; s < TAPE_SLOTS; ++s) tg[s] = tn[s];
         }
+        xp.to_lds(xb + ((t + 1) & 1) * 32 * LX, trash, LX);  // (the last step's is unused)
         lds_barrier();  // step hand-off
       }
       __syncthreads();  // (C) the data wave has stored h_{T-1}
@@ -1714,19 +1754,22 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
   } else if (wave == 7) {
     for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
       const int row0 = rb * 32;
-      const rsrc_t rx = tile_rsrc(x, row0, B, Tn, K), rh = tile_rsrc(hs, row0, B, Tn, H);
-      XTile<KX> xt;
-      xt.load(rx, Tn, 0, true, K, lane);
+      const rsrc_t rh = tile_rsrc(hs, row0, B, Tn, H);
+      const rsrc_t rt = tape_rsrc(TAPE ? tape : nullptr, rb, nrb, Tn);
+      const bool ton = !(dbg & 1);
       __syncthreads();  // (A)
-      xt.to_lds(xb, LX, K, lane);
       __syncthreads();  // (B)
+      // stores only: with no load of its own this wave never waits on vmcnt (which retires loads
+      // and stores in issue order), so the tape / h stream runs beside the recurrence
       for (int t = 0; t < Tn; ++t) {
-        xt.load(rx, Tn, t + 1, t + 1 < Tn, K, lane);  // loads first
-        tile8_store_w<H>(hb + (t & 1) * 32 * LH, LH, rh, Tn, t - 1, t > 0, lane);
-        if (t + 1 < Tn) xt.to_lds(xb + ((t + 1) & 1) * 32 * LX, LX, K, lane);
+        tile8_store_w<H>(hb + (t & 1) * 32 * LH, LH, rh, Tn, t - 1, t > 0 && !(dbg & 2), lane);
+        if constexpr (TAPE)
+          tape_image_store<H>(tsg + ((t + 1) & 1) * FW4_STAGE, rt, (dbg & 256) ? 0 : t - 1, t > 0 && ton, lane);
         lds_barrier();
       }
       tile8_store_w<H>(hb + (Tn & 1) * 32 * LH, LH, rh, Tn, Tn - 1, true, lane);
+      if constexpr (TAPE)
+        tape_image_store<H>(tsg + ((Tn - 1) & 1) * FW4_STAGE, rt, (dbg & 256) ? 0 : Tn - 1, ton, lane);
       __syncthreads();  // (C)
     }
   } else {
@@ -1796,6 +1839,7 @@ static void launch(Kern k, int grid, int threads, size_t smem, hipStream_t s, Ar
 // row tiles per workgroup for the fwd / bwd kernels (HFREP_LSTM_TILES=1 or 2, default 2)
 // timing-only ablation mask for the forward kernel (HFREP_LSTM_DBG; 0 in every real run):
 // 1 no tape store, 2 no h store, 4 no x load, 8 no MFMA, 16 no h LDS write, 32 no step barrier
+// (v4 forward: 1, 2, 4 and 256 = every step's tape stores to step 0's slots, i.e. L2-resident)
 static int lstm_dbg() {
   static int d = -1;
   if (d < 0) {
@@ -1822,9 +1866,9 @@ static int lstm_fwd_version() {  // HFREP_LSTM_FWD=2: the v2 forward / tangent f
   }
   return v;
 }
-static size_t fwd4_smem(int H, int K) {  // generous: the 32-rounded extents (>= the tail-split ones)
+static size_t fwd4_smem(int H, int K, bool tape) {  // generous: the 32-rounded extents (>= the tail-split ones)
   const int LX = ((K + 31) & ~31) + 8, LH = ((H + 31) / 32) * 32 + 8;
-  return (size_t)(2 * 32 * LX + 2 * 32 * LH) * 2;
+  return (size_t)(2 * 32 * LX + 2 * 32 * LH + (tape ? 2 * FW4_STAGE : 0) + 8) * 2;  // + trash
 }
 #define HFREP_FWD4_ACT(KXV, TP, TN, ...)                                                          \
   switch (act) {                                                                                 \
@@ -1846,12 +1890,12 @@ void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float
   const bf16_t* xp = (const bf16_t*)x;
   if (lstm_fwd_version() == 4 && !(lstm_dbg() & 64)) {
     const int g = persistent_grid(B, 1);
-    const size_t sm = fwd4_smem(H, K);
+    const size_t sm = fwd4_smem(H, K, tape != nullptr);
     if (tape)
-      HFREP_FWD4_K(true, false, g, 512, sm, s, xp, W, b, U, (const bf16_t*)nullptr, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K)
+      HFREP_FWD4_K(true, false, g, 512, sm, s, xp, W, b, U, (const bf16_t*)nullptr, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
     else
       HFREP_FWD4_K(false, false, g, 512, sm, s, xp, W, b, U, (const bf16_t*)nullptr, (bf16_t*)hs, (bf16_t*)nullptr, B,
-                   Tn, K)
+                   Tn, K, lstm_dbg())
     return;
   }
   if (K == 100 && (lstm_dbg() & 64) && act == 2) {  // diagnostic phase-timer build
@@ -1882,8 +1926,8 @@ void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const voi
   const bf16_t* xp = (const bf16_t*)xd;
   if (lstm_fwd_version() == 4) {
     const int g = persistent_grid(B, 1);
-    HFREP_FWD4_K(true, true, g, 512, fwd4_smem(H, K), s, xp, W, (const float*)nullptr, U, (const bf16_t*)tape,
-                 (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
+    HFREP_FWD4_K(true, true, g, 512, fwd4_smem(H, K, true), s, xp, W, (const float*)nullptr, U, (const bf16_t*)tape,
+                 (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K, lstm_dbg())
     return;
   }
   const int g = persistent_grid(B, 1);

@@ -51,6 +51,7 @@ def main():
     dZ_ = Fn.lstm_layer_bwd(dH, tape, U, a.act)
     ops = {
         "fwd": lambda: Fn.lstm_layer_fwd(x, W, b, U, a.act, True),
+        "fwd_notape": lambda: Fn.lstm_layer_fwd(x, W, b, U, a.act, False),
         "tfwd": lambda: Fn.lstm_layer_tfwd(xd, W, tape, U, a.act),
         "bwd": lambda: Fn.lstm_layer_bwd(dH, tape, U, a.act),
         "tbwd": lambda: Fn.lstm_layer_tbwd(dH, dHd, tape, ttape, U, a.act),
