@@ -20,7 +20,13 @@ U = torch.randn(H, 4 * H, generator=g) * (1.0 / H ** 0.5)
 hs, tape = Fn.lstm_layer_fwd(x.to(dev), W.to(dev), b.to(dev), U.to(dev), act, True)
 zx = x.double() @ W.double() + b.double()
 rh, rg, rc = R.lstm_seq_fwd(zx, U.double(), act)
-print("fwd err", (hs.double().cpu() - rh).abs().max().item())
+ef = (hs.double().cpu() - rh).abs()
+print("fwd err", ef.max().item())
+badf = (ef > 0.05).nonzero()
+if badf.shape[0]:
+    print("fwd bad rows", sorted(set(badf[:, 0].tolist()))[:40])
+    print("fwd bad steps", sorted(set(badf[:, 1].tolist())))
+    print("fwd bad units", sorted(set(badf[:, 2].tolist()))[:60])
 xd = (torch.randn(B, T, K, generator=g) * 0.3).to(torch.bfloat16)
 hds, ttape = Fn.lstm_layer_tfwd(xd.to(dev), W.to(dev), tape, U.to(dev), act)
 th, tz, tc = R.lstm_seq_tfwd(xd.double() @ W.double(), rg, rc, U.double(), act)

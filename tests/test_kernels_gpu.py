@@ -522,6 +522,10 @@ def test_lstm2_head_adjoint_in_kernel(cuda):
         for seeds, mats in (((None, oad), (None, dHdm)), ((oa, oad), (dHm, dHdm))):
             t1 = Fn.lstm_layer_tbwd(seeds[0], seeds[1], tape, ttape, U, act, W=Wx)
             t2 = Fn.lstm_layer_tbwd(mats[0], mats[1], tape, ttape, U, act, W=Wx)
+            # run-to-run bitwise (the generated-adjoint DX instantiation was not: stale accumulator
+            # reads; it is no longer dispatched, functional.lstm_layer_tbwd)
+            t1b = Fn.lstm_layer_tbwd(seeds[0], seeds[1], tape, ttape, U, act, W=Wx)
+            assert all(torch.equal(a, c) for a, c in zip(t1, t1b))
             # (the GEN and tensor-fed instantiations may contract the gate math differently: 1-ulp
             # bf16 differences that the recurrence carries back, so compare at bf16 tolerance)
             for a, c in zip(t1, t2):
