@@ -125,7 +125,7 @@ def main():
             "losses_finite": bool(finite),
             # the W-dist half of the metric is a training-quality run, not a throughput step:
             # `python -m hfrep parity` (fp32 vs bf16, B=32 vs 4096) -> profiles/r01_parity
-            "w_dist_parity": "profiles/r01_parity/README.md",
+            "w_dist_parity": "profiles/r01_parity3/README.md",
             "peak_mem_gb_rank0": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
         }
         print(json.dumps(rec))
