@@ -457,6 +457,21 @@ std::tuple<Tensor, Tensor> gp_coef(Tensor g, double weight) {
   return {pen, v};
 }
 
+// (segment losses [2] fp32, dL/dp like p): see csrc/misc.hip gan_loss_kernel
+std::tuple<Tensor, Tensor> gan_loss(Tensor p, int64_t split, double la, double lb, int64_t kind) {
+  CHECK_GPU(p); GUARD(p);
+  TORCH_CHECK(p.is_contiguous(), "gan_loss: contiguous scores");
+  TORCH_CHECK(kind == 0 || kind == 1, "gan_loss: kind 0 (wasserstein) or 1 (bce)");
+  const int64_t n = p.numel();
+  TORCH_CHECK(split >= 0 && split <= n, "gan_loss: split");
+  Tensor grad = out_empty_like(p);
+  Tensor out = out_empty({2}, p.options().dtype(at::kFloat));
+  Tensor partial = at::empty({2 * hfrep::gan_loss_partials()}, p.options().dtype(at::kFloat));
+  hfrep::launch_gan_loss(dt_of(p), p.data_ptr(), n, split, (float)la, (float)lb, (int)kind, grad.data_ptr(),
+                         partial.data_ptr<float>(), out.data_ptr<float>(), cur_stream(p));
+  return {out, grad};
+}
+
 Tensor interpolate(Tensor real, Tensor fake, Tensor alpha) {
   CHECK_GPU(real); CHECK_GPU(fake); same_dt(real, fake); CHECK_F32(alpha);
   TORCH_CHECK(real.sizes() == fake.sizes() && alpha.numel() == real.size(0), "interpolate: shapes");
@@ -558,6 +573,7 @@ TORCH_LIBRARY(hfrep, m) {
         "(Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, Tensor(a!)? ggamma, Tensor(b!)? gbeta) -> Tensor");
   m.def("gp_coef(Tensor g, float weight) -> (Tensor, Tensor)");
+  m.def("gan_loss(Tensor p, int split, float la, float lb, int kind) -> (Tensor, Tensor)");
   m.def("im2col_causal(Tensor x, int k, int dil) -> Tensor");
   m.def("col2im_causal(Tensor dcols, int k, int dil, int C) -> Tensor");
   m.def("interpolate(Tensor real, Tensor fake, Tensor alpha) -> Tensor");
@@ -589,6 +605,7 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("layernorm_bwd_", &layernorm_bwd_);
   m.impl("gp_coef", &gp_coef);
+  m.impl("gan_loss", &gan_loss);
   m.impl("im2col_causal", &im2col_causal);
   m.impl("col2im_causal", &col2im_causal);
   m.impl("interpolate", &interpolate);

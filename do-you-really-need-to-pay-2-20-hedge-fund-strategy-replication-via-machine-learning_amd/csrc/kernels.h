@@ -98,6 +98,9 @@ int layernorm_bwd_splits(int64_t rows);
 void launch_layernorm_bwd(int dt, const void* dy, const void* xhat, const float* rstd, const float* gamma,
                           void* dx, float* ggamma, float* gbeta, float* ws, int64_t rows, int D, hipStream_t s);
 // v = dGP/dg per row, pen += sum_b (1 - |g_b|)^2 / B  (rowpen: B floats of workspace)
+void launch_gan_loss(int dt, const void* p, int64_t n, int64_t split, float la, float lb, int kind, void* grad,
+                     float* partial, float* out, hipStream_t s);
+int gan_loss_partials();
 void launch_gp_coef(int dt, const void* g, void* v, float* pen, float* rowpen, int B, int64_t D, float weight,
                     hipStream_t s);
 void launch_interpolate(int dt, const void* real, const void* fake, const float* alpha, void* out, int B,

@@ -7,6 +7,7 @@
 // (GAN/MTSS_WGAN_GP.py:191-199) with a per-sample alpha of ANY batch size.
 #include "common.h"
 #include "kernels.h"
+#include <algorithm>
 
 namespace hfrep {
 
@@ -272,6 +273,71 @@ void launch_gp_coef(int dt, const void* g, void* v, float* pen, float* rowpen, i
                        weight);
   hipLaunchKernelGGL(sum_into_kernel, dim3(1), dim3(1024), 0, s, rowpen, B, pen);
 }
+
+// ------------------------------------------------------------------ GAN losses
+// Value and gradient of the critic / generator losses in one pass over the scores p (N rows,
+// flattened).  Elements [0, split) are segment 0 with label la, [split, n) segment 1 with label lb;
+// each segment's loss is a mean over its own element count (the W terms on [real; fake] are one
+// launch).  kind 0: Wasserstein, loss = label * p, grad = label.  kind 1: Keras binary
+// cross-entropy on probabilities (clip to [eps, 1 - eps], log(o + eps); zero gradient where the
+// clip is active).  Per-block partial sums, reduced in a fixed order: bitwise reproducible.
+constexpr int LOSS_BLOCKS = 256;
+template <typename T>
+__global__ void __launch_bounds__(256) gan_loss_kernel(const T* __restrict__ p, int64_t n, int64_t split, float la,
+                                                       float lb, int kind, T* __restrict__ grad,
+                                                       float* __restrict__ partial) {
+  __shared__ float red[4];
+  constexpr float eps = 1e-7f;
+  const float inv0 = split > 0 ? 1.f / (float)split : 0.f, inv1 = n > split ? 1.f / (float)(n - split) : 0.f;
+  float s0 = 0.f, s1 = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const bool seg0 = i < split;
+    const float y = seg0 ? la : lb, inv = seg0 ? inv0 : inv1;
+    const float x = ld_f(p + i);
+    float l, g;
+    if (kind == 0) {
+      l = y * x;
+      g = y * inv;
+    } else {
+      const float o = fminf(fmaxf(x, eps), 1.f - eps);
+      l = -(y * logf(o + eps) + (1.f - y) * logf(1.f - o + eps));
+      const bool inside = x > eps && x < 1.f - eps;
+      g = inside ? -(y / (o + eps) - (1.f - y) / (1.f - o + eps)) * inv : 0.f;
+    }
+    st_f(grad + i, g);
+    if (seg0) s0 += l * inv;
+    else s1 += l * inv;
+  }
+  s0 = block_sum<4>(s0, red);
+  __syncthreads();
+  s1 = block_sum<4>(s1, red);
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = s0;
+    partial[2 * blockIdx.x + 1] = s1;
+  }
+}
+__global__ void __launch_bounds__(256) gan_loss_reduce_kernel(const float* __restrict__ partial, int nb,
+                                                              float* __restrict__ out) {
+  __shared__ float red[4];
+  float s0 = 0.f, s1 = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) { s0 += partial[2 * i]; s1 += partial[2 * i + 1]; }
+  s0 = block_sum<4>(s0, red);
+  __syncthreads();
+  s1 = block_sum<4>(s1, red);
+  if (threadIdx.x == 0) { out[0] = s0; out[1] = s1; }
+}
+void launch_gan_loss(int dt, const void* p, int64_t n, int64_t split, float la, float lb, int kind, void* grad,
+                     float* partial, float* out, hipStream_t s) {
+  const int nb = (int)std::min<int64_t>(LOSS_BLOCKS, std::max<int64_t>(1, (n + 1023) / 1024));
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(gan_loss_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, (const bf16_t*)p, n, split, la, lb, kind,
+                       (bf16_t*)grad, partial);
+  else
+    hipLaunchKernelGGL(gan_loss_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)p, n, split, la, lb, kind,
+                       (float*)grad, partial);
+  hipLaunchKernelGGL(gan_loss_reduce_kernel, dim3(1), dim3(256), 0, s, partial, nb, out);
+}
+int gan_loss_partials() { return LOSS_BLOCKS; }
 
 // ------------------------------------------------------------------ interpolation
 template <typename T>

@@ -191,6 +191,16 @@ def col2im_causal(dcols: torch.Tensor, k: int, dil: int, C: int) -> torch.Tensor
 # ---------------------------------------------------------------------------------------
 # WGAN-GP helpers
 # ---------------------------------------------------------------------------------------
+def gan_loss(p: torch.Tensor, split: int, la: float, lb: float, kind: int):
+    """(per-segment losses [2], dL/dp) of a Wasserstein (kind 0) or BCE (kind 1) loss over the
+    scores p split into two labelled segments (one launch for the W terms on [real; fake]).
+    bf16 / fp32 on the GPU: one native pass (csrc/misc.hip gan_loss_kernel); else the reference."""
+    if _nat(p) and p.dtype in (torch.bfloat16, torch.float32):
+        return _ops().gan_loss(p.contiguous(), int(split), float(la), float(lb), int(kind))
+    return R.gan_loss(p, int(split), float(la), float(lb), int(kind),
+                      acc=torch.float64 if p.dtype == torch.float64 else torch.float32)
+
+
 def gp_coef(g: torch.Tensor, weight: float):
     """(penalty, v): penalty = mean((1-||g_b||)^2); v = d(weight*penalty)/dg."""
     if _nat(g):

@@ -157,6 +157,30 @@ def gradient_penalty_from_grad(g: torch.Tensor) -> torch.Tensor:
     return torch.mean((1 - n) ** 2)
 
 
+def gan_loss(p: torch.Tensor, split: int, la: float, lb: float, kind: int, acc=torch.float32):
+    """Contract of the native ``gan_loss`` op (csrc/misc.hip): the flattened scores p are two
+    segments, [0, split) with label ``la`` and [split, n) with label ``lb``; returns
+    (per-segment mean losses [2] in ``acc``, dL/dp like p) for L = loss_0 + loss_1.
+    kind 0: Wasserstein ``mean(y * p)`` (GAN/WGAN.py:126-127); kind 1: Keras binary cross-entropy
+    on probabilities with the [eps, 1 - eps] clip (zero gradient where the clip is active)."""
+    pf = p.reshape(-1).to(acc)
+    n = pf.numel()
+    y = torch.full_like(pf, lb)
+    y[:split] = la
+    inv = torch.full_like(pf, 1.0 / max(n - split, 1))
+    inv[:split] = 1.0 / max(split, 1)
+    if kind == 0:
+        lo, g = y * pf, y * inv
+    else:
+        o = pf.clamp(KERAS_EPS, 1 - KERAS_EPS)
+        lo = -(y * torch.log(o + KERAS_EPS) + (1 - y) * torch.log(1 - o + KERAS_EPS))
+        inside = ((pf > KERAS_EPS) & (pf < 1 - KERAS_EPS)).to(acc)
+        g = -(y / (o + KERAS_EPS) - (1 - y) / (1 - o + KERAS_EPS)) * inside * inv
+    li = lo * inv
+    out = torch.stack([li[:split].sum(), li[split:].sum()])
+    return out, g.to(p.dtype).reshape(p.shape)
+
+
 def gp_coef(g: torch.Tensor, weight: float):
     """Explicit GP adjoint: returns (penalty value, v = dL/dg) for L = weight*mean((1-||g||)^2)."""
     B = g.shape[0]

@@ -30,7 +30,6 @@ import torch
 
 from ..models import gan as zoo
 from ..ops import functional as Fn
-from ..ops import reference as R
 from ..utils.rng import DeviceRNG
 from ..utils.trace import trange
 from .optim import KerasOptimizer
@@ -142,24 +141,18 @@ class GANTrainer:
     def _bce_step(self, x, label: float):
         C = self.critic
         p, tape = C.efwd(x, save=True)
-        pf = p.to(self._acc)
-        n = pf.numel()
-        o = pf.clamp(R.KERAS_EPS, 1 - R.KERAS_EPS)
-        loss = -(label * torch.log(o + R.KERAS_EPS) + (1 - label) * torch.log(1 - o + R.KERAS_EPS)).mean()
-        inside = ((pf > R.KERAS_EPS) & (pf < 1 - R.KERAS_EPS)).to(pf.dtype)
-        dp = -(label / (o + R.KERAS_EPS) - (1 - label) / (1 - o + R.KERAS_EPS)) * inside / n
-        C.ebwd(tape, dp.to(p.dtype), hook=self._hook(C))
+        out, dp = Fn.gan_loss(p, p.numel(), label, label, 1)  # K10: value + gradient, one pass
+        C.ebwd(tape, dp, hook=self._hook(C))
         self._apply(C)
-        return loss
+        return out[0].to(self._acc)
 
     def _wgan_step(self, x, label: float, clip: float):
         C = self.critic
         s, tape = C.efwd(x, save=True)
-        loss = label * s.to(self._acc).mean()
-        ds = torch.full_like(s, label / s.numel())
+        out, ds = Fn.gan_loss(s, s.numel(), label, label, 0)
         C.ebwd(tape, ds, hook=self._hook(C))
         self._apply(C, clip=clip)
-        return loss
+        return out[0].to(self._acc)
 
     def _gp_step(self, real, noise):
         with trange("critic/generate"):
@@ -172,15 +165,13 @@ class GANTrainer:
     def critic_gp_grads(self, real, fake, alpha):
         """Accumulate d/dtheta_C of W(real,-1) + W(fake,+1) + lambda*GP(x_hat) into C.flat.grad."""
         C = self.critic
-        B = real.shape[0]
         xh = Fn.interpolate(real, fake, alpha)
         # W terms on [real; fake]
         with trange("critic/w_terms"):
             xrf = torch.cat([real, fake], 0)
             s, tape = C.efwd(xrf, save=True)
-            ds = torch.empty_like(s)
-            ds[:B] = -1.0 / B
-            ds[B:] = 1.0 / B
+            # W(real, -1) and W(fake, +1): both segment means and the score gradient in one launch
+            w, ds = Fn.gan_loss(s, s.numel() // 2, -1.0, 1.0, 0)
             C.ebwd(tape, ds)
         # gradient penalty: g = dD/dx_hat (input gradient only), v = dGP/dg, then the
         # theta-gradient of <v, g> as reverse-over-tangent
@@ -191,9 +182,9 @@ class GANTrainer:
         with trange("critic/gp_second_order"):
             sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
             C.etbwd(tape_h, ttape, None, torch.ones_like(sd), hook=self._hook(C))
-        sf = s.to(self._acc)
-        w_real = -sf[:B].mean()
-        w_fake = sf[B:].mean()
+        w = w.to(self._acc)
+        w_real, w_fake = w[0], w[1]
+        pen = pen.to(self._acc)
         return torch.stack([w_real + w_fake + self.gp_weight * pen, w_real, w_fake, pen])
 
     # ---- generator ------------------------------------------------------------------------
@@ -209,15 +200,10 @@ class GANTrainer:
         fake, tg = G.efwd(noise, save=True)
         s, tc = C.efwd(fake, save=True)
         if self.cfg.loss == "gan":
-            pf = s.to(self._acc)
-            n = pf.numel()
-            o = pf.clamp(R.KERAS_EPS, 1 - R.KERAS_EPS)
-            loss = -torch.log(o + R.KERAS_EPS).mean()
-            inside = ((pf > R.KERAS_EPS) & (pf < 1 - R.KERAS_EPS)).to(pf.dtype)
-            ds = (-(1.0 / (o + R.KERAS_EPS)) * inside / n).to(s.dtype)
+            out, ds = Fn.gan_loss(s, s.numel(), 1.0, 1.0, 1)
         else:
-            loss = -s.to(self._acc).mean()
-            ds = torch.full_like(s, -1.0 / s.numel())
+            out, ds = Fn.gan_loss(s, s.numel(), -1.0, -1.0, 0)
+        loss = out[0].to(self._acc)
         dfake = C.ebwd(tc, ds, need_dx=True, wgrad=False)
         G.ebwd(tg, dfake, hook=self._hook(G))
         return loss

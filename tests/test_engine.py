@@ -131,3 +131,22 @@ def test_keras_init_semantics():
     assert torch.all(b[5:10] == 1) and torch.all(b[:5] == 0) and torch.all(b[10:] == 0)
     names = [n for n, _ in m.named_weights()]
     assert names[0].endswith("/kernel:0") and "lstm_cell" in names[1]
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_gan_loss_contract_matches_keras_losses(kind):
+    """R.gan_loss (the native op's contract) = the Keras losses and their autograd gradients."""
+    g = torch.Generator().manual_seed(5)
+    B, T = 6, 4
+    p = torch.rand(2 * B, T, 1, generator=g, dtype=torch.float64)
+    p[0, 0, 0], p[1, 1, 0] = 0.0, 1.0  # clipped entries: zero BCE gradient
+    la, lb = (-1.0, 1.0) if kind == 0 else (1.0, 0.0)
+    out, grad = R.gan_loss(p, B * T, la, lb, kind, acc=torch.float64)
+    q = p.clone().requires_grad_(True)
+    f = R.wasserstein_loss if kind == 0 else R.binary_crossentropy
+    ya = torch.full((B, T), la, dtype=torch.float64)
+    yb = torch.full((B, T), lb, dtype=torch.float64)
+    la_, lb_ = f(ya, q[:B]), f(yb, q[B:])
+    (la_ + lb_).backward()
+    assert torch.allclose(out, torch.stack([la_, lb_]).detach(), rtol=1e-12, atol=1e-12)
+    assert torch.allclose(grad, q.grad, rtol=1e-12, atol=1e-12)

@@ -530,3 +530,25 @@ def test_lstm2_head_adjoint_in_kernel(cuda):
             # bf16 differences that the recurrence carries back, so compare at bf16 tolerance)
             for a, c in zip(t1, t2):
                 _close(a, c.double(), torch.bfloat16)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("n,split", [(64, 32), (70 * 24, 35 * 24), (1 << 20, 1 << 19), (1000, 1000)])
+def test_gan_loss_native(cuda, dt, kind, n, split):
+    """Native loss value + gradient (csrc/misc.hip gan_loss_kernel) vs the fp32 reference contract,
+    and bitwise run-to-run."""
+    from hfrep.ops import functional as Fn
+
+    g = torch.Generator().manual_seed(n + kind)
+    p = torch.rand(n, 1, generator=g) if kind == 1 else torch.randn(n, 1, generator=g)
+    if kind == 1:
+        p[:3] = torch.tensor([[0.0], [1.0], [1e-9]])  # clip boundaries
+    p = p.to(dt)
+    la, lb = (-1.0, 1.0) if kind == 0 else (1.0, 0.0)
+    out, grad = Fn.gan_loss(p.to(cuda), split, la, lb, kind)
+    rout, rgrad = R.gan_loss(p, split, la, lb, kind)
+    assert torch.allclose(out.cpu(), rout, rtol=1e-5, atol=1e-6), (out, rout)
+    _close(grad, rgrad.double(), dt)
+    out2, grad2 = Fn.gan_loss(p.to(cuda), split, la, lb, kind)
+    assert torch.equal(out, out2) and torch.equal(grad, grad2)
