@@ -236,8 +236,19 @@ def cmd_replicate(a) -> int:
     res = {}
     if a.method in ("linear", "all"):
         b = LinearCloneBenchmark(window=a.window).fit(etf.iloc[half:], hfd.iloc[half:], rf.iloc[half:])
-        post = b.post(etf.iloc[half:])
-        res["linear"] = {"sharpe_ex_post": {k: float(analytics.annualized_sharpe_ratio(post[k])) for k in post.columns}}
+        post = b.post()
+        # excess-return Sharpe, as the AE clones' data_analysis (autoencoder_v4.ipynb:774, rf[-144:])
+        rf_al = rf.iloc[:, 0].reindex(post.index).to_numpy(np.float64)
+        real = hfd.reindex(post.index)
+        res["linear"] = {
+            "window": a.window, "months": int(len(post)),
+            "period": [str(post.index[0].date()), str(post.index[-1].date())],
+            "sharpe_ex_ante": {k: analytics.annualized_sharpe_ratio(b.ante_[k], rf_al) for k in post.columns},
+            "sharpe_ex_post": {k: analytics.annualized_sharpe_ratio(post[k], rf_al) for k in post.columns},
+            # the notebook's convention for the real index (hfd_res table, autoencoder_v4.ipynb:1015)
+            "sharpe_real": {k: analytics.annualized_sharpe_ratio(real[k], rf_al) for k in post.columns},
+            "turnover": dict(zip(post.columns, map(float, b.turnover()))),
+        }
     if a.method in ("ae", "all"):
         from .finance.autoencoder_replication import AE
 

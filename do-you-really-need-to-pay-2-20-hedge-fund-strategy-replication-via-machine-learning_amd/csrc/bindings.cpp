@@ -250,6 +250,50 @@ std::tuple<Tensor, Tensor> lstm_tbwd(optional<Tensor> dH, Tensor dHd, Tensor gat
   return {dZ, dZd};
 }
 
+// ------------------------------------------------------------------------------------ LSTM fp32 fused
+bool lstmf_supported(int64_t H, int64_t K, int64_t act) { return hfrep::lstmf_supported((int)H, (int)K, (int)act); }
+
+std::tuple<Tensor, Tensor, Tensor> lstmf_fwd(Tensor x, Tensor W, optional<Tensor> b, Tensor U, int64_t act, bool save) {
+  CHECK_F32(x); CHECK_F32(W);
+  TORCH_CHECK(x.dim() == 3, "x must be (B, T, K)");
+  const int B = x.size(0), Tn = x.size(1), K = x.size(2), H = U.size(0);
+  check_lstm_U(U, H);
+  TORCH_CHECK(W.size(0) == K && W.size(1) == 4 * H, "W must be (K, 4H)");
+  if (b.has_value()) { CHECK_F32(*b); TORCH_CHECK(b->numel() == 4 * H, "bias size"); }
+  TORCH_CHECK(hfrep::lstmf_supported(H, K, (int)act), "lstmf_fwd: unsupported H/K/act");
+  GUARD(x);
+  Tensor hs = out_empty({B, Tn, H}, x.options());
+  Tensor gates = save ? out_empty({B, Tn, 4 * H}, x.options()) : out_empty({0}, x.options());
+  Tensor cs = save ? out_empty({B, Tn, H}, x.options()) : out_empty({0}, x.options());
+  const bool ok = hfrep::launch_lstmf_fwd(x.data_ptr<float>(), W.data_ptr<float>(),
+                                          b.has_value() ? b->data_ptr<float>() : nullptr, U.data_ptr<float>(),
+                                          hs.data_ptr<float>(), save ? gates.data_ptr<float>() : nullptr,
+                                          save ? cs.data_ptr<float>() : nullptr, B, Tn, K, H, (int)act, cur_stream(x));
+  TORCH_CHECK(ok, "lstmf_fwd: launch failed");
+  return {hs, gates, cs};
+}
+
+std::tuple<Tensor, Tensor, Tensor> lstmf_tfwd(Tensor xd, Tensor W, Tensor U, Tensor gates, Tensor cs, int64_t act) {
+  CHECK_F32(xd); CHECK_F32(W); CHECK_F32(gates); CHECK_F32(cs);
+  TORCH_CHECK(xd.dim() == 3, "xd must be (B, T, K)");
+  const int B = xd.size(0), Tn = xd.size(1), K = xd.size(2), H = U.size(0);
+  check_lstm_U(U, H);
+  TORCH_CHECK(W.size(0) == K && W.size(1) == 4 * H, "W must be (K, 4H)");
+  TORCH_CHECK(gates.dim() == 3 && gates.size(0) == B && gates.size(1) == Tn && gates.size(2) == 4 * H, "gates shape");
+  TORCH_CHECK(cs.dim() == 3 && cs.size(0) == B && cs.size(1) == Tn && cs.size(2) == H, "cs shape");
+  TORCH_CHECK(hfrep::lstmf_supported(H, K, (int)act), "lstmf_tfwd: unsupported H/K/act");
+  GUARD(xd);
+  Tensor hds = out_empty({B, Tn, H}, xd.options());
+  Tensor zds = out_empty({B, Tn, 4 * H}, xd.options());
+  Tensor cds = out_empty({B, Tn, H}, xd.options());
+  const bool ok = hfrep::launch_lstmf_tfwd(xd.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
+                                           gates.data_ptr<float>(), cs.data_ptr<float>(), hds.data_ptr<float>(),
+                                           zds.data_ptr<float>(), cds.data_ptr<float>(), B, Tn, K, H, (int)act,
+                                           cur_stream(xd));
+  TORCH_CHECK(ok, "lstmf_tfwd: launch failed");
+  return {hds, zds, cds};
+}
+
 // ------------------------------------------------------------------------------------ LSTM v2 (bf16 fused)
 void check_lstm2(const Tensor& x, const Tensor& U, int64_t H) {
   TORCH_CHECK(x.scalar_type() == at::kBFloat16, "lstm2 kernels are bf16-only");
@@ -561,6 +605,9 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstm_bwd(Tensor dH, Tensor gates, Tensor cs, Tensor U, int act) -> Tensor");
   m.def("lstm_tfwd(Tensor dzx, Tensor gates, Tensor cs, Tensor U, int act) -> (Tensor, Tensor, Tensor)");
   m.def("lstm_tbwd(Tensor? dH, Tensor dHd, Tensor gates, Tensor cs, Tensor zds, Tensor cds, Tensor U, int act) -> (Tensor, Tensor)");
+  m.def("lstmf_supported(int H, int K, int act) -> bool", &lstmf_supported);  // no tensor inputs: catch-all kernel
+  m.def("lstmf_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor, Tensor)");
+  m.def("lstmf_tfwd(Tensor xd, Tensor W, Tensor U, Tensor gates, Tensor cs, int act) -> (Tensor, Tensor, Tensor)");
   m.def("lstm2_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
   m.def("lstm2_bwd(Tensor? dH, Tensor tape, Tensor U, int act, Tensor? W=None, bool need_dz=True, Tensor? head_d=None, "
         "Tensor? head_w=None) -> (Tensor, Tensor)");
@@ -595,6 +642,8 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("act_bwd", &act_bwd);
   m.impl("act_tangent_bwd", &act_tangent_bwd);
   m.impl("lstm_fwd", &lstm_fwd);
+  m.impl("lstmf_fwd", &lstmf_fwd);
+  m.impl("lstmf_tfwd", &lstmf_tfwd);
   m.impl("lstm_bwd", &lstm_bwd);
   m.impl("lstm_tfwd", &lstm_tfwd);
   m.impl("lstm_tbwd", &lstm_tbwd);

@@ -40,6 +40,14 @@ void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const 
                        hipStream_t s, const void* head_d = nullptr, const void* head_dd = nullptr,
                        const float* hw = nullptr);
 
+// ---- lstm_f32.hip (fp32, fused input projection, exact-fp32 MFMA; H == 100, K in {32, 35, 36, 100},
+//      act in {linear, sigmoid, tanh}; false = not supported).  Row-major v1-contract outputs. ----
+bool lstmf_supported(int H, int K, int act);
+bool launch_lstmf_fwd(const float* x, const float* W, const float* b, const float* U, float* hs, float* gates, float* cs,
+                      int B, int Tn, int K, int H, int act, hipStream_t s);
+bool launch_lstmf_tfwd(const float* xd, const float* W, const float* U, const float* gates, const float* cs, float* hds,
+                       float* zds, float* cds, int B, int Tn, int K, int H, int act, hipStream_t s);
+
 // ---- gemm.hip ----
 // C[M,N] = act(A[M,K] . op(W) + bias);  op(W) = W (K,N) or W^T when w_trans (W stored (N,K)).
 // A and C share the activation dtype `dt`; W and bias are fp32 (converted while staging).

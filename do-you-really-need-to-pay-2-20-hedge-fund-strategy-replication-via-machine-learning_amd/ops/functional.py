@@ -10,6 +10,8 @@ dtype of the explicit engine); gradients are always fp32.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native
@@ -226,11 +228,23 @@ def _use_lstm2(x: torch.Tensor, U: torch.Tensor) -> bool:
             and not _native.fallback_allowed())
 
 
+_LSTMF = os.environ.get("HFREP_LSTMF", "1") != "0"  # 0: the fp32 path falls back to zx GEMM + v1 (A/B only)
+
+
+def _use_lstmf(x: torch.Tensor, U: torch.Tensor, act: int) -> bool:
+    """fp32 fused-projection kernels (csrc/lstm_f32.hip): H = 100, K in {32, 35, 36, 100}."""
+    return (_LSTMF and x.dtype == torch.float32 and _nat(x) and not _native.fallback_allowed()
+            and bool(_ops().lstmf_supported(int(U.shape[0]), int(x.shape[-1]), int(act))))
+
+
 def lstm_layer_fwd(x, W, b, U, act: int, save: bool):
     """h_seq and a tape for act(x W + b ...) recurrences; x (B, T, K)."""
     if _use_lstm2(x, U):
         hs, tape = _ops().lstm2_fwd(x.contiguous(), W, b, U, int(act), bool(save))
         return hs, (tape if save else None)
+    if _use_lstmf(x, U, act):
+        hs, gates, cs = _ops().lstmf_fwd(x.contiguous(), W, b, U, int(act), bool(save))
+        return hs, ((gates, cs) if save else None)
     zx = linear(x, W, b, 0)
     hs, gates, cs = lstm_seq_fwd(zx, U, act, save)
     return hs, ((gates, cs) if save else None)
@@ -288,6 +302,9 @@ def lstm_layer_tfwd(xd, W, tape, U, act: int):
         hds, ttape = _ops().lstm2_tfwd(xd.contiguous(), W, U, tape, int(act))
         return hds, ttape
     gates, cs = tape
+    if _use_lstmf(xd, U, act):
+        hds, zds, cds = _ops().lstmf_tfwd(xd.contiguous(), W, U, gates, cs, int(act))
+        return hds, (zds, cds)
     dzx = linear(xd, W, None, 0)
     hds, zds, cds = lstm_seq_tfwd(dzx, gates, cs, U, act)
     return hds, (zds, cds)

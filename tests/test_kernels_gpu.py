@@ -552,3 +552,58 @@ def test_gan_loss_native(cuda, dt, kind, n, split):
     _close(grad, rgrad.double(), dt)
     out2, grad2 = Fn.gan_loss(p.to(cuda), split, la, lb, kind)
     assert torch.equal(out, out2) and torch.equal(grad, grad2)
+
+
+@pytest.mark.parametrize("act", [2, 1, 0])
+@pytest.mark.parametrize("B,T,K", [(70, 24, 32), (33, 12, 100), (64, 7, 35), (40, 5, 36)])
+def test_lstmf_fused_layer(cuda, act, B, T, K):
+    """fp32 fused-projection kernels (csrc/lstm_f32.hip: exact-f32 16x16x4 MFMA, gate-interleaved
+    tiles + quad transpose) vs the fp64 reference: forward, tape, tangent forward, and the v1
+    reverse kernels consuming their row-major tapes."""
+    from hfrep.ops import functional as Fn
+
+    H = 100
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(B, T, K, generator=g) * 0.5
+    W = torch.randn(K, 4 * H, generator=g) * (1.0 / K ** 0.5)
+    b = torch.randn(4 * H, generator=g) * 0.1
+    U = torch.randn(H, 4 * H, generator=g) * (1.0 / H ** 0.5)
+    assert _ops().lstmf_supported(H, K, act)
+    hs, tape = Fn.lstm_layer_fwd(x.to(cuda), W.to(cuda), b.to(cuda), U.to(cuda), act, True)
+    gates, cs = tape
+    zx = x.double() @ W.double() + b.double()
+    rh, rg, rc = R.lstm_seq_fwd(zx, U.double(), act)
+    f32 = torch.float32
+    _close(hs, rh, f32)
+    _close(gates, rg, f32)
+    _close(cs, rc, f32)
+    hs0, none = Fn.lstm_layer_fwd(x.to(cuda), W.to(cuda), b.to(cuda), U.to(cuda), act, False)
+    assert none is None and torch.equal(hs0, hs)
+    xd = torch.randn(B, T, K, generator=g) * 0.3
+    hds, (zds, cds) = Fn.lstm_layer_tfwd(xd.to(cuda), W.to(cuda), tape, U.to(cuda), act)
+    th, tz, tc = R.lstm_seq_tfwd(xd.double() @ W.double(), gates.double().cpu(), cs.double().cpu(), U.double(), act)
+    _close(hds, th, f32)
+    _close(zds, tz, f32)
+    _close(cds, tc, f32)
+    # bitwise run-to-run reproducibility of both kernels
+    hs2, (g2, c2) = Fn.lstm_layer_fwd(x.to(cuda), W.to(cuda), b.to(cuda), U.to(cuda), act, True)
+    hds2, (z2, cd2) = Fn.lstm_layer_tfwd(xd.to(cuda), W.to(cuda), tape, U.to(cuda), act)
+    for a_, b_ in ((hs, hs2), (gates, g2), (cs, c2), (hds, hds2), (zds, z2), (cds, cd2)):
+        assert torch.equal(a_, b_)
+
+
+def test_lstmf_persistent_multi_pass(cuda):
+    """More row tiles than CUs (every persistent workgroup walks several tiles) and a partial last
+    tile: B = 256 * 32 + 45 rows."""
+    from hfrep.ops import functional as Fn
+
+    H, K, T, B = 100, 32, 6, 256 * 32 + 45
+    g = torch.Generator().manual_seed(22)
+    x = torch.randn(B, T, K, generator=g) * 0.5
+    W = torch.randn(K, 4 * H, generator=g) * (1.0 / K ** 0.5)
+    b = torch.randn(4 * H, generator=g) * 0.1
+    U = torch.randn(H, 4 * H, generator=g) * (1.0 / H ** 0.5)
+    hs, (gates, cs) = Fn.lstm_layer_fwd(x.to(cuda), W.to(cuda), b.to(cuda), U.to(cuda), 2, True)
+    rh, rg, rc = R.lstm_seq_fwd(x.double() @ W.double() + b.double(), U.double(), 2)
+    _close(hs, rh, torch.float32)
+    _close(cs, rc, torch.float32)
