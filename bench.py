@@ -10,7 +10,8 @@ the whole-job aggregate over all ranks.
 Model: the reference architecture at the north-star shape — generator LSTM(100, sigmoid) -> LN ->
 LSTM(100, sigmoid) -> LeakyReLU -> LN -> Dense(32); critic LSTM(100) -> LSTM(100) -> Flatten ->
 Dense(1); random init; synthetic return windows (no dataset/network on the box); compute dtype
-bf16 (MFMA bf16 with fp32 accumulation, fp32 master weights/optimizer).
+fp32 (the reference's Keras float32; exact-f32 MFMA) for the headline record, and a bf16 sub-record
+(bf16 MFMA with fp32 accumulation, fp32 master weights / optimizer) of the same config.
 
 Usage:
     python bench.py                         # 1 GPU, defaults
@@ -27,42 +28,20 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    # per-GPU batch sized for HBM (≈87 GB of 288 GB): throughput 2.21 M (32k) -> 2.35 M (65k) ->
-    # 2.42 M (131k) -> 2.48 M seq/s (262k) on one MI355X (profiles/r01_batch_sweep)
-    ap.add_argument("--batch-per-gpu", type=int, default=262144)
-    ap.add_argument("--window", type=int, default=24)
-    ap.add_argument("--features", type=int, default=32)
-    ap.add_argument("--dtype", default="bfloat16")
-    ap.add_argument("--dataset-windows", type=int, default=8192)
-    ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (e.g. for rocprof)")
-    ap.add_argument("--trace-out", default="", help="after the timed steps: torch.profiler Chrome trace of "
-                    "--profile-steps (default 2) untimed steps with the trainer's phase ranges")
-    args = ap.parse_args()
-
+def _measure(args, dtype, rank, world, pg, dev):
+    """Warm up, then time exactly args.steps training iterations at one compute dtype."""
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    import hfrep
     from hfrep.data.windows import synthetic_windows
-    from hfrep.parallel.dp import init_distributed
     from hfrep.train.gan_trainer import GANConfig, GANTrainer
-
-    rank, local_rank, world, pg = init_distributed()
-    if world != args.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
 
     T, F, B = args.window, args.features, args.batch_per_gpu
     ds = synthetic_windows(args.dataset_windows, T, F, seed=1234)
-    cfg = GANConfig(arch="lstm", loss="wgan_gp", window=T, features=F, batch_size=B, dtype=args.dtype, seed=123)
+    cfg = GANConfig(arch="lstm", loss="wgan_gp", window=T, features=F, batch_size=B, dtype=dtype, seed=123)
     tr = GANTrainer(cfg, ds, device=dev, process_group=pg, rank=rank, world=world)
+    torch.cuda.reset_peak_memory_stats(dev)
 
     def barrier():
         if world > 1:
@@ -92,25 +71,70 @@ def main():
         for _ in range(args.profile_steps):
             tr.train_step()
     torch.cuda.synchronize()
-
-    ms = elapsed / args.steps * 1e3
-    per_rank = tr.windows_per_iteration()
-    value = per_rank * world * args.steps / elapsed
     losses = tr.losses()
+    per_rank = tr.windows_per_iteration()
+    out = {
+        "value": round(per_rank * world * args.steps / elapsed, 2),
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "windows_per_step": per_rank * world,
+        "losses_finite": bool(all(np.isfinite(v) for k, v in losses.items() if k != "iteration")),
+        "peak_mem_gb_rank0": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
+    }
+    del tr, ds
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    # per-GPU batch sized for HBM (fp32 ~147 GB, bf16 ~85 GB of 288 GB at 262144 windows per GPU):
+    # bf16 throughput 2.21 M (32k) -> 2.48 M seq/s (262k) on one MI355X (profiles/r01_batch_sweep)
+    ap.add_argument("--batch-per-gpu", type=int, default=262144)
+    ap.add_argument("--window", type=int, default=24)
+    ap.add_argument("--features", type=int, default=32)
+    ap.add_argument("--dtype", default="both", choices=["both", "float32", "bfloat16"],
+                    help="both (default): the reference-precision fp32 record, plus a bf16 sub-record timed the "
+                         "same way right after it")
+    ap.add_argument("--dataset-windows", type=int, default=8192)
+    ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (e.g. for rocprof)")
+    ap.add_argument("--trace-out", default="", help="after the timed steps: torch.profiler Chrome trace of "
+                    "--profile-steps (default 2) untimed steps with the trainer's phase ranges")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import hfrep  # noqa: F401
+    from hfrep.parallel.dp import init_distributed
+
+    rank, local_rank, world, pg = init_distributed()
+    if world != args.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    primary = "float32" if args.dtype in ("both", "float32") else "bfloat16"
+    res = _measure(args, primary, rank, world, pg, dev)
+    sub = _measure(args, "bfloat16", rank, world, pg, dev) if args.dtype == "both" else None
+    T, F, B = args.window, args.features, args.batch_per_gpu
     if rank == 0:
-        finite = all(np.isfinite(v) for k, v in losses.items() if k != "iteration")
         rec = {
             "metric": "seq/sec/node MTSS-WGAN-GP train (24x32 windows) at 1/2/4/8 GPUs; W-dist parity",
-            "value": round(value, 2),
+            "value": res["value"],
             "unit": "seq/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms, 3),
+            "ms_per_step": res["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if args.dtype in ("bfloat16", "bf16") else args.dtype,
+            # fp32 = the reference's precision (Keras float32): exact-f32 MFMA (v_mfma_f32_16x16x4_f32),
+            # fp32 activations, tapes, gradients and optimizer state
+            "dtype": "fp32" if primary == "float32" else "bf16",
             "data": "synthetic",
             "config": {
                 "model": "MTSS-WGAN-GP (G: LSTM100(sigmoid)-LN-LSTM100(sigmoid)-LReLU-LN-Dense32; "
@@ -120,14 +144,17 @@ def main():
                 "seq_len": T,
                 "features": F,
                 "parallelism": f"dp{world}",
-                "windows_per_step": per_rank * world,
+                "windows_per_step": res["windows_per_step"],
             },
-            "losses_finite": bool(finite),
-            # the W-dist half of the metric is a training-quality run, not a throughput step:
-            # `python -m hfrep parity` (fp32 vs bf16, B=32 vs 4096) -> profiles/r01_parity
-            "w_dist_parity": "profiles/r01_parity3/README.md",
-            "peak_mem_gb_rank0": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
+            "losses_finite": res["losses_finite"],
+            # the W-dist half of the metric is a training-quality run, not a throughput step
+            "w_dist_parity": "profiles/r02_parity/README.md",
+            "peak_mem_gb_rank0": res["peak_mem_gb_rank0"],
         }
+        if sub is not None:
+            # same config, same step count, timed after the fp32 run: bf16 MFMA with fp32 accumulation,
+            # bf16 activations / tapes, fp32 master weights and optimizer state
+            rec["bf16"] = {k: sub[k] for k in ("value", "ms_per_step", "losses_finite", "peak_mem_gb_rank0")}
         print(json.dumps(rec))
     if world > 1:
         dist.destroy_process_group()

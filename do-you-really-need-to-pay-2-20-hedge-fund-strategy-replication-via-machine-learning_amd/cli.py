@@ -249,14 +249,25 @@ def cmd_replicate(a) -> int:
             "sharpe_real": {k: analytics.annualized_sharpe_ratio(real[k], rf_al) for k in post.columns},
             "turnover": dict(zip(post.columns, map(float, b.turnover()))),
         }
+    dev = _device(a.device) if a.device != "cpu" else "cpu"
+    dt = _torch_dtype(a.dtype)
     if a.method in ("ae", "all"):
         from .finance.autoencoder_replication import AE
 
-        x_tr, x_te = etf.iloc[:half].to_numpy(), etf.iloc[half:].to_numpy()
-        y_tr, y_te = hfd.iloc[:half].to_numpy(), hfd.iloc[half:].to_numpy()
-        ae = AE(x_tr, y_tr, x_te, y_te, a.latent)
+        x_tr, x_te = etf.iloc[:half], etf.iloc[half:]
+        y_tr, y_te = hfd.iloc[:half], hfd.iloc[half:]
+        ae = AE(x_tr.to_numpy(), y_tr.to_numpy(), x_te.to_numpy(), y_te, a.latent, device=dev, dtype=dt, seed=a.seed)
         ae.train(verbose=0, plot=False)
-        res["ae"] = {"latent": a.latent, "IS_r2": float(ae.model_IS_r2()), "OOS_r2": float(np.mean(ae.model_OOS_r2()))}
+        ante = ae.ante(rf.iloc[half:], y_te, window=a.window)
+        post = ae.post(etf)
+        rf_ae = rf.iloc[:, 0].reindex(post.index).to_numpy(np.float64)
+        res["ae"] = {"latent": a.latent, "device": str(dev), "dtype": a.dtype,
+                     "IS_r2": float(ae.model_IS_r2()), "IS_RMSE": float(ae.model_IS_RMSE()),
+                     "OOS_r2": float(np.mean(ae.model_OOS_r2())), "OOS_RMSE": float(np.mean(ae.model_OOS_RMSE())),
+                     "sharpe_ex_ante": {k: analytics.annualized_sharpe_ratio(ante[k], rf_ae) for k in ante.columns},
+                     "sharpe_ex_post": {k: analytics.annualized_sharpe_ratio(post[k], rf_ae) for k in post.columns},
+                     "turnover": dict(zip(post.columns, map(float, ae.turnover(c.get("hfd_fullname", {k: k for k in
+                                                                                   post.columns}))["Turnover"])))}
     if a.method == "ae-sweep":
         from .finance.experiment import generated_augmentation, latent_sweep
 
@@ -265,12 +276,25 @@ def cmd_replicate(a) -> int:
         xe = ye = None
         if a.augment:
             xe, ye = generated_augmentation(np.load(a.augment, allow_pickle=False), c)
-        sw = latent_sweep(c, latents=latents, window=a.window, x_extra=xe, y_extra=ye, verbose=True)
-        res["ae_sweep"] = {"metrics": sw.metrics.to_dict(orient="index"),
+        sw = latent_sweep(c, latents=latents, window=a.window, x_extra=xe, y_extra=ye, verbose=True, device=dev,
+                          dtype=dt, seed=a.seed)
+        res["ae_sweep"] = {"device": str(dev), "dtype": a.dtype, "seed": a.seed, "augmented": bool(a.augment),
+                           "metrics": sw.metrics.to_dict(orient="index"),
+                           "sharpe_ante": sw.sharpe_ante.to_dict(orient="index"),
+                           "turnover": sw.turnover.to_dict(orient="index"),
                            "sharpe_post": sw.sharpe_post.to_dict(orient="index"),
                            "best": sw.best.to_dict(orient="index")}
     print(json.dumps(res, indent=1, default=float))
+    if a.out:
+        with open(a.out, "w") as fh:
+            json.dump(res, fh, indent=1, default=float)
     return 0
+
+
+def _torch_dtype(name: str):
+    import torch
+
+    return {"float32": torch.float32, "bfloat16": torch.bfloat16, "float64": torch.float64}[name]
 
 
 def cmd_bench(a, rest) -> int:
@@ -316,6 +340,10 @@ def main(argv=None) -> int:
     r.add_argument("--augment", default=None, help="ae-sweep: generated windows .npy (F=36) to add to training")
     r.add_argument("--window", type=int, default=24)
     r.add_argument("--latent", type=int, default=12)
+    r.add_argument("--device", default="cpu", help="cpu | cuda (the autoencoder's training / inference device)")
+    r.add_argument("--dtype", default="float32", choices=["float32", "bfloat16", "float64"])
+    r.add_argument("--seed", type=int, default=123)
+    r.add_argument("--out", default=None, help="also write the JSON result here")
     sub.add_parser("bench", help="flagship throughput benchmark (bench.py flags)")
     a = ap.parse_args(argv)
     return {"train": cmd_train, "parity": cmd_parity, "generate": cmd_generate, "eval": cmd_eval,

@@ -125,7 +125,9 @@ void linear_wgrad_(Tensor x, Tensor dz, Tensor gW, optional<Tensor> gb, int64_t 
 void lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<Tensor> gb, optional<Tensor> xd,
                  optional<Tensor> hds, optional<Tensor> dZd, int64_t impl) {
   CHECK_GPU(x); CHECK_GPU(hs); CHECK_GPU(dZ); same_dt(x, dZ); same_dt(hs, dZ);
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "lstm_wgrad_: bf16 only");
+  const bool f32 = x.scalar_type() == at::kFloat;
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || (f32 && hfrep::lstmf_wgrad_supported(x.size(2), hs.size(2), dZ.size(2))),
+              "lstm_wgrad_: bf16, or fp32 with K in {32, 36, 100}, H = 100");
   TORCH_CHECK(x.dim() == 3 && hs.dim() == 3 && dZ.dim() == 3, "lstm_wgrad_: (B,T,*) tensors");
   const int B = x.size(0), Tn = x.size(1), K = x.size(2), Hd = hs.size(2), N = dZ.size(2);
   TORCH_CHECK(hs.size(0) == B && dZ.size(0) == B && hs.size(1) == Tn && dZ.size(1) == Tn, "lstm_wgrad_: B/T");
@@ -144,6 +146,14 @@ void lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<
   const void* H1 = tangent ? hds->data_ptr() : nullptr;
   const void* D1 = tangent ? dZd->data_ptr() : nullptr;
   float* gbp = gb.has_value() ? gb->data_ptr<float>() : nullptr;
+  if (f32) {
+    Tensor ws = out_empty({(int64_t)hfrep::lstmf_wgrad_workspace_floats(M, K)}, x.options());
+    hfrep::launch_lstmf_wgrad(x.data_ptr<float>(), hs.data_ptr<float>(), dZ.data_ptr<float>(),
+                              tangent ? xd->data_ptr<float>() : nullptr, tangent ? hds->data_ptr<float>() : nullptr,
+                              tangent ? dZd->data_ptr<float>() : nullptr, gW.data_ptr<float>(), gU.data_ptr<float>(), gbp,
+                              M, K, Tn, ws.data_ptr<float>(), cur_stream(x));
+    return;
+  }
   // impl: 0 = auto (LDS-DMA streaming v3 where supported), 2 = force v2 (tests / A-B)
   if (impl != 2 && hfrep::lstm_wgrad3_supported(M, K, Hd, N)) {
     Tensor ws = out_empty({(int64_t)hfrep::lstm_wgrad3_workspace_floats(K, Hd, N)}, x.options().dtype(at::kFloat));
@@ -409,7 +419,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm2_tbwd(optional<Tensor> dH, optio
   TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstm2_tape_elems(B, Tn) && ttape.numel() == tape.numel(), "tape size");
   GUARD(tape);
   const int K = check_dx_W(W, H);
-  const bool gen = head && hfrep::lstm2_head_fusion();
+  // the in-kernel generated head adjoint is only combined with the dX-free instantiation: the
+  // DX + GEN tangent reverse gave run-to-run different rows (profiles/r01_fwd5/README.md); with W
+  // the head adjoint is materialised instead (the native op can never reach that instantiation)
+  const bool gen = head && hfrep::lstm2_head_fusion() && K == 0;
   optional<Tensor> dHm = dH;
   Tensor dHd;
   if (head && !gen) {  // materialise for the v2 kernels

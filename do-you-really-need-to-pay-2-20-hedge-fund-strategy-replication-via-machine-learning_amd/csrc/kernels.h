@@ -48,6 +48,14 @@ bool launch_lstmf_fwd(const float* x, const float* W, const float* b, const floa
 bool launch_lstmf_tfwd(const float* xd, const float* W, const float* U, const float* gates, const float* cs, float* hds,
                        float* zds, float* cds, int B, int Tn, int K, int H, int act, hipStream_t s);
 
+// fused fp32 LSTM weight gradients (K in {32, 36, 100}, H = 100, N = 400): gW += X^T dZ (+ Xd^T dZd),
+// gU += Hprev^T dZ (+ Hdprev^T dZd), gb += colsum dZ, through per-workgroup slabs in ws
+// (lstmf_wgrad_workspace_floats) and one fixed-order reduce
+bool lstmf_wgrad_supported(int K, int H, int N);
+size_t lstmf_wgrad_workspace_floats(int M, int K);
+bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
+                        float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s);
+
 // ---- gemm.hip ----
 // C[M,N] = act(A[M,K] . op(W) + bias);  op(W) = W (K,N) or W^T when w_trans (W stored (N,K)).
 // A and C share the activation dtype `dt`; W and bias are fp32 (converted while staging).

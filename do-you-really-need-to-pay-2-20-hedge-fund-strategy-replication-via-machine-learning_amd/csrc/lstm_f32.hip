@@ -361,6 +361,155 @@ lstmf_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W, const
 }
 
 // ==========================================================================================
+// fused fp32 LSTM weight gradients
+// ==========================================================================================
+// slab[z] ((K + H + 1) x 4H) = sum over workgroup z's rows m of [x_m | h_{m-1} | 1]^T dz_m, plus the
+// tangent segment [xd_m | hd_{m-1} | 0]^T dzd_m when given; one fixed-order reduce folds the slabs
+// into gW / gU / gb (launch_lstm_wgrad2_reduce).  The v1 fp32 path ran one tiled GEMM per product
+// (X^T dZ, H^T dZ, Xd^T dZd, Hd^T dZd: each re-reading dZ, ~35 TF/s, profiles/r02_fp32): here every
+// (row chunk) is staged once and feeds all products.
+//
+// 8 waves (2 per SIMD), 16-row chunks = four 16x16x4 k-steps; output tiles 16 x 16: wave w owns the
+// full i range of column tiles 3 w .. 3 w + 2 plus i-tiles 2 w, 2 w + 1 of the 25th column tile,
+// i.e. 3 NI + 2 accumulators (K = 100: 41 x 4 AGPRs), the same MFMA count on every wave.
+// Chunks are double-buffered in LDS through a register prefetch of the next chunk.
+constexpr int WF_R = 16, WF_LA = 272, WF_LD = 400;  // row strides = 16 mod 64 dwords: conflict-free b32 reads
+template <int KX>
+struct WFGeo {
+  static constexpr int KR = KX + FH + 1;
+  static constexpr int NI = (KR + 15) / 16;
+  static_assert(NI <= 16 && 16 * 16 <= WF_LA, "wgrad i tiles");
+  static constexpr int NX4 = WF_R * KX / 4, NH4 = WF_R * FH / 4, ND4 = WF_R * FG / 4;
+  static constexpr int JX = (NX4 + 511) / 512, JH = (NH4 + 511) / 512, JD = (ND4 + 511) / 512;
+};
+
+template <int KX>
+__global__ void __launch_bounds__(512)
+lstmf_wgrad_kernel(const float* __restrict__ X, const float* __restrict__ Hs, const float* __restrict__ D,
+                   const float* __restrict__ Xd, const float* __restrict__ Hds, const float* __restrict__ Dd,
+                   float* __restrict__ slab, int M, int Tn, int rows_per_wg) {
+  using WG = WFGeo<KX>;
+  constexpr int NI = WG::NI, KR = WG::KR;
+  __shared__ __attribute__((aligned(16))) float As[2][WF_R * WF_LA];
+  __shared__ __attribute__((aligned(16))) float Ds[2][WF_R * WF_LD];
+  __shared__ __attribute__((aligned(16))) float trash4[4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int mb = blockIdx.x * rows_per_wg, me = min(M, mb + rows_per_wg);
+  for (int i = tid; i < 2 * WF_R * WF_LA; i += 512) (&As[0][0])[i] = 0.f;
+
+  f32x4 acc[NI][3], accx[2];
+#pragma unroll
+  for (int it = 0; it < NI; ++it)
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) acc[it][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  accx[0] = accx[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ie0 = min(2 * w, 15), ie1 = min(2 * w + 1, 15);  // i tiles >= NI read LDS zeros
+
+  // per-thread chunk loads: X (JX), H_{m-1} (JH), D (JD) float4s
+  f32x4 vx[WG::JX], vh[WG::JH], vd[WG::JD];
+  for (int seg = 0; seg < (Xd ? 2 : 1); ++seg) {
+    const float* Xs = seg ? Xd : X;
+    const float* Hq = seg ? Hds : Hs;
+    const float* Dq = seg ? Dd : D;
+    const rsrc_t rx = make_rsrc(Xs, M * KX * 4), rh = make_rsrc(Hq, M * FH * 4), rd = make_rsrc(Dq, M * FG * 4);
+    auto load = [&](int m0) {
+#pragma unroll
+      for (int j = 0; j < WG::JX; ++j) {
+        const int e = tid + 512 * j, r = e / (KX / 4), c = e - r * (KX / 4);
+        const bool ok = e < WG::NX4 && m0 + r < me;
+        vx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? ((m0 + r) * KX + 4 * c) * 4 : kOOB, 0, 0));
+      }
+#pragma unroll
+      for (int j = 0; j < WG::JH; ++j) {
+        const int e = tid + 512 * j, r = e / (FH / 4), c = e - r * (FH / 4);
+        const int m = m0 + r;
+        const bool ok = e < WG::NH4 && m < me && (m % Tn) != 0;  // h_{-1} = 0 at t = 0
+        vh[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, ok ? ((m - 1) * FH + 4 * c) * 4 : kOOB, 0, 0));
+      }
+#pragma unroll
+      for (int j = 0; j < WG::JD; ++j) {
+        const int e = tid + 512 * j, r = e / (FG / 4), c = e - r * (FG / 4);
+        const bool ok = e < WG::ND4 && m0 + r < me;
+        vd[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, ok ? ((m0 + r) * FG + 4 * c) * 4 : kOOB, 0, 0));
+      }
+    };
+    auto to_lds = [&](int buf) {
+#pragma unroll
+      for (int j = 0; j < WG::JX; ++j) {
+        const int e = tid + 512 * j, r = e / (KX / 4), c = e - r * (KX / 4);
+        *reinterpret_cast<f32x4*>(e < WG::NX4 ? &As[buf][r * WF_LA + 4 * c] : trash4) = vx[j];
+      }
+#pragma unroll
+      for (int j = 0; j < WG::JH; ++j) {
+        const int e = tid + 512 * j, r = e / (FH / 4), c = e - r * (FH / 4);
+        *reinterpret_cast<f32x4*>(e < WG::NH4 ? &As[buf][r * WF_LA + KX + 4 * c] : trash4) = vh[j];
+      }
+#pragma unroll
+      for (int j = 0; j < WG::JD; ++j) {
+        const int e = tid + 512 * j, r = e / (FG / 4), c = e - r * (FG / 4);
+        *reinterpret_cast<f32x4*>(e < WG::ND4 ? &Ds[buf][r * WF_LD + 4 * c] : trash4) = vd[j];
+      }
+    };
+    __syncthreads();  // (previous segment's reads done)
+    if (tid < 2 * WF_R) As[tid >> 4][(tid & 15) * WF_LA + KR - 1] = seg ? 0.f : 1.f;  // the bias column
+    if (mb < me) {
+      load(mb);
+      to_lds(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int m0 = mb; m0 < me; m0 += WF_R) {
+      const bool more = m0 + WF_R < me;
+      if (more) load(m0 + WF_R);
+      const float* A_ = As[buf];
+      const float* D_ = Ds[buf];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const float* ar = A_ + (4 * ks + g) * WF_LA + c16;
+        const float* dr = D_ + (4 * ks + g) * WF_LD + c16;
+        float a[NI], b[3];
+#pragma unroll
+        for (int it = 0; it < NI; ++it) a[it] = ar[16 * it];
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) b[jj] = dr[16 * (3 * w + jj)];
+        const float bx = dr[16 * 24], ax0 = ar[16 * ie0], ax1 = ar[16 * ie1];
+#pragma unroll
+        for (int it = 0; it < NI; ++it)
+#pragma unroll
+          for (int jj = 0; jj < 3; ++jj) acc[it][jj] = mma4(a[it], b[jj], acc[it][jj]);
+        accx[0] = mma4(ax0, bx, accx[0]);
+        accx[1] = mma4(ax1, bx, accx[1]);
+      }
+      if (more) to_lds(buf ^ 1);
+      buf ^= 1;
+      __syncthreads();
+    }
+  }
+  // ---- slab store: C[i0 + 4 g + r][j0 + c16] ----
+  float* out = slab + (size_t)blockIdx.x * KR * FG;
+#pragma unroll
+  for (int it = 0; it < NI; ++it)
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * it + 4 * g + r;
+        if (i < KR) out[(size_t)i * FG + 16 * (3 * w + jj) + c16] = acc[it][jj][r];
+      }
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int it = 2 * w + e;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 16 * it + 4 * g + r;
+      if (it < NI && i < KR) out[(size_t)i * FG + 16 * 24 + c16] = accx[e][r];
+    }
+  }
+}
+
+// ==========================================================================================
 // host side
 // ==========================================================================================
 namespace {
@@ -423,6 +572,28 @@ bool launch_lstmf_tfwd(const float* xd, const float* W, const float* U, const fl
                        float* zds, float* cds, int B, int Tn, int K, int H, int act, hipStream_t s) {
   if (!lstmf_supported(H, K, act) || B <= 0 || Tn <= 0) return false;
   return fwdf_k<true, true>(K, act, xd, W, nullptr, U, gates, cs, hds, zds, cds, B, Tn, s);
+}
+
+static int wgradf_grid(int M) {
+  const int chunks = (M + WF_R - 1) / WF_R, cus = device_cu_count();
+  return chunks < cus ? chunks : cus;
+}
+bool lstmf_wgrad_supported(int K, int H, int N) { return H == FH && N == FG && (K == 32 || K == 36 || K == 100); }
+size_t lstmf_wgrad_workspace_floats(int M, int K) { return (size_t)wgradf_grid(M) * (K + FH + 1) * FG; }
+
+bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
+                        float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s) {
+  if (!lstmf_wgrad_supported(K, FH, FG) || M <= 0) return false;
+  const int grid = wgradf_grid(M);
+  const int rpw = ((M + grid - 1) / grid + WF_R - 1) / WF_R * WF_R;
+  const int z = (M + rpw - 1) / rpw;
+  switch (K) {
+    case 32: hipLaunchKernelGGL(lstmf_wgrad_kernel<32>, dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
+    case 36: hipLaunchKernelGGL(lstmf_wgrad_kernel<36>, dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
+    default: hipLaunchKernelGGL(lstmf_wgrad_kernel<100>, dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
+  }
+  launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s);
+  return true;
 }
 
 }  // namespace hfrep

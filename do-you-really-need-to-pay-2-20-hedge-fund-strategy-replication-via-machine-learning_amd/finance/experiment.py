@@ -45,11 +45,13 @@ def chronological_split(cleaned: dict, frac: float = 0.5):
 
 def latent_sweep(cleaned: dict, latents=range(1, 22), window: int = 24, frac: float = 0.5,
                  x_extra: np.ndarray | None = None, y_extra: np.ndarray | None = None, seed: int = 123,
-                 device="cpu", verbose: bool = False) -> SweepResult:
+                 device="cpu", verbose: bool = False, dtype=None) -> SweepResult:
     """Train one autoencoder per latent size and evaluate it as a hedge-fund clone.
 
     ``x_extra`` / ``y_extra``: extra (generated) training rows appended to the real training rows
-    (the augmented study); the test period is always real data.
+    (the augmented study); the test period is always real data.  ``device`` / ``dtype``: where and
+    in which compute dtype the autoencoders train and predict (fp32 on the CPU by default; ``cuda``
+    runs the engine's native Dense / optimizer kernels, BASELINE config 2).
     """
     x_tr, y_tr, x_te, y_te = chronological_split(cleaned, frac)
     xtr, ytr = x_tr.to_numpy(), y_tr.to_numpy()
@@ -60,7 +62,7 @@ def latent_sweep(cleaned: dict, latents=range(1, 22), window: int = 24, frac: fl
     names = cleaned.get("hfd_fullname", {c: c for c in y_te.columns})
     rows, s_ante, s_post, turns, posts = [], [], [], [], []
     for k in latents:
-        ae = AE(xtr, ytr, x_te, y_te, k, device=device, seed=seed)
+        ae = AE(xtr, ytr, x_te, y_te, k, device=device, seed=seed, **({"dtype": dtype} if dtype is not None else {}))
         ae.train(verbose=0, plot=False)
         oos_r2, oos_rmse = ae.model_OOS_r2(), ae.model_OOS_RMSE()
         rows.append({"latent": k, "IS_r2": float(ae.model_IS_r2()), "IS_RMSE": float(ae.model_IS_RMSE()),

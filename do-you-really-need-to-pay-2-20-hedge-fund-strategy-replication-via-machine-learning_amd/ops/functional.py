@@ -313,9 +313,12 @@ def lstm_layer_tfwd(xd, W, tape, U, act: int):
 def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None, impl: int = 0) -> None:
     """All weight gradients of one LSTM layer: gW += X^T dZ (+ Xd^T dZd), gU += H_{t-1}^T dZ (+ ...),
     gb += sum(dZ).  bf16 GPU: ONE fused launch (csrc/wgrad3.hip LDS-DMA streaming kernel where the
-    shape is supported, csrc/gemm2.hip otherwise; ``impl=2`` forces the latter); otherwise
-    per-product calls."""
-    if dZ.dtype == torch.bfloat16 and _nat(dZ):
+    shape is supported, csrc/gemm2.hip otherwise; ``impl=2`` forces the latter); fp32 GPU at the
+    model widths: ONE fused launch of csrc/lstm_f32.hip lstmf_wgrad_kernel; otherwise per-product
+    calls."""
+    f32 = (dZ.dtype == torch.float32 and _LSTMF and x.shape[-1] in (32, 36, 100) and hs.shape[-1] == 100
+           and dZ.shape[-1] == 400)
+    if (dZ.dtype == torch.bfloat16 or f32) and _nat(dZ):
         _ops().lstm_wgrad_(x.contiguous(), hs.contiguous(), dZ.contiguous(), gW, gU, gb,
                            None if xd is None else xd.contiguous(), None if hds is None else hds.contiguous(),
                            None if dZd is None else dZd.contiguous(), int(impl))

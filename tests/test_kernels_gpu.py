@@ -304,17 +304,47 @@ def test_lstm2_fused_layer(cuda, act, B, T, K):
         _close(dXd3, rzd @ Wd.t(), torch.bfloat16, scale=(rzd.abs() @ Wd.abs().t()).max().item())
 
 
-@pytest.mark.parametrize("key", [("lstm", "wgan_gp"), ("lstm", "wgan")])
-def test_trainer_gradients_bf16_fused(cuda, key):
-    """bf16 training step (fused v2 LSTM kernels) vs the fp64 CPU engine: gradient direction agrees."""
+def _block_errors(model_g, model_c):
+    """(global relative L2 error, worst per-parameter-block relative L2 error, block name) of the
+    flat gradients of two copies of one model (every Keras weight is its own block, so an error in
+    one layer cannot be averaged away by the others)."""
+    a_all, b_all = model_g.flat.grad.cpu().double(), model_c.flat.grad.double().cpu()
+    # a block whose exact gradient vanishes (the critic head bias under the Wasserstein terms:
+    # sum of -1/B over real + 1/B over fake = 0) is measured against 1e-3 of the whole gradient
+    floor = 1e-3 * b_all.norm().item()
+    worst, wname = 0.0, ""
+    for (name, _), (_, _) in zip(model_g.named_weights(), model_c.named_weights()):
+        lay = [l for l in model_g.layers for s_ in l.specs if s_.keras == name][0]
+        spec = [s_ for s_ in lay.specs if s_.keras == name][0]
+        n = int(np.prod(spec.shape))
+        a, b = a_all[spec.offset:spec.offset + n], b_all[spec.offset:spec.offset + n]
+        rel = ((a - b).norm() / max(b.norm().item(), floor, 1e-30)).item()
+        if rel > worst:
+            worst, wname = rel, name
+    return ((a_all - b_all).norm() / max(b_all.norm().item(), 1e-30)).item(), worst, wname
+
+
+# bf16 bounds.  Measured on MI355X (r02, profiles/r02_tests/bf16_errors.txt): global 2.7e-3 .. 5.9e-3,
+# worst block 4.0e-3 .. 2.3e-2 (the generator's first LSTM kernel at T = 168).  The compute is bf16
+# MFMA with bf16 activations / tapes against an fp64 reference of the same inputs, so ~1e-2 is the
+# bf16 noise floor; a stale or wrong row tile moves these by O(0.1 .. 1)
+BF16_GLOBAL, BF16_BLOCK = 1.5e-2, 5e-2
+
+
+@pytest.mark.parametrize("key,T,F,B,lrelu", [(("lstm", "wgan_gp"), 24, 32, 64, False), (("lstm", "wgan"), 24, 32, 64, False),
+                                             (("lstm", "wgan_gp"), 24, 32, 256 * 32 + 70, False),
+                                             (("lstm", "wgan_gp"), 168, 36, 40, True)])
+def test_trainer_gradients_bf16_fused(cuda, key, T, F, B, lrelu):
+    """bf16 training step (fused LSTM kernels) vs the fp64 CPU engine: norm-relative error of the
+    whole gradient and of every parameter block.  Cases: the bench shape at small B, a multi-pass
+    batch (more 32-row tiles than CUs + a partial tile), and the production generator shape
+    (T = 168, F = 36, LeakyReLU after the first LSTM)."""
     from hfrep.train.gan_trainer import GANConfig, GANTrainer
 
-    T, F, B = 24, 32, 64
     ds = np.random.RandomState(0).rand(64, T, F).astype(np.float32)
-    tg = GANTrainer(GANConfig(arch=key[0], loss=key[1], window=T, features=F, batch_size=B, dtype="bfloat16"), ds,
-                    device=cuda)
-    tc = GANTrainer(GANConfig(arch=key[0], loss=key[1], window=T, features=F, batch_size=B, dtype="float64"), ds,
-                    param_dtype=torch.float64)
+    kw = dict(arch=key[0], loss=key[1], window=T, features=F, batch_size=B, lrelu_after_first=lrelu)
+    tg = GANTrainer(GANConfig(dtype="bfloat16", **kw), ds, device=cuda)
+    tc = GANTrainer(GANConfig(dtype="float64", **kw), ds, param_dtype=torch.float64)
     with torch.no_grad():
         tc.generator.flat.copy_(tg.generator.flat.double().cpu())
         tc.critic.flat.copy_(tg.critic.flat.double().cpu())
@@ -327,14 +357,14 @@ def test_trainer_gradients_bf16_fused(cuda, key):
             fg = tg.generator.predict(noise.to(cuda, torch.bfloat16))
             tg.critic_gp_grads(real.to(cuda, torch.bfloat16), fg, alpha.to(cuda))
             tc.critic_gp_grads(real.to(torch.bfloat16).double(), fg.double().cpu(), alpha.double())
-            a, b = tg.critic.flat.grad.cpu().double(), tc.critic.flat.grad
-            cos = (a @ b) / (a.norm() * b.norm())
-            assert cos > 0.995, f"critic grad cosine {cos:.4f}"
+            rel, worst, name = _block_errors(tg.critic, tc.critic)
+            print(f"critic bf16 rel {rel:.3e} worst block {worst:.3e} ({name})")
+            assert rel < BF16_GLOBAL and worst < BF16_BLOCK, (rel, worst, name)
         tg.generator_grads(noise.to(cuda, torch.bfloat16))
         tc.generator_grads(noise.to(torch.bfloat16).double())
-        a, b = tg.generator.flat.grad.cpu().double(), tc.generator.flat.grad
-        cos = (a @ b) / (a.norm() * b.norm())
-        assert cos > 0.995, f"generator grad cosine {cos:.4f}"
+        rel, worst, name = _block_errors(tg.generator, tc.generator)
+        print(f"generator bf16 rel {rel:.3e} worst block {worst:.3e} ({name})")
+        assert rel < BF16_GLOBAL and worst < BF16_BLOCK, (rel, worst, name)
 
 
 @pytest.mark.parametrize("impl", [0, 2])
@@ -607,3 +637,30 @@ def test_lstmf_persistent_multi_pass(cuda):
     rh, rg, rc = R.lstm_seq_fwd(x.double() @ W.double() + b.double(), U.double(), 2)
     _close(hs, rh, torch.float32)
     _close(cs, rc, torch.float32)
+
+
+@pytest.mark.parametrize("B,T,K,tangent", [(70, 24, 32, False), (33, 12, 100, True), (1000, 24, 100, False),
+                                           (41, 5, 36, True)])
+def test_lstmf_wgrad_fused(cuda, B, T, K, tangent):
+    """fp32 fused LSTM weight gradient (one launch for every product) vs fp64."""
+    from hfrep.ops import functional as Fn
+
+    H, N = 100, 400
+    g = torch.Generator().manual_seed(23)
+    x, hs, dz = torch.randn(B, T, K, generator=g), torch.randn(B, T, H, generator=g), torch.randn(B, T, N, generator=g)
+    xd, hds, dzd = (torch.randn(B, T, K, generator=g), torch.randn(B, T, H, generator=g),
+                    torch.randn(B, T, N, generator=g)) if tangent else (None, None, None)
+    gW0, gU0, gb0 = torch.randn(K, N, generator=g), torch.randn(H, N, generator=g), torch.randn(N, generator=g)
+    gW, gU, gb = gW0.clone().to(cuda), gU0.clone().to(cuda), gb0.clone().to(cuda)
+    dev = lambda t: None if t is None else t.to(cuda)  # noqa: E731
+    Fn.lstm_wgrad_(dev(x), dev(hs), dev(dz), gW, gU, gb, dev(xd), dev(hds), dev(dzd))
+    X, Hp, D = x.double().reshape(-1, K), R.shift_prev(hs.double()).reshape(-1, H), dz.double().reshape(-1, N)
+    rW, rU, rb = gW0.double() + X.t() @ D, gU0.double() + Hp.t() @ D, gb0.double() + D.sum(0)
+    sW, sU = (X.abs().t() @ D.abs()).max().item(), (Hp.abs().t() @ D.abs()).max().item()
+    if tangent:
+        Xd, Hdp, Dd = xd.double().reshape(-1, K), R.shift_prev(hds.double()).reshape(-1, H), dzd.double().reshape(-1, N)
+        rW, rU = rW + Xd.t() @ Dd, rU + Hdp.t() @ Dd
+        sW, sU = sW + (Xd.abs().t() @ Dd.abs()).max().item(), sU + (Hdp.abs().t() @ Dd.abs()).max().item()
+    _close(gW, rW, torch.float32, scale=sW)
+    _close(gU, rU, torch.float32, scale=sU)
+    _close(gb, rb, torch.float32, scale=D.abs().sum(0).max().item())
