@@ -190,6 +190,34 @@ def wasserstein_parity(real_train, real_holdout, fake, seed=0):
             "w_uniform_vs_real": float(w_unif), "n": int(n)}
 
 
+REFERENCE_GENERATOR = "GAN/trained_generator/old/MTSS_WGAN_GP20220613_20-40-15.h5"  # 48 x 35 LSTM G (MTSS_WGAN_GP.py)
+
+
+def reference_anchor(h5: str | None = None, seed: int = 123, n: int = 1000, window: int = 48, features: int = 35,
+                     device="cpu"):
+    """W-dist of the REFERENCE's own trained generator under the parity protocol: 1000 windows from
+    N(0,1) noise (the trainer's generate() stream, seed + 7) vs the held-out real windows (seed +
+    1000) of the MinMax-scaled cleaned panel, with the real-vs-real floor.  This is the number a
+    reference-semantics training run should land near (GAN/GAN_eval.py:309-326; the .h5 is the
+    author's MTSS-WGAN-GP generator, GAN/MTSS_WGAN_GP.py:285-287)."""
+    import torch
+
+    from .data.io import require_data_root
+    from .utils import checkpoint
+    from .utils.rng import DeviceRNG
+
+    h5 = h5 or os.path.join(require_data_root(), REFERENCE_GENERATOR)
+    g, _ = checkpoint.load_generator(h5, device=device)
+    train = _dataset("cleaned", n, window, features, seed)
+    hold = _dataset("cleaned", n, window, features, seed + 1000)
+    rng = DeviceRNG(seed + 7, torch.device(device), stream=10_000)
+    with torch.no_grad():
+        fake = g.predict(rng.normal((n, window, features), dtype=torch.float32)).float().cpu().numpy()
+    res = wasserstein_parity(train, hold, fake)
+    res["generator"] = os.path.basename(h5)
+    return res
+
+
 def cmd_parity(a) -> int:
     import torch
 
@@ -206,8 +234,15 @@ def cmd_parity(a) -> int:
     fake = tr.generate(len(hold), seed=s["seed"] + 7)
     res = wasserstein_parity(tr.dataset.float().cpu().numpy(), hold, fake)
     res.update(model=a.model, preset=a.preset, iterations=tr.iteration, dtype=s["dtype"],
-               batch_size=s["batch_size"], world=tr.world,
+               batch_size=s["batch_size"], world=tr.world, seed=s["seed"],
                device=torch.cuda.get_device_name() if tr.device.type == "cuda" else "cpu")
+    if a.preset == "reference" and s["window"] == 48 and s["features"] == 35 and s["data"] == "cleaned":
+        try:  # the reference's own trained generator under the same protocol (absent data: skipped)
+            anc = reference_anchor(seed=s["seed"])
+            res.update(w_reference_generator=anc["w_fake_vs_real"], reference_generator=anc["generator"],
+                       w_abs_diff_vs_reference=abs(res["w_fake_vs_real"] - anc["w_fake_vs_real"]))
+        except FileNotFoundError:
+            pass
     print(json.dumps(res))
     if a.out:
         with open(a.out, "w") as fh:

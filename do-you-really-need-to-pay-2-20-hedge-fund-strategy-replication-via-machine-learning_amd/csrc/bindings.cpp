@@ -263,7 +263,7 @@ std::tuple<Tensor, Tensor> lstm_tbwd(optional<Tensor> dH, Tensor dHd, Tensor gat
 // ------------------------------------------------------------------------------------ LSTM fp32 fused
 bool lstmf_supported(int64_t H, int64_t K, int64_t act) { return hfrep::lstmf_supported((int)H, (int)K, (int)act); }
 
-std::tuple<Tensor, Tensor, Tensor> lstmf_fwd(Tensor x, Tensor W, optional<Tensor> b, Tensor U, int64_t act, bool save) {
+std::tuple<Tensor, Tensor> lstmf_fwd(Tensor x, Tensor W, optional<Tensor> b, Tensor U, int64_t act, bool save) {
   CHECK_F32(x); CHECK_F32(W);
   TORCH_CHECK(x.dim() == 3, "x must be (B, T, K)");
   const int B = x.size(0), Tn = x.size(1), K = x.size(2), H = U.size(0);
@@ -273,35 +273,64 @@ std::tuple<Tensor, Tensor, Tensor> lstmf_fwd(Tensor x, Tensor W, optional<Tensor
   TORCH_CHECK(hfrep::lstmf_supported(H, K, (int)act), "lstmf_fwd: unsupported H/K/act");
   GUARD(x);
   Tensor hs = out_empty({B, Tn, H}, x.options());
-  Tensor gates = save ? out_empty({B, Tn, 4 * H}, x.options()) : out_empty({0}, x.options());
-  Tensor cs = save ? out_empty({B, Tn, H}, x.options()) : out_empty({0}, x.options());
+  Tensor tape = at::empty({save ? (int64_t)hfrep::lstmf_tape_elems(B, Tn) : 0}, x.options());  // (padding slots unwritten)
   const bool ok = hfrep::launch_lstmf_fwd(x.data_ptr<float>(), W.data_ptr<float>(),
                                           b.has_value() ? b->data_ptr<float>() : nullptr, U.data_ptr<float>(),
-                                          hs.data_ptr<float>(), save ? gates.data_ptr<float>() : nullptr,
-                                          save ? cs.data_ptr<float>() : nullptr, B, Tn, K, H, (int)act, cur_stream(x));
+                                          hs.data_ptr<float>(), save ? tape.data_ptr<float>() : nullptr, B, Tn, K, H,
+                                          (int)act, cur_stream(x));
   TORCH_CHECK(ok, "lstmf_fwd: launch failed");
-  return {hs, gates, cs};
+  return {hs, tape};
 }
 
-std::tuple<Tensor, Tensor, Tensor> lstmf_tfwd(Tensor xd, Tensor W, Tensor U, Tensor gates, Tensor cs, int64_t act) {
-  CHECK_F32(xd); CHECK_F32(W); CHECK_F32(gates); CHECK_F32(cs);
+std::tuple<Tensor, Tensor> lstmf_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int64_t act) {
+  CHECK_F32(xd); CHECK_F32(W); CHECK_F32(tape);
   TORCH_CHECK(xd.dim() == 3, "xd must be (B, T, K)");
   const int B = xd.size(0), Tn = xd.size(1), K = xd.size(2), H = U.size(0);
   check_lstm_U(U, H);
   TORCH_CHECK(W.size(0) == K && W.size(1) == 4 * H, "W must be (K, 4H)");
-  TORCH_CHECK(gates.dim() == 3 && gates.size(0) == B && gates.size(1) == Tn && gates.size(2) == 4 * H, "gates shape");
-  TORCH_CHECK(cs.dim() == 3 && cs.size(0) == B && cs.size(1) == Tn && cs.size(2) == H, "cs shape");
+  TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstmf_tape_elems(B, Tn), "lstmf_tfwd: tape size");
   TORCH_CHECK(hfrep::lstmf_supported(H, K, (int)act), "lstmf_tfwd: unsupported H/K/act");
   GUARD(xd);
   Tensor hds = out_empty({B, Tn, H}, xd.options());
-  Tensor zds = out_empty({B, Tn, 4 * H}, xd.options());
-  Tensor cds = out_empty({B, Tn, H}, xd.options());
+  Tensor ttape = at::empty_like(tape);
   const bool ok = hfrep::launch_lstmf_tfwd(xd.data_ptr<float>(), W.data_ptr<float>(), U.data_ptr<float>(),
-                                           gates.data_ptr<float>(), cs.data_ptr<float>(), hds.data_ptr<float>(),
-                                           zds.data_ptr<float>(), cds.data_ptr<float>(), B, Tn, K, H, (int)act,
-                                           cur_stream(xd));
+                                           tape.data_ptr<float>(), hds.data_ptr<float>(), ttape.data_ptr<float>(), B, Tn,
+                                           K, H, (int)act, cur_stream(xd));
   TORCH_CHECK(ok, "lstmf_tfwd: launch failed");
-  return {hds, zds, cds};
+  return {hds, ttape};
+}
+
+Tensor lstmf_bwd(optional<Tensor> dH, Tensor tape, Tensor U, int64_t act, int64_t B, int64_t Tn) {
+  CHECK_F32(tape);
+  const int H = U.size(0);
+  check_lstm_U(U, H);
+  TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstmf_tape_elems(B, Tn), "lstmf_bwd: tape size");
+  if (dH.has_value()) { CHECK_F32(*dH); TORCH_CHECK(dH->numel() == B * Tn * H, "lstmf_bwd: dH shape"); }
+  GUARD(tape);
+  Tensor dZ = out_empty({B, Tn, 4 * H}, tape.options());
+  const bool ok = hfrep::launch_lstmf_bwd(dH.has_value() ? dH->data_ptr<float>() : nullptr, tape.data_ptr<float>(),
+                                          U.data_ptr<float>(), dZ.data_ptr<float>(), B, Tn, H, (int)act,
+                                          cur_stream(tape));
+  TORCH_CHECK(ok, "lstmf_bwd: unsupported H / act");
+  return dZ;
+}
+
+std::tuple<Tensor, Tensor> lstmf_tbwd(optional<Tensor> dH, optional<Tensor> dHd, Tensor tape, Tensor ttape, Tensor U,
+                                      int64_t act, int64_t B, int64_t Tn) {
+  CHECK_F32(tape); CHECK_F32(ttape);
+  const int H = U.size(0);
+  check_lstm_U(U, H);
+  TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstmf_tape_elems(B, Tn) && ttape.numel() == tape.numel(), "tape size");
+  for (const auto* d : {&dH, &dHd})
+    if (d->has_value()) { CHECK_F32(**d); TORCH_CHECK((*d)->numel() == B * Tn * H, "lstmf_tbwd: adjoint shape"); }
+  GUARD(tape);
+  Tensor dZ = out_empty({B, Tn, 4 * H}, tape.options()), dZd = out_empty({B, Tn, 4 * H}, tape.options());
+  const bool ok = hfrep::launch_lstmf_tbwd(dH.has_value() ? dH->data_ptr<float>() : nullptr,
+                                           dHd.has_value() ? dHd->data_ptr<float>() : nullptr, tape.data_ptr<float>(),
+                                           ttape.data_ptr<float>(), U.data_ptr<float>(), dZ.data_ptr<float>(),
+                                           dZd.data_ptr<float>(), B, Tn, H, (int)act, cur_stream(tape));
+  TORCH_CHECK(ok, "lstmf_tbwd: unsupported H / act");
+  return {dZ, dZd};
 }
 
 // ------------------------------------------------------------------------------------ LSTM v2 (bf16 fused)
@@ -619,8 +648,10 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstm_tfwd(Tensor dzx, Tensor gates, Tensor cs, Tensor U, int act) -> (Tensor, Tensor, Tensor)");
   m.def("lstm_tbwd(Tensor? dH, Tensor dHd, Tensor gates, Tensor cs, Tensor zds, Tensor cds, Tensor U, int act) -> (Tensor, Tensor)");
   m.def("lstmf_supported(int H, int K, int act) -> bool", &lstmf_supported);  // no tensor inputs: catch-all kernel
-  m.def("lstmf_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor, Tensor)");
-  m.def("lstmf_tfwd(Tensor xd, Tensor W, Tensor U, Tensor gates, Tensor cs, int act) -> (Tensor, Tensor, Tensor)");
+  m.def("lstmf_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
+  m.def("lstmf_bwd(Tensor? dH, Tensor tape, Tensor U, int act, int B, int T) -> Tensor");
+  m.def("lstmf_tbwd(Tensor? dH, Tensor? dHd, Tensor tape, Tensor ttape, Tensor U, int act, int B, int T) -> (Tensor, Tensor)");
+  m.def("lstmf_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int act) -> (Tensor, Tensor)");
   m.def("lstm2_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
   m.def("lstm2_bwd(Tensor? dH, Tensor tape, Tensor U, int act, Tensor? W=None, bool need_dz=True, Tensor? head_d=None, "
         "Tensor? head_w=None) -> (Tensor, Tensor)");
@@ -657,6 +688,8 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("lstm_fwd", &lstm_fwd);
   m.impl("lstmf_fwd", &lstmf_fwd);
   m.impl("lstmf_tfwd", &lstmf_tfwd);
+  m.impl("lstmf_bwd", &lstmf_bwd);
+  m.impl("lstmf_tbwd", &lstmf_tbwd);
   m.impl("lstm_bwd", &lstm_bwd);
   m.impl("lstm_tfwd", &lstm_tfwd);
   m.impl("lstm_tbwd", &lstm_tbwd);

@@ -41,13 +41,19 @@ void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const 
                        const float* hw = nullptr);
 
 // ---- lstm_f32.hip (fp32, fused input projection, exact-fp32 MFMA; H == 100, K in {32, 35, 36, 100},
-//      act in {linear, sigmoid, tanh}; false = not supported).  Row-major v1-contract outputs. ----
+//      act in {linear, sigmoid, tanh}; false = not supported).  Tapes: lane-native blocked fp32
+//      (lstmf_tape_elems floats; primal = gate activations + c, tangent = zdot + cdot). ----
 bool lstmf_supported(int H, int K, int act);
-bool launch_lstmf_fwd(const float* x, const float* W, const float* b, const float* U, float* hs, float* gates, float* cs,
-                      int B, int Tn, int K, int H, int act, hipStream_t s);
-bool launch_lstmf_tfwd(const float* xd, const float* W, const float* U, const float* gates, const float* cs, float* hds,
-                       float* zds, float* cds, int B, int Tn, int K, int H, int act, hipStream_t s);
-
+size_t lstmf_tape_elems(int B, int Tn);
+bool launch_lstmf_fwd(const float* x, const float* W, const float* b, const float* U, float* hs, float* tape, int B,
+                      int Tn, int K, int H, int act, hipStream_t s);
+bool launch_lstmf_tfwd(const float* xd, const float* W, const float* U, const float* tape, float* hds, float* ttape,
+                       int B, int Tn, int K, int H, int act, hipStream_t s);
+// BPTT / tangent reverse on those tapes (dH / dHd may be null = zeros); dZ / dZd row-major (B,T,4H)
+bool launch_lstmf_bwd(const float* dH, const float* tape, const float* U, float* dZ, int B, int Tn, int H, int act,
+                      hipStream_t s);
+bool launch_lstmf_tbwd(const float* dH, const float* dHd, const float* tape, const float* ttape, const float* U, float* dZ,
+                       float* dZd, int B, int Tn, int H, int act, hipStream_t s);
 // fused fp32 LSTM weight gradients (K in {32, 36, 100}, H = 100, N = 400): gW += X^T dZ (+ Xd^T dZd),
 // gU += Hprev^T dZ (+ Hdprev^T dZd), gb += colsum dZ, through per-workgroup slabs in ws
 // (lstmf_wgrad_workspace_floats) and one fixed-order reduce

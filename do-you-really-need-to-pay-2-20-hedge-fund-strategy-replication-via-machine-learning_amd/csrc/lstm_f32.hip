@@ -39,6 +39,7 @@ namespace hfrep {
 namespace {
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef int v4i_t __attribute__((ext_vector_type(4)));
 constexpr int kOOB = 0x7fff0000;  // voffset past every descriptor's num_records (see lstm2.hip)
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, int bytes) {
@@ -148,6 +149,29 @@ struct FXPart {
   }
 };
 
+// fp32 tape: a lane-native blocked layout.  Per (32-row block, step) and per wave w and accumulator
+// pair (m, n) one SLOT of 64 lanes x {4 gate values (16 bytes), 1 cell value}: the lane that computed
+// the (row, unit) in the forward reads it back in the reverse kernels, and every wave-level access is
+// a contiguous 1 KiB (gates) or 256 B (cell).  Primal tape: gate activations (i, f, g, o) and c_t;
+// tangent tape: the gate pre-activation tangents zdot and cdot.  Slots of wave 3's padding tiles
+// (units 100..111) are never written nor read.
+constexpr int FT_MN = 2 * FNT, FT_SLOT = 64 * 5, FT_STEP = 4 * FT_MN * FT_SLOT;
+__device__ __forceinline__ rsrc_t ftape_rsrc(const float* tape, int rb, int nrb, int Tn) {
+  rb = __builtin_amdgcn_readfirstlane(rb);
+  const bool on = tape && rb < nrb;
+  return make_rsrc(tape + (on ? (size_t)rb * Tn * FT_STEP : 0), on ? Tn * FT_STEP * 4 : 0);
+}
+// byte offset of this lane's gate quad in slot (w, m, n) at step 0; the cell value is at +1024 - 12 lane
+__device__ __forceinline__ int ftape_lane(int w, int lane) { return (w * FT_MN * FT_SLOT) * 4 + lane * 16; }
+__device__ __forceinline__ int ftape_cell(int w, int lane) { return (w * FT_MN * FT_SLOT + 256 + lane) * 4; }
+__device__ __forceinline__ constexpr int ftape_slot(int m, int n) { return (m * FNT + n) * FT_SLOT * 4; }
+__device__ __forceinline__ f32x4 ld4(rsrc_t r, int voff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
+__device__ __forceinline__ void st4(f32x4 v, rsrc_t r, int voff) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), r, voff, 0, 0);
+}
+
 }  // namespace
 
 // ==========================================================================================
@@ -156,8 +180,8 @@ struct FXPart {
 template <int ACT, int KX, bool TAPE, bool TAN>
 __global__ void __launch_bounds__(256, 1)
 lstmf_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
-                 const float* __restrict__ U, const float* __restrict__ pgates, const float* __restrict__ pcs,
-                 float* __restrict__ hs, float* __restrict__ gout, float* __restrict__ cout, int B, int Tn) {
+                 const float* __restrict__ U, const float* __restrict__ ptape, float* __restrict__ hs,
+                 float* __restrict__ tape, int B, int Tn) {
   using GX = FGeo<KX>;
   using GH = FGeo<FH>;
   constexpr int NWR = f_nwr<KX>(), NWL = f_nwl<KX>();
@@ -218,24 +242,22 @@ lstmf_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W, const
     const int row0 = rb * 32;
     const rsrc_t rx = ftile_rsrc(x, row0, B, Tn, KX);
     const rsrc_t rh = ftile_rsrc(hs, row0, B, Tn, FH);
-    const rsrc_t rgo = ftile_rsrc(gout, row0, B, Tn, FG);
-    const rsrc_t rco = ftile_rsrc(cout, row0, B, Tn, FH);
-    const rsrc_t rpg = ftile_rsrc(TAN ? pgates : nullptr, row0, B, Tn, FG);
-    const rsrc_t rpc = ftile_rsrc(TAN ? pcs : nullptr, row0, B, Tn, FH);
-    // byte offsets at step 0 of this lane's rows (the descriptors cover rows < B only, so a row
-    // past B is out of range by itself): post-transpose (row 16 m + 4 g + q, unit ub) of (B,T,H) and
-    // (B,T,4H); pre-transpose row 16 m + 4 g at column q H + ub of (B,T,4H).  Every store / load
-    // offset below is (this base + t * row stride) + an immediate, so nothing per tile is hoisted
-    // out of the step loop into registers.
-    int vp1[2], vp4[2], vq4[2];
+    const rsrc_t rt = ftape_rsrc(TAPE ? tape : nullptr, rb, nrb, Tn);  // primal (or tangent) tape out
+    const rsrc_t rp = ftape_rsrc(TAN ? ptape : nullptr, rb, nrb, Tn);  // tangent: the primal tape
+    // byte offsets at step 0 of this lane's (row 16 m + 4 g + q, unit ub) in (B,T,H) (the descriptor
+    // covers rows < B only, so a row past B is out of range by itself); every offset below is
+    // (base + t * step stride) + an immediate, so nothing per tile is hoisted out of the step loop
+    int vp1[2];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int r = 16 * m + 4 * g + q, r0 = 16 * m + 4 * g;
-      vp1[m] = (r * Tn * FH + ub) * 4;
-      vp4[m] = (r * Tn * FG + ub) * 4;
-      vq4[m] = (r0 * Tn * FG + q * FH + ub) * 4;
+    for (int m = 0; m < 2; ++m) vp1[m] = ((16 * m + 4 * g + q) * Tn * FH + ub) * 4;
+    const int tl = ftape_lane(w, lane), tcl = ftape_cell(w, lane);
+    float cprev[TAN ? 2 : 1][FNT];  // tangent: c_{t-1} of the primal (carried)
+    if constexpr (TAN) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < FNT; ++n) cprev[m][n] = 0.f;
     }
-    const int rs4 = Tn * FG * 4;  // row stride of (B,T,4H)
     float cst[2][FNT];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -254,18 +276,17 @@ lstmf_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W, const
       xp.load(rx, Tn, t + 1, t + 1 < Tn);  // x_{t+1}: lands during this step's MFMAs
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
-        // tangent: primal gates of this lane's 4 accumulator rows, c_t and c_{t-1} of its (row, unit);
+        // tangent: the primal gates and c_t of this lane's (row, unit), from its own tape slots;
         // issued before this half's MFMAs, consumed after them
-        float py[TAN ? FNT : 1][4], pc0[TAN ? FNT : 1], pc1[TAN ? FNT : 1];
-        const int p1 = vp1[m] + t * FH * 4, p4 = vp4[m] + t * FG * 4, q4 = vq4[m] + t * FG * 4;
+        f32x4 pg[TAN ? FNT : 1];
+        float pc[TAN ? FNT : 1];
+        const int p1 = vp1[m] + t * FH * 4, tb = t * FT_STEP * 4;
         if constexpr (TAN) {
 #pragma unroll
           for (int n = 0; n < FNT; ++n) {
             const bool tok = !(w == 3 && n >= 4);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) py[n][i] = ld1(rpg, tok ? q4 + i * rs4 + 16 * n : kOOB, 0);
-            pc0[n] = ld1(rpc, tok ? p1 + 16 * n : kOOB, 0);
-            pc1[n] = ld1(rpc, (tok && t > 0) ? p1 - FH * 4 + 16 * n : kOOB, 0);
+            pg[n] = ld4(rp, tok ? tl + tb + ftape_slot(m, n) : kOOB);
+            pc[n] = ld1(rp, tok ? tcl + tb + ftape_slot(m, n) : kOOB, 0);
           }
         }
         f32x4 acc[FNT];
@@ -323,32 +344,26 @@ lstmf_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W, const
             hv = tok ? y[3] * ca : 0.f;
             cst[m][n] = cn;
             if constexpr (TAPE) {
-              const int v4 = tok ? p4 + 16 * n : kOOB;
-#pragma unroll
-              for (int k = 0; k < 4; ++k) st1(y[k], rgo, v4 + k * FH * 4, 0);
-              st1(cn, rco, v1, 0);
+              st4(f32x4{y[0], y[1], y[2], y[3]}, rt, tok ? tl + tb + ftape_slot(m, n) : kOOB);
+              st1(cn, rt, tok ? tcl + tb + ftape_slot(m, n) : kOOB, 0);
             }
           } else {
-            float gd[4], y[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float yy = py[n][i];
-              const float der = q == 2 ? act_dy(ACT, yy) : yy * (1.f - yy);
-              gd[i] = der * acc[n][i];
-              y[i] = yy;
-              // zdot, pre-transpose: row 16 m + 4 g + i, gate q, unit ub + 4 n
-              st1(acc[n][i], rgo, tok ? q4 + i * rs4 + 16 * n : kOOB, 0);
-            }
-            quad_transpose(gd, q);
-            quad_transpose(y, q);
-            const float c = pc0[n], cp = pc1[n];
-            float cdn = gd[1] * cp + y[1] * cst[m][n] + gd[0] * y[2] + y[0] * gd[2];
+            // zdot of (row, unit) for all four gates: transpose the accumulator quad
+            float zd[4] = {acc[n][0], acc[n][1], acc[n][2], acc[n][3]};
+            quad_transpose(zd, q);
+            const f32x4 y = pg[n];
+            const float idot = y[0] * (1.f - y[0]) * zd[0], fdot = y[1] * (1.f - y[1]) * zd[1];
+            const float gdot = act_dy(ACT, y[2]) * zd[2], odot = y[3] * (1.f - y[3]) * zd[3];
+            const float c = pc[n];
+            float cdn = fdot * cprev[m][n] + y[1] * cst[m][n] + idot * y[2] + y[0] * gdot;
             const float ca = act_f(ACT, c);
-            float hd = gd[3] * ca + y[3] * act_dy(ACT, ca) * cdn;
+            float hd = odot * ca + y[3] * act_dy(ACT, ca) * cdn;
             if (!tok) { cdn = 0.f; hd = 0.f; }
             cst[m][n] = cdn;
+            cprev[m][n] = c;
             hv = hd;
-            st1(cdn, rco, v1, 0);
+            st4(f32x4{zd[0], zd[1], zd[2], zd[3]}, rt, tok ? tl + tb + ftape_slot(m, n) : kOOB);
+            st1(cdn, rt, tok ? tcl + tb + ftape_slot(m, n) : kOOB, 0);
           }
           hnext[hw + 16 * m * GH::LR + n] = hv;  // padded units (u < 112) write their zeros
           st1(hv, rh, v1, 0);
@@ -357,6 +372,346 @@ lstmf_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W, const
       xp.to_lds(xb + ((t + 1) & 1) * 32 * GX::LR, trash);
       lds_barrier();
     }
+  }
+}
+
+// ==========================================================================================
+// BPTT (fp32): dZ_t = dL/dz_t (ops/reference.py lstm_seq_bwd) from the row-major fp32 tapes
+// ==========================================================================================
+// Same wave / lane decomposition as the forward: after the quad transpose lane (g, j4, q) of wave
+// w owns (row 16 m + 4 g + q, unit 28 w + 4 n + j4) for m < 2, n < 7, and keeps that cell's dc.
+// Per step, two phases between LDS barriers:
+//   A. dh_rec = dz_{t+1} U^T on 16x16x4 MFMAs: A = the dz tile in LDS (k = 4 u' + q, row layout
+//      [q][u'] so one ds_read_b128 feeds four k-steps), B = U^T fragments pinned in AGPRs; wave w
+//      owns output column tiles 2 w, 2 w + 1 (16 units each) for both row halves (400 MFMAs), and
+//      the step's tape / dH loads are issued before it so their latency hides under the MFMAs;
+//   B. the cell adjoint math per (row, unit), dZ_t to HBM (row-major, for the weight gradient and the
+//      input-gradient GEMM) and to the dz tile for the next step.
+constexpr int BZ_KQ = 100, BZ_LR = 408, BH_LR = 116;  // dz tile: conflict-free b128 reads (scripted search)
+
+// dZ_{t+1} leaves through 16-byte row-major stores read back from the dz tile during phase A of step
+// t (the tile holds it anyway), and step t-1's tape loads are issued at the end of phase B of step t,
+// reusing the registers just consumed: every load is older than the stores it could queue behind
+// (vmcnt retires loads and stores in issue order), and every store is coalesced.
+// step t's tape for the BPTT: the gate quad at t and c_{t-1} (c_t is carried from the step above)
+__device__ __forceinline__ void bwdf_tape_load(f32x4& tg, float& tcp, float& tdh, rsrc_t rt, rsrc_t rdh, int og, int ocp,
+                                               int p1, bool tok, bool prev) {
+  tg = ld4(rt, tok ? og : kOOB);
+  tcp = ld1(rt, (tok && prev) ? ocp : kOOB, 0);
+  tdh = ld1(rdh, tok ? p1 : kOOB, 0);
+}
+// the dz tile (32 rows x [q][u'], u' < 100) -> dZ[:, t, :] (row-major, 4H per row) in 16-byte chunks:
+// threads 0..199 own chunk (tid % 100) of rows 2 k + tid / 100 (k < 16); the row step lives in the
+// uniform soffset, so a thread holds one LDS and one global base (rows past B: voffset out of range)
+struct BwdfStore {
+  int lo, go, rr;
+  __device__ __forceinline__ void set(int tid, int Tn) {
+    rr = tid / 100;
+    const int ch = tid - 100 * rr, qq = ch / 25, c = ch - 25 * qq;
+    lo = (rr & 1) * BZ_LR + qq * BZ_KQ + 4 * c;
+    go = tid < 200 ? (rr * Tn * FG + qq * FH + 4 * c) * 4 : kOOB;
+  }
+  __device__ __forceinline__ void store(const float* zt, rsrc_t rz, int Tn, int t, int nr) const {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(zt + lo + 2 * k * BZ_LR);
+      // (16-byte store with soffset != 0 and data overwritten right after: the data VGPRs are the
+      // ds_read result, not re-written by VALU before the store retires its operands)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rz, 2 * k + rr < nr ? go : kOOB,
+                                             (2 * k * Tn + t) * FG * 4, 0);
+    }
+  }
+};
+
+// 16-row variant for the tangent reverse: threads 0..199 own chunk tid % 100 of rows 2 k + tid / 100
+__device__ __forceinline__ void bwdf_store16(const float* zt, rsrc_t rz, int Tn, int t, int nr, int tid) {
+  const int rr = tid / 100, ch = tid - 100 * rr, qq = ch / 25, c = ch - 25 * qq;
+  const int lo = (rr & 1) * BZ_LR + qq * BZ_KQ + 4 * c;
+  const int go = tid < 200 ? (rr * Tn * FG + qq * FH + 4 * c) * 4 : kOOB;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(zt + lo + 2 * k * BZ_LR);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rz, 2 * k + rr < nr ? go : kOOB,
+                                           (2 * k * Tn + t) * FG * 4, 0);
+  }
+}
+
+template <int ACT>
+__global__ void __launch_bounds__(256, 1)
+lstmf_bwd_kernel(const float* __restrict__ dH, const float* __restrict__ tape, const float* __restrict__ U,
+                 float* __restrict__ dZ, int B, int Tn) {
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  float* zt = fsm;                  // dz_{t+1} tile [32][BZ_LR]: [q][u'] per row
+  float* ht = zt + 32 * BZ_LR;      // dh_rec tile [32][BH_LR]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane & 3, g = lane >> 4, j4 = (lane & 15) >> 2, c16 = lane & 15;
+  const int ub = FUW * w + j4;
+  const int nrb = (B + 31) / 32;
+  // U^T fragments: B[k = 4 u' + g][col c16 of output tile nt] = U[16 nt + c16][g H + u']
+  float ut[2][FH];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int j = 16 * (2 * w + e) + c16;
+    const bool ok = j < FH;
+#pragma unroll
+    for (int k = 0; k < FH; ++k) {
+      const float v = U[(ok ? j : 0) * FG + g * FH + k];
+      ut[e][k] = ok ? v : 0.f;
+      asm volatile("" : "+a"(ut[e][k]));
+    }
+  }
+  const int hr = (4 * g + q) * BH_LR + ub, zw = (4 * g + q) * BZ_LR + ub;  // (+16 m rows, + 4 n units)
+  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+    const int row0 = rb * 32;
+    const rsrc_t rdh = ftile_rsrc(dH, row0, B, Tn, FH), rt = ftape_rsrc(tape, rb, nrb, Tn);
+    const rsrc_t rz = ftile_rsrc(dZ, row0, B, Tn, FG);
+    const int nr = min(32, B - row0);
+    BwdfStore st;
+    st.set(tid, Tn);
+    int vp1[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) vp1[m] = ((16 * m + 4 * g + q) * Tn * FH + ub) * 4;
+    const int tl = ftape_lane(w, lane), tcl = ftape_cell(w, lane);
+    float dc[2][FNT], tc[2][FNT];
+    f32x4 tg[2][FNT];
+    float tcp[2][FNT], tdh[2][FNT];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < FNT; ++n) {
+        const bool tok = !(w == 3 && n >= 4);
+        const int T1 = Tn - 1;
+        dc[m][n] = 0.f;
+        tc[m][n] = ld1(rt, tok ? tcl + T1 * FT_STEP * 4 + ftape_slot(m, n) : kOOB, 0);  // c_{T-1}
+        bwdf_tape_load(tg[m][n], tcp[m][n], tdh[m][n], rt, rdh, tl + T1 * FT_STEP * 4 + ftape_slot(m, n),
+                       tcl + (T1 - 1) * FT_STEP * 4 + ftape_slot(m, n), vp1[m] + T1 * FH * 4 + 16 * n, tok, T1 > 0);
+      }
+    for (int i = tid; i < 32 * BZ_LR; i += 256) zt[i] = 0.f;  // dz_T = 0
+    __syncthreads();
+    for (int t = Tn - 1; t >= 0; --t) {
+      // ---- phase A: dZ_{t+1} out of the tile; dh_rec = dz_{t+1} U^T ----
+      if (t < Tn - 1) st.store(zt, rz, Tn, t + 1, nr);
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        const float* ar = zt + (16 * m + c16) * BZ_LR + g * BZ_KQ;
+#pragma unroll
+        for (int jj = 0; jj < FH / 4; ++jj) {
+          const f32x4 a4 = *reinterpret_cast<const f32x4*>(ar + 4 * jj);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            acc[0] = mma4(a4[s], ut[0][4 * jj + s], acc[0]);
+            acc[1] = mma4(a4[s], ut[1][4 * jj + s], acc[1]);
+          }
+          if ((jj & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int col = 16 * (2 * w + e) + c16;
+          if (2 * w + e < 7) {  // (wave 3's second tile is past the 112-unit tile: uniform skip)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ht[(16 * m + 4 * g + i) * BH_LR + col] = acc[e][i];
+          }
+        }
+      }
+      lds_barrier();
+      // ---- phase B: cell adjoints -> dz_t tile; then step t-1's tape loads ----
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+#pragma unroll
+        for (int n = 0; n < FNT; ++n) {
+          const bool tok = !(w == 3 && n >= 4);
+          const float ig = tg[m][n][0], fg = tg[m][n][1], gg = tg[m][n][2], og = tg[m][n][3];
+          const float dht = tdh[m][n] + ht[hr + 16 * m * BH_LR + 4 * n];
+          const float ca = act_f(ACT, tc[m][n]);
+          const float dov = dht * ca;
+          const float dct = dc[m][n] + dht * og * act_dy(ACT, ca);
+          dc[m][n] = tok ? dct * fg : 0.f;
+          float z4[4];
+          z4[0] = dct * gg * ig * (1.f - ig);
+          z4[1] = dct * tcp[m][n] * fg * (1.f - fg);
+          z4[2] = dct * ig * act_dy(ACT, gg);
+          z4[3] = dov * og * (1.f - og);
+          if (tok) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) zt[zw + 16 * m * BZ_LR + k * BZ_KQ + 4 * n] = z4[k];
+          }
+          tc[m][n] = tcp[m][n];  // c_{t-1} is the next step's c
+          const int tp = t > 0 ? t - 1 : 0;
+          bwdf_tape_load(tg[m][n], tcp[m][n], tdh[m][n], rt, rdh, tl + tp * FT_STEP * 4 + ftape_slot(m, n),
+                         tcl + (tp - 1) * FT_STEP * 4 + ftape_slot(m, n), vp1[m] + tp * FH * 4 + 16 * n, tok && t > 0,
+                         tp > 0);
+          __builtin_amdgcn_sched_barrier(0);  // consume-then-reload per cell: one register set
+        }
+      }
+      lds_barrier();
+    }
+    st.store(zt, rz, Tn, 0, nr);
+    __syncthreads();  // (the tile is re-zeroed for the next row block)
+  }
+}
+
+// ==========================================================================================
+// tangent reverse (fp32): (dZ, dZdot) of the reverse-over-tangent pass (ops/reference.py
+// lstm_seq_tbwd) from the primal and tangent tapes of lstmf_fwd<TAPE> / lstmf_fwd<TAN>
+// ==========================================================================================
+// The BPTT's two-phase step with two adjoint streams: phase A runs dz_{t+1} U^T and dzdot_{t+1} U^T
+// (800 MFMAs per wave) from two dz tiles, phase B the second-order cell adjoints per (row, unit).
+// dZ / dZdot leave through the tiles' coalesced row-major stores during the next phase A.
+// Register budget: a cell carries 16 values here (c, cdot, two adjoint carries, the gate and zdot
+// quads, c_{t-1}, cdot_{t-1}, dH, dHd), so the kernel walks 16-ROW tiles (one accumulator half of a
+// 32-row tape block: 7 cells per lane) to stay inside the register file without spills.
+template <int ACT>
+__global__ void __launch_bounds__(256, 1)
+lstmf_tbwd_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, const float* __restrict__ tape,
+                  const float* __restrict__ ttape, const float* __restrict__ U, float* __restrict__ dZ,
+                  float* __restrict__ dZd, int B, int Tn) {
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  float* zt = fsm;                 // dz_{t+1}      [16][BZ_LR]
+  float* zdt = zt + 16 * BZ_LR;    // dzdot_{t+1}
+  float* ht = zdt + 16 * BZ_LR;    // dz_{t+1} U^T  [16][BH_LR]
+  float* hdt = ht + 16 * BH_LR;    // dzdot_{t+1} U^T
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane & 3, g = lane >> 4, j4 = (lane & 15) >> 2, c16 = lane & 15;
+  const int ub = FUW * w + j4;
+  const int nrb32 = (B + 31) / 32, nt16 = (B + 15) / 16;
+  float ut[2][FH];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int j = 16 * (2 * w + e) + c16;
+    const bool ok = j < FH;
+#pragma unroll
+    for (int k = 0; k < FH; ++k) {
+      const float v = U[(ok ? j : 0) * FG + g * FH + k];
+      ut[e][k] = ok ? v : 0.f;
+      asm volatile("" : "+a"(ut[e][k]));
+    }
+  }
+  const int hr = (4 * g + q) * BH_LR + ub, zw = (4 * g + q) * BZ_LR + ub;
+  for (int tb16 = blockIdx.x; tb16 < nt16; tb16 += gridDim.x) {
+    const int row0 = tb16 * 16, mh = tb16 & 1;  // tape block tb16 / 2, accumulator half mh
+    const int nr = min(16, B - row0);
+    const rsrc_t rdh = make_rsrc(dH ? dH + (size_t)row0 * Tn * FH : nullptr, dH ? nr * Tn * FH * 4 : 0);
+    const rsrc_t rdhd = make_rsrc(dHd ? dHd + (size_t)row0 * Tn * FH : nullptr, dHd ? nr * Tn * FH * 4 : 0);
+    const rsrc_t rt = ftape_rsrc(tape, tb16 >> 1, nrb32, Tn), rtt = ftape_rsrc(ttape, tb16 >> 1, nrb32, Tn);
+    const rsrc_t rz = make_rsrc(dZ + (size_t)row0 * Tn * FG, nr * Tn * FG * 4);
+    const rsrc_t rzd = make_rsrc(dZd + (size_t)row0 * Tn * FG, nr * Tn * FG * 4);
+    const int vp1 = ((4 * g + q) * Tn * FH + ub) * 4;
+    const int tl = ftape_lane(w, lane) + mh * FNT * FT_SLOT * 4, tcl = ftape_cell(w, lane) + mh * FNT * FT_SLOT * 4;
+    // per cell: carried c_t, cdot_t, c-bar, cdot-bar; step loads: gates, zdot (t), c_{t-1},
+    // cdot_{t-1}, dH, dHd (t)
+    float tc[FNT], tcd[FNT], acn[FNT], acdn[FNT];
+    f32x4 tg[FNT], tz[FNT];
+    float tcp[FNT], tcdp[FNT], tdh[FNT], tdhd[FNT];
+    auto load_step = [&](int n, int tt, bool on) {
+      const bool tok = on && !(w == 3 && n >= 4);
+      const int og = tl + tt * FT_STEP * 4 + ftape_slot(0, n), ocp = tcl + (tt - 1) * FT_STEP * 4 + ftape_slot(0, n);
+      tg[n] = ld4(rt, tok ? og : kOOB);
+      tz[n] = ld4(rtt, tok ? og : kOOB);
+      tcp[n] = ld1(rt, (tok && tt > 0) ? ocp : kOOB, 0);
+      tcdp[n] = ld1(rtt, (tok && tt > 0) ? ocp : kOOB, 0);
+      tdh[n] = ld1(rdh, tok ? vp1 + tt * FH * 4 + 16 * n : kOOB, 0);
+      tdhd[n] = ld1(rdhd, tok ? vp1 + tt * FH * 4 + 16 * n : kOOB, 0);
+    };
+#pragma unroll
+    for (int n = 0; n < FNT; ++n) {
+      const bool tok = !(w == 3 && n >= 4);
+      const int oc = tcl + (Tn - 1) * FT_STEP * 4 + ftape_slot(0, n);
+      acn[n] = 0.f;
+      acdn[n] = 0.f;
+      tc[n] = ld1(rt, tok ? oc : kOOB, 0);
+      tcd[n] = ld1(rtt, tok ? oc : kOOB, 0);
+      load_step(n, Tn - 1, true);
+    }
+    for (int i = tid; i < 2 * 16 * BZ_LR; i += 256) zt[i] = 0.f;  // dz_T = dzdot_T = 0
+    __syncthreads();
+    for (int t = Tn - 1; t >= 0; --t) {
+      // ---- phase A ----
+      if (t < Tn - 1) {
+        bwdf_store16(zt, rz, Tn, t + 1, nr, tid);
+        bwdf_store16(zdt, rzd, Tn, t + 1, nr, tid);
+      }
+      {
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) acc[a][0] = acc[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* ar = zt + c16 * BZ_LR + g * BZ_KQ;
+        const float* adr = zdt + c16 * BZ_LR + g * BZ_KQ;
+#pragma unroll
+        for (int jj = 0; jj < FH / 4; ++jj) {
+          const f32x4 a4 = *reinterpret_cast<const f32x4*>(ar + 4 * jj);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(adr + 4 * jj);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            acc[0][0] = mma4(a4[s], ut[0][4 * jj + s], acc[0][0]);
+            acc[0][1] = mma4(a4[s], ut[1][4 * jj + s], acc[0][1]);
+            acc[1][0] = mma4(d4[s], ut[0][4 * jj + s], acc[1][0]);
+            acc[1][1] = mma4(d4[s], ut[1][4 * jj + s], acc[1][1]);
+          }
+          if ((jj & 1) == 1) __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int col = 16 * (2 * w + e) + c16;
+          if (2 * w + e < 7) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              ht[(4 * g + i) * BH_LR + col] = acc[0][e][i];
+              hdt[(4 * g + i) * BH_LR + col] = acc[1][e][i];
+            }
+          }
+        }
+      }
+      lds_barrier();
+      // ---- phase B ----
+#pragma unroll
+      for (int n = 0; n < FNT; ++n) {
+        const bool tok = !(w == 3 && n >= 4);
+        const float i_ = tg[n][0], f_ = tg[n][1], g_ = tg[n][2], o_ = tg[n][3];
+        const float zdi = tz[n][0], zdf = tz[n][1], zdg = tz[n][2], zdo = tz[n][3];
+        const float c = tc[n], cd = tcd[n], cp = tcp[n], cdp = tcdp[n];
+        const float si = i_ * (1.f - i_), sf = f_ * (1.f - f_), so = o_ * (1.f - o_), sg = act_dy(ACT, g_);
+        const float idot = si * zdi, fdot = sf * zdf, gdot = sg * zdg, odot = so * zdo;
+        const float ca = act_f(ACT, c), d1 = act_dy(ACT, ca), d2 = act_d2y(ACT, ca);
+        const int hi = hr + 4 * n;
+        const float a_h = tdh[n] + ht[hi], a_hd = tdhd[n] + hdt[hi];
+        const float a_od = a_hd * ca;
+        const float a_o = a_h * ca + a_hd * d1 * cd;
+        const float a_cd = acdn[n] + a_hd * o_ * d1;
+        const float a_c = acn[n] + a_h * o_ * d1 + a_hd * (odot * d1 + o_ * d2 * cd);
+        const float a_fd = a_cd * cp, a_id = a_cd * g_, a_gd = a_cd * i_;
+        const float a_f = a_c * cp + a_cd * cdp;
+        const float a_i = a_c * g_ + a_cd * gdot;
+        const float a_g = a_c * i_ + a_cd * idot;
+        acn[n] = tok ? a_c * f_ + a_cd * fdot : 0.f;
+        acdn[n] = tok ? a_cd * f_ : 0.f;
+        const float s2i = si * (1.f - 2.f * i_), s2f = sf * (1.f - 2.f * f_), s2o = so * (1.f - 2.f * o_);
+        const float s2g = act_d2y(ACT, g_);
+        float zd4[4], z4[4];
+        zd4[0] = a_id * si; zd4[1] = a_fd * sf; zd4[2] = a_gd * sg; zd4[3] = a_od * so;
+        z4[0] = a_i * si + a_id * s2i * zdi;
+        z4[1] = a_f * sf + a_fd * s2f * zdf;
+        z4[2] = a_g * sg + a_gd * s2g * zdg;
+        z4[3] = a_o * so + a_od * s2o * zdo;
+        if (tok) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            zt[zw + k * BZ_KQ + 4 * n] = z4[k];
+            zdt[zw + k * BZ_KQ + 4 * n] = zd4[k];
+          }
+        }
+        tc[n] = cp;
+        tcd[n] = cdp;
+        load_step(n, t > 0 ? t - 1 : 0, t > 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      lds_barrier();
+    }
+    bwdf_store16(zt, rz, Tn, 0, nr, tid);
+    bwdf_store16(zdt, rzd, Tn, 0, nr, tid);
+    __syncthreads();
   }
 }
 
@@ -528,30 +883,30 @@ void allow_lds(const void* k) {
     HFREP_CHECK_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)F_LDS_MAX));
 }
 template <int ACT, int KX, bool TAPE, bool TAN>
-void fwdf_launch(const float* x, const float* W, const float* b, const float* U, const float* pg, const float* pc, float* hs,
-                 float* go, float* co, int B, int Tn, hipStream_t s) {
+void fwdf_launch(const float* x, const float* W, const float* b, const float* U, const float* pt, float* hs, float* tp,
+                 int B, int Tn, hipStream_t s) {
   auto k = lstmf_fwd_kernel<ACT, KX, TAPE, TAN>;
   allow_lds(reinterpret_cast<const void*>(k));
   const int nrb = (B + 31) / 32, cus = device_cu_count();
-  hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(256), fwdf_smem<KX>(), s, x, W, b, U, pg, pc, hs, go, co, B, Tn);
+  hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(256), fwdf_smem<KX>(), s, x, W, b, U, pt, hs, tp, B, Tn);
 }
 template <int KX, bool TAPE, bool TAN>
-void fwdf_act(int act, const float* x, const float* W, const float* b, const float* U, const float* pg, const float* pc,
-              float* hs, float* go, float* co, int B, int Tn, hipStream_t s) {
+void fwdf_act(int act, const float* x, const float* W, const float* b, const float* U, const float* pt, float* hs,
+              float* tp, int B, int Tn, hipStream_t s) {
   switch (act) {
-    case ACT_LINEAR: fwdf_launch<ACT_LINEAR, KX, TAPE, TAN>(x, W, b, U, pg, pc, hs, go, co, B, Tn, s); break;
-    case ACT_SIGMOID: fwdf_launch<ACT_SIGMOID, KX, TAPE, TAN>(x, W, b, U, pg, pc, hs, go, co, B, Tn, s); break;
-    default: fwdf_launch<ACT_TANH, KX, TAPE, TAN>(x, W, b, U, pg, pc, hs, go, co, B, Tn, s); break;
+    case ACT_LINEAR: fwdf_launch<ACT_LINEAR, KX, TAPE, TAN>(x, W, b, U, pt, hs, tp, B, Tn, s); break;
+    case ACT_SIGMOID: fwdf_launch<ACT_SIGMOID, KX, TAPE, TAN>(x, W, b, U, pt, hs, tp, B, Tn, s); break;
+    default: fwdf_launch<ACT_TANH, KX, TAPE, TAN>(x, W, b, U, pt, hs, tp, B, Tn, s); break;
   }
 }
 template <bool TAPE, bool TAN>
-bool fwdf_k(int K, int act, const float* x, const float* W, const float* b, const float* U, const float* pg,
-            const float* pc, float* hs, float* go, float* co, int B, int Tn, hipStream_t s) {
+bool fwdf_k(int K, int act, const float* x, const float* W, const float* b, const float* U, const float* pt, float* hs,
+            float* tp, int B, int Tn, hipStream_t s) {
   switch (K) {
-    case 32: fwdf_act<32, TAPE, TAN>(act, x, W, b, U, pg, pc, hs, go, co, B, Tn, s); return true;
-    case 35: fwdf_act<35, TAPE, TAN>(act, x, W, b, U, pg, pc, hs, go, co, B, Tn, s); return true;
-    case 36: fwdf_act<36, TAPE, TAN>(act, x, W, b, U, pg, pc, hs, go, co, B, Tn, s); return true;
-    case 100: fwdf_act<100, TAPE, TAN>(act, x, W, b, U, pg, pc, hs, go, co, B, Tn, s); return true;
+    case 32: fwdf_act<32, TAPE, TAN>(act, x, W, b, U, pt, hs, tp, B, Tn, s); return true;
+    case 35: fwdf_act<35, TAPE, TAN>(act, x, W, b, U, pt, hs, tp, B, Tn, s); return true;
+    case 36: fwdf_act<36, TAPE, TAN>(act, x, W, b, U, pt, hs, tp, B, Tn, s); return true;
+    case 100: fwdf_act<100, TAPE, TAN>(act, x, W, b, U, pt, hs, tp, B, Tn, s); return true;
     default: return false;
   }
 }
@@ -561,18 +916,59 @@ bool lstmf_supported(int H, int K, int act) {
   return H == FH && (K == 32 || K == 35 || K == 36 || K == 100) && (act == ACT_LINEAR || act == ACT_SIGMOID || act == ACT_TANH);
 }
 
-bool launch_lstmf_fwd(const float* x, const float* W, const float* b, const float* U, float* hs, float* gates, float* cs,
-                      int B, int Tn, int K, int H, int act, hipStream_t s) {
+bool launch_lstmf_fwd(const float* x, const float* W, const float* b, const float* U, float* hs, float* tape, int B,
+                      int Tn, int K, int H, int act, hipStream_t s) {
   if (!lstmf_supported(H, K, act) || B <= 0 || Tn <= 0) return false;
-  if (gates) return fwdf_k<true, false>(K, act, x, W, b, U, nullptr, nullptr, hs, gates, cs, B, Tn, s);
-  return fwdf_k<false, false>(K, act, x, W, b, U, nullptr, nullptr, hs, nullptr, nullptr, B, Tn, s);
+  if (tape) return fwdf_k<true, false>(K, act, x, W, b, U, nullptr, hs, tape, B, Tn, s);
+  return fwdf_k<false, false>(K, act, x, W, b, U, nullptr, hs, nullptr, B, Tn, s);
 }
 
-bool launch_lstmf_tfwd(const float* xd, const float* W, const float* U, const float* gates, const float* cs, float* hds,
-                       float* zds, float* cds, int B, int Tn, int K, int H, int act, hipStream_t s) {
+bool launch_lstmf_tfwd(const float* xd, const float* W, const float* U, const float* tape, float* hds, float* ttape,
+                       int B, int Tn, int K, int H, int act, hipStream_t s) {
   if (!lstmf_supported(H, K, act) || B <= 0 || Tn <= 0) return false;
-  return fwdf_k<true, true>(K, act, xd, W, nullptr, U, gates, cs, hds, zds, cds, B, Tn, s);
+  return fwdf_k<true, true>(K, act, xd, W, nullptr, U, tape, hds, ttape, B, Tn, s);
 }
+
+template <int ACT>
+void bwdf_launch(const float* dH, const float* tape, const float* U, float* dZ, int B, int Tn, hipStream_t s) {
+  auto k = lstmf_bwd_kernel<ACT>;
+  allow_lds(reinterpret_cast<const void*>(k));
+  const int nrb = (B + 31) / 32, cus = device_cu_count();
+  const size_t sm = (size_t)(32 * BZ_LR + 32 * BH_LR) * 4;
+  hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(256), sm, s, dH, tape, U, dZ, B, Tn);
+}
+bool launch_lstmf_bwd(const float* dH, const float* tape, const float* U, float* dZ, int B, int Tn, int H, int act,
+                      hipStream_t s) {
+  if (H != FH || B <= 0 || Tn <= 0) return false;
+  switch (act) {
+    case ACT_LINEAR: bwdf_launch<ACT_LINEAR>(dH, tape, U, dZ, B, Tn, s); return true;
+    case ACT_SIGMOID: bwdf_launch<ACT_SIGMOID>(dH, tape, U, dZ, B, Tn, s); return true;
+    case ACT_TANH: bwdf_launch<ACT_TANH>(dH, tape, U, dZ, B, Tn, s); return true;
+    default: return false;
+  }
+}
+
+template <int ACT>
+void tbwdf_launch(const float* dH, const float* dHd, const float* tape, const float* ttape, const float* U, float* dZ,
+                  float* dZd, int B, int Tn, hipStream_t s) {
+  auto k = lstmf_tbwd_kernel<ACT>;
+  allow_lds(reinterpret_cast<const void*>(k));
+  const int cus = device_cu_count();
+  const size_t sm = (size_t)(2 * 16 * BZ_LR + 2 * 16 * BH_LR) * 4;
+  const int nt16 = (B + 15) / 16;
+  hipLaunchKernelGGL(k, dim3(nt16 < cus ? nt16 : cus), dim3(256), sm, s, dH, dHd, tape, ttape, U, dZ, dZd, B, Tn);
+}
+bool launch_lstmf_tbwd(const float* dH, const float* dHd, const float* tape, const float* ttape, const float* U, float* dZ,
+                       float* dZd, int B, int Tn, int H, int act, hipStream_t s) {
+  if (H != FH || B <= 0 || Tn <= 0) return false;
+  switch (act) {
+    case ACT_LINEAR: tbwdf_launch<ACT_LINEAR>(dH, dHd, tape, ttape, U, dZ, dZd, B, Tn, s); return true;
+    case ACT_SIGMOID: tbwdf_launch<ACT_SIGMOID>(dH, dHd, tape, ttape, U, dZ, dZd, B, Tn, s); return true;
+    case ACT_TANH: tbwdf_launch<ACT_TANH>(dH, dHd, tape, ttape, U, dZ, dZd, B, Tn, s); return true;
+    default: return false;
+  }
+}
+size_t lstmf_tape_elems(int B, int Tn) { return (size_t)((B + 31) / 32) * Tn * FT_STEP; }
 
 static int wgradf_grid(int M) {
   const int chunks = (M + WF_R - 1) / WF_R, cus = device_cu_count();

@@ -33,8 +33,23 @@ def _2d(x: torch.Tensor) -> torch.Tensor:
 # ---------------------------------------------------------------------------------------
 # dense / GEMM family
 # ---------------------------------------------------------------------------------------
+# fp32 plain GEMMs with many rows go to the vendor library (hipBLASLt through torch.mm; exact fp32
+# on gfx950, which has no xf32): at M = 786k it ran the step's shapes 1.4-2.6x faster than the
+# generic tile kernel of csrc/gemm.hip (profiles/r02_fp32/gemm_fp32_native_vs_hipblaslt.jsonl).
+# Everything with an epilogue, bf16, or small M stays on the native kernels.
+_BLAS_MIN_ROWS = int(os.environ.get("HFREP_FP32_BLAS_MIN_ROWS", "65536"))
+
+
+def _blas_fp32(a: torch.Tensor, rows: int) -> bool:
+    return a.dtype == torch.float32 and _BLAS_MIN_ROWS > 0 and rows >= _BLAS_MIN_ROWS
+
+
 def linear(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: int) -> torch.Tensor:
     """act(x @ W + b) on the last axis. Output dtype = x dtype."""
+    if _nat(x) and act == 0 and W.shape[1] > 4 and _blas_fp32(x, x.numel() // x.shape[-1]):
+        x2 = _2d(x.contiguous())
+        y = torch.addmm(b, x2, W) if b is not None else torch.mm(x2, W)
+        return y.reshape(*x.shape[:-1], W.shape[1])
     if _nat(x):
         y = _ops().linear(_2d(x.contiguous()), W, b, int(act))
         return y.reshape(*x.shape[:-1], W.shape[1])
@@ -46,6 +61,8 @@ def linear(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: int) -
 
 def linear_dgrad(dz: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     """dz @ W^T (input gradient)."""
+    if _nat(dz) and W.shape[1] > 4 and _blas_fp32(dz, dz.numel() // dz.shape[-1]):
+        return torch.mm(_2d(dz.contiguous()), W.t()).reshape(*dz.shape[:-1], W.shape[0])
     if _nat(dz):
         return _ops().linear_dgrad(_2d(dz.contiguous()), W).reshape(*dz.shape[:-1], W.shape[0])
     return torch.matmul(dz, W.t().to(dz.dtype))
@@ -237,14 +254,26 @@ def _use_lstmf(x: torch.Tensor, U: torch.Tensor, act: int) -> bool:
             and bool(_ops().lstmf_supported(int(U.shape[0]), int(x.shape[-1]), int(act))))
 
 
+class FTape:
+    """fp32 tape of the fused fp32 kernels (csrc/lstm_f32.hip): one lane-native blocked tensor
+    (per 32-row block and step: 4 waves x 14 slots x 64 lanes x {4 gate values, 1 cell value}), plus
+    the (B, T) it was written for.  Primal tapes hold gate activations and c_t, tangent tapes the
+    gate pre-activation tangents and cdot_t."""
+
+    __slots__ = ("t", "B", "T")
+
+    def __init__(self, t: torch.Tensor, B: int, T: int):
+        self.t, self.B, self.T = t, int(B), int(T)
+
+
 def lstm_layer_fwd(x, W, b, U, act: int, save: bool):
     """h_seq and a tape for act(x W + b ...) recurrences; x (B, T, K)."""
     if _use_lstm2(x, U):
         hs, tape = _ops().lstm2_fwd(x.contiguous(), W, b, U, int(act), bool(save))
         return hs, (tape if save else None)
     if _use_lstmf(x, U, act):
-        hs, gates, cs = _ops().lstmf_fwd(x.contiguous(), W, b, U, int(act), bool(save))
-        return hs, ((gates, cs) if save else None)
+        hs, tape = _ops().lstmf_fwd(x.contiguous(), W, b, U, int(act), bool(save))
+        return hs, (FTape(tape, x.shape[0], x.shape[1]) if save else None)
     zx = linear(x, W, b, 0)
     hs, gates, cs = lstm_seq_fwd(zx, U, act, save)
     return hs, ((gates, cs) if save else None)
@@ -282,6 +311,10 @@ def lstm_layer_bwd(dH, tape, U, act: int, W=None, need_dz: bool = True):
     returned as ``(dZ, dX)`` (the v2 kernel produces it in the same launch, csrc/lstm2.hip).
     ``need_dz=False`` (only dX wanted, e.g. the gradient penalty's dD/dx) lets the v2 kernel skip
     writing dZ to HBM; the returned dZ is then None."""
+    if isinstance(tape, FTape):
+        dH = _mat(dH)
+        dZ = _ops().lstmf_bwd(None if dH is None else dH.contiguous(), tape.t, U, int(act), tape.B, tape.T)
+        return dZ if W is None else (dZ, linear_dgrad(dZ, W))
     if isinstance(tape, torch.Tensor):
         nd = bool(need_dz or W is None)
         if isinstance(dH, OuterAdjoint):  # head adjoint generated in-kernel
@@ -298,13 +331,13 @@ def lstm_layer_bwd(dH, tape, U, act: int, W=None, need_dz: bool = True):
 
 
 def lstm_layer_tfwd(xd, W, tape, U, act: int):
+    if isinstance(tape, FTape):
+        hds, ttape = _ops().lstmf_tfwd(xd.contiguous(), W, U, tape.t, int(act))
+        return hds, FTape(ttape, tape.B, tape.T)
     if isinstance(tape, torch.Tensor):
         hds, ttape = _ops().lstm2_tfwd(xd.contiguous(), W, U, tape, int(act))
         return hds, ttape
     gates, cs = tape
-    if _use_lstmf(xd, U, act):
-        hds, zds, cds = _ops().lstmf_tfwd(xd.contiguous(), W, U, gates, cs, int(act))
-        return hds, (zds, cds)
     dzx = linear(xd, W, None, 0)
     hds, zds, cds = lstm_seq_tfwd(dzx, gates, cs, U, act)
     return hds, (zds, cds)
@@ -333,6 +366,11 @@ def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None, impl: int = 
 
 def lstm_layer_tbwd(dH, dHd, tape, ttape, U, act: int, W=None):
     """(dZ, dZd) of the reverse-over-tangent pass; with ``W`` also (dX, dXd) = (dZ W^T, dZd W^T)."""
+    if isinstance(tape, FTape):
+        dH, dHd = _mat(dH), _mat(dHd)
+        dZ, dZd = _ops().lstmf_tbwd(None if dH is None else dH.contiguous(), None if dHd is None else dHd.contiguous(),
+                                    tape.t, ttape.t, U, int(act), tape.B, tape.T)
+        return (dZ, dZd) if W is None else (dZ, dZd, linear_dgrad(dZ, W), linear_dgrad(dZd, W))
     if isinstance(tape, torch.Tensor):
         heads = [a for a in (dH, dHd) if isinstance(a, OuterAdjoint)]
         # the in-kernel generated head adjoint is used without the fused input gradient only: the

@@ -37,7 +37,8 @@ def init_distributed(backend: str | None = None, timeout_s: float = 600.0):
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29511")
+    # torchrun always sets MASTER_PORT; a hand-launched job may choose it with HFREP_MASTER_PORT
+    os.environ.setdefault("MASTER_PORT", os.environ.get("HFREP_MASTER_PORT", "29511"))
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
         # surface RCCL errors as Python exceptions instead of hanging a collective forever

@@ -6,8 +6,9 @@ prints every iteration and saves the generator once at the very end - a crash lo
 
 * structured JSONL logging every ``log_every`` iterations through deferred (non-blocking)
   device->host snapshots (:mod:`hfrep.utils.logger`);
-* a NaN/Inf guard: a device-side finiteness flag of the losses, MIN-all-reduced across ranks so
-  every rank stops at the same iteration (no rank is left waiting in a collective);
+* a NaN/Inf guard: a device-side finiteness flag of the losses, all-reduced across ranks together
+  with the logged losses (averaged over ranks), so every rank stops at the same iteration (no rank
+  is left waiting in a collective) and every rank logs the global-batch losses;
 * periodic atomic checkpoints of the full training state (G, C, optimizer slots, the shared
   iteration counter, the RNG counter) by rank 0, keeping the newest ``keep`` files, and
   ``resume="auto"`` to continue from the newest one bitwise-identically;
@@ -81,8 +82,13 @@ class GraphedStep:
             raise RuntimeError("graph capture needs a GPU trainer")
         if not trainer.rng.native:
             raise RuntimeError("graph capture needs the native (device-counter) RNG")
-        if trainer.grad_sync is not None:
-            raise RuntimeError("graph capture is single-process (collectives stay eager)")
+        if trainer.grad_sync is not None and trainer.world > 1:
+            # RCCL collectives are graph-capturable (ProcessGroupNCCL records them on the captured
+            # stream); gloo / CPU collectives are not.  Opt-in (HFREP_GRAPH_DP=1) until a multi-GPU
+            # run validates replayed all-reduces against the eager step.
+            if trainer.grad_sync.backend != "nccl" or os.environ.get("HFREP_GRAPH_DP", "0") != "1":
+                raise RuntimeError("graph capture under data parallelism needs RCCL and HFREP_GRAPH_DP=1 "
+                                   "(collectives stay eager otherwise)")
         self.t, self.warmup, self.calls = trainer, warmup, 0
         self.graph = None
 
@@ -106,14 +112,50 @@ class GraphedStep:
         self.t.iteration += 1
 
 
-def _finite_flag(trainer):
-    ok = torch.isfinite(trainer._d_acc).all() & torch.isfinite(trainer._g_acc).all()
-    ok = ok.to(torch.float32).reshape(1)
-    if trainer.grad_sync is not None:
+def _log_tensors(trainer, nan_guard: bool) -> dict:
+    """The logged loss scalars, averaged over ranks, and the all-ranks finiteness flag.
+
+    One packed SUM all-reduce per log interval: [d_loss, d_real, d_fake, gp, g_loss..., finite]; a
+    rank's non-finite loss makes the summed flag < world on every rank, so all ranks stop at the
+    same iteration (no rank left waiting in a collective)."""
+    d, g = trainer._d_acc.reshape(-1), trainer._g_acc.reshape(-1)
+    if trainer.grad_sync is None or trainer.world <= 1:
+        out = {"d": d, "g": g}
+        if nan_guard:
+            out["ok"] = (torch.isfinite(d).all() & torch.isfinite(g).all()).to(torch.float32).reshape(1)
+        return out
+    import torch.distributed as dist
+
+    ok = (torch.isfinite(d).all() & torch.isfinite(g).all()).to(d.dtype).reshape(1)
+    # a non-finite rank contributes zeros to the mean (its flag reports it)
+    pack = torch.cat([torch.nan_to_num(d, nan=0.0, posinf=0.0, neginf=0.0),
+                      torch.nan_to_num(g.to(d.dtype), nan=0.0, posinf=0.0, neginf=0.0), ok])
+    dist.all_reduce(pack, op=dist.ReduceOp.SUM, group=trainer.grad_sync.group)
+    nd, ng, w = d.numel(), g.numel(), float(trainer.world)
+    out = {"d": pack[:nd] / w, "g": pack[nd:nd + ng] / w}
+    if nan_guard:
+        out["ok"] = (pack[nd + ng:] >= w - 0.5).to(torch.float32)
+    return out
+
+
+def resolve_resume(opts: RunOptions, trainer) -> str | None:
+    """Checkpoint path to resume from.  Under data parallelism rank 0 resolves it and broadcasts
+    the path, so every rank loads the same iteration even when ``ckpt_dir`` is rank-local or
+    rank 0 is rotating files."""
+    if not opts.resume:
+        return None
+    if opts.resume == "auto" and not opts.ckpt_dir:
+        raise ValueError("resume='auto' needs ckpt_dir")
+    path = None
+    if trainer.rank == 0 or trainer.grad_sync is None:
+        path = latest_checkpoint(opts.ckpt_dir) if opts.resume == "auto" else opts.resume
+    if trainer.grad_sync is not None and trainer.world > 1:
         import torch.distributed as dist
 
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=trainer.grad_sync.group)
-    return ok
+        box = [path]
+        dist.broadcast_object_list(box, src=0, group=trainer.grad_sync.group)
+        path = box[0]
+    return path
 
 
 def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[dict]:
@@ -138,11 +180,10 @@ def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[di
         records.append(rec)
         logger.log(rec)
 
-    if opts.resume:
-        path = latest_checkpoint(opts.ckpt_dir) if opts.resume == "auto" else opts.resume
-        if path:
-            load_training_state(path, trainer)
-            logger.log({"event": "resumed", "path": path, "iteration": trainer.iteration})
+    path = resolve_resume(opts, trainer)
+    if path:
+        load_training_state(path, trainer)
+        logger.log({"event": "resumed", "path": path, "iteration": trainer.iteration})
     step = GraphedStep(trainer) if opts.graph else trainer.train_step
     snap = AsyncScalars()
     wpi = trainer.windows_per_iteration() * trainer.world
@@ -158,12 +199,14 @@ def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[di
                 now = time.time()
                 meta = {"iteration": it, "windows_per_s": wpi * (it - it_last) / max(now - t_last, 1e-9)}
                 t_last, it_last = now, it
-                tensors = {"d": trainer._d_acc, "g": trainer._g_acc}
-                if opts.nan_guard:
-                    tensors["ok"] = _finite_flag(trainer)
-                emit(snap.snapshot(meta, **tensors))
-            if opts.ckpt_dir and opts.ckpt_every and it % opts.ckpt_every == 0 and trainer.rank == 0:
-                _checkpoint(trainer, opts)
+                emit(snap.snapshot(meta, **_log_tensors(trainer, opts.nan_guard)))
+            if opts.ckpt_dir and opts.ckpt_every and it % opts.ckpt_every == 0:
+                if trainer.rank == 0:
+                    _checkpoint(trainer, opts)
+                if trainer.grad_sync is not None and trainer.world > 1:
+                    import torch.distributed as dist
+
+                    dist.barrier(group=trainer.grad_sync.group)  # the file exists before any rank goes on
         emit(snap.collect())
     finally:
         if own_logger:

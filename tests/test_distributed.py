@@ -62,7 +62,7 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_gloo_matches_single_process(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -100,3 +100,63 @@ def test_dp_gloo_matches_single_process(world):
         np.testing.assert_array_equal(res[0]["critic"], res[r]["critic"])
         # after DP training every rank holds identical parameters
         np.testing.assert_array_equal(res[0]["params"], res[r]["params"])
+
+
+def _runner_worker(rank, world, port, ckdir, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        import hfrep  # noqa: F401
+        from hfrep.parallel.dp import init_distributed
+        from hfrep.train.gan_trainer import GANConfig, GANTrainer
+        from hfrep.train.runner import RunOptions, run
+
+        r, _, w, pg = init_distributed(backend="gloo")
+        ds = np.random.RandomState(0).rand(30, 6, 4)
+
+        def trainer():
+            cfg = GANConfig(arch="lstm", loss="wgan_gp", window=6, features=4, batch_size=4, hidden=8, dtype="float64")
+            return GANTrainer(cfg, ds, process_group=pg, rank=r, world=w, param_dtype=torch.float64)
+
+        a = trainer()
+        recs = run(a, RunOptions(epochs=4, log_every=1, echo=False, ckpt_dir=ckdir, ckpt_every=2))
+        # a second job resumes from the newest checkpoint; rank 0 resolves the path for everyone
+        b = trainer()
+        recs_b = run(b, RunOptions(epochs=6, log_every=1, echo=False, ckpt_dir=ckdir, ckpt_every=2, resume="auto"))
+        losses = [[x["d_loss"], x["g_loss"], x["gp"]] for x in recs]
+        local = [float(v) for v in a._d_acc.reshape(-1).tolist()]
+        q.put((r, {"losses": losses, "resumed_at": [x["iteration"] for x in recs_b][0], "local_last": local,
+                   "params": torch.cat([b.generator.flat.detach(), b.critic.flat.detach()]).numpy()}))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+
+
+def test_dp_runner_averages_logged_losses_and_resumes_consistently(tmp_path):
+    """C5: logged losses are the all-rank average (identical on every rank, != a rank's local
+    value); resume='auto' resolves one checkpoint on rank 0 for all ranks, after a barrier that
+    follows every checkpoint write."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_runner_worker, args=(r, world, port, str(tmp_path / "ck"), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, v = q.get(timeout=300)
+        assert not isinstance(v, str), v
+        res[r] = v
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0]["losses"] == res[1]["losses"]
+    last = res[0]["losses"][-1][0]
+    mean_local = 0.5 * (res[0]["local_last"][0] + res[1]["local_last"][0])
+    assert abs(last - mean_local) < 1e-6 * max(1.0, abs(mean_local))  # (logged through fp32 snapshots)
+    assert res[0]["local_last"][0] != res[1]["local_last"][0]
+    assert res[0]["resumed_at"] == res[1]["resumed_at"] == 5
+    np.testing.assert_array_equal(res[0]["params"], res[1]["params"])

@@ -587,9 +587,9 @@ def test_gan_loss_native(cuda, dt, kind, n, split):
 @pytest.mark.parametrize("act", [2, 1, 0])
 @pytest.mark.parametrize("B,T,K", [(70, 24, 32), (33, 12, 100), (64, 7, 35), (40, 5, 36)])
 def test_lstmf_fused_layer(cuda, act, B, T, K):
-    """fp32 fused-projection kernels (csrc/lstm_f32.hip: exact-f32 16x16x4 MFMA, gate-interleaved
-    tiles + quad transpose) vs the fp64 reference: forward, tape, tangent forward, and the v1
-    reverse kernels consuming their row-major tapes."""
+    """fp32 fused kernels (csrc/lstm_f32.hip: exact-f32 16x16x4 MFMA, gate-interleaved tiles + quad
+    transpose, lane-native blocked tapes) vs the fp64 reference: forward, BPTT (+ input gradient),
+    tangent forward and tangent reverse, each bitwise reproducible run to run."""
     from hfrep.ops import functional as Fn
 
     H = 100
@@ -599,32 +599,50 @@ def test_lstmf_fused_layer(cuda, act, B, T, K):
     b = torch.randn(4 * H, generator=g) * 0.1
     U = torch.randn(H, 4 * H, generator=g) * (1.0 / H ** 0.5)
     assert _ops().lstmf_supported(H, K, act)
-    hs, tape = Fn.lstm_layer_fwd(x.to(cuda), W.to(cuda), b.to(cuda), U.to(cuda), act, True)
-    gates, cs = tape
+    dev = lambda *ts: [t_.to(cuda) for t_ in ts]  # noqa: E731
+    xg, Wg, bg, Ug = dev(x, W, b, U)
+    hs, tape = Fn.lstm_layer_fwd(xg, Wg, bg, Ug, act, True)
+    assert isinstance(tape, Fn.FTape)
     zx = x.double() @ W.double() + b.double()
     rh, rg, rc = R.lstm_seq_fwd(zx, U.double(), act)
     f32 = torch.float32
     _close(hs, rh, f32)
-    _close(gates, rg, f32)
-    _close(cs, rc, f32)
-    hs0, none = Fn.lstm_layer_fwd(x.to(cuda), W.to(cuda), b.to(cuda), U.to(cuda), act, False)
+    hs0, none = Fn.lstm_layer_fwd(xg, Wg, bg, Ug, act, False)
     assert none is None and torch.equal(hs0, hs)
+    # BPTT (+ dX through the input-gradient GEMM)
+    dH = torch.randn(B, T, H, generator=g)
+    dZ, dX = Fn.lstm_layer_bwd(dH.to(cuda), tape, Ug, act, W=Wg)
+    rdz = R.lstm_seq_bwd(dH.double(), rg, rc, U.double(), act)
+    _close(dZ, rdz, f32)
+    _close(dX, rdz @ W.double().t(), f32, scale=(rdz.abs() @ W.double().abs().t()).max().item())
+    # tangent forward + tangent reverse (with and without the primal adjoint)
     xd = torch.randn(B, T, K, generator=g) * 0.3
-    hds, (zds, cds) = Fn.lstm_layer_tfwd(xd.to(cuda), W.to(cuda), tape, U.to(cuda), act)
-    th, tz, tc = R.lstm_seq_tfwd(xd.double() @ W.double(), gates.double().cpu(), cs.double().cpu(), U.double(), act)
+    hds, ttape = Fn.lstm_layer_tfwd(xd.to(cuda), Wg, tape, Ug, act)
+    th, tz, tc = R.lstm_seq_tfwd(xd.double() @ W.double(), rg, rc, U.double(), act)
     _close(hds, th, f32)
-    _close(zds, tz, f32)
-    _close(cds, tc, f32)
-    # bitwise run-to-run reproducibility of both kernels
-    hs2, (g2, c2) = Fn.lstm_layer_fwd(x.to(cuda), W.to(cuda), b.to(cuda), U.to(cuda), act, True)
-    hds2, (z2, cd2) = Fn.lstm_layer_tfwd(xd.to(cuda), W.to(cuda), tape, U.to(cuda), act)
-    for a_, b_ in ((hs, hs2), (gates, g2), (cs, c2), (hds, hds2), (zds, z2), (cds, cd2)):
-        assert torch.equal(a_, b_)
+    dHd = torch.randn(B, T, H, generator=g)
+    for with_dh in (True, False):
+        dZ2, dZd2, dX2, dXd2 = Fn.lstm_layer_tbwd(dH.to(cuda) if with_dh else None, dHd.to(cuda), tape, ttape, Ug, act,
+                                                  W=Wg)
+        rz, rzd = R.lstm_seq_tbwd(dH.double() if with_dh else torch.zeros(B, T, H, dtype=torch.float64),
+                                  dHd.double(), rg, rc, tz, tc, U.double(), act)
+        _close(dZ2, rz, f32)
+        _close(dZd2, rzd, f32)
+        Wd = W.double()
+        _close(dXd2, rzd @ Wd.t(), f32, scale=(rzd.abs() @ Wd.abs().t()).max().item())
+    # bitwise run-to-run reproducibility
+    # (the tapes' padding slots are never written, so the tapes are compared through their readers)
+    hs2, tape2 = Fn.lstm_layer_fwd(xg, Wg, bg, Ug, act, True)
+    hds2, ttape2 = Fn.lstm_layer_tfwd(xd.to(cuda), Wg, tape2, Ug, act)
+    assert torch.equal(hs, hs2) and torch.equal(hds, hds2)
+    assert torch.equal(dZ, Fn.lstm_layer_bwd(dH.to(cuda), tape2, Ug, act))
+    dZ3, dZd3 = Fn.lstm_layer_tbwd(None, dHd.to(cuda), tape2, ttape2, Ug, act)
+    assert torch.equal(dZ3, dZ2) and torch.equal(dZd3, dZd2)
 
 
 def test_lstmf_persistent_multi_pass(cuda):
     """More row tiles than CUs (every persistent workgroup walks several tiles) and a partial last
-    tile: B = 256 * 32 + 45 rows."""
+    tile: B = 256 * 32 + 45 rows (the 16-row tangent reverse walks twice as many)."""
     from hfrep.ops import functional as Fn
 
     H, K, T, B = 100, 32, 6, 256 * 32 + 45
@@ -633,10 +651,21 @@ def test_lstmf_persistent_multi_pass(cuda):
     W = torch.randn(K, 4 * H, generator=g) * (1.0 / K ** 0.5)
     b = torch.randn(4 * H, generator=g) * 0.1
     U = torch.randn(H, 4 * H, generator=g) * (1.0 / H ** 0.5)
-    hs, (gates, cs) = Fn.lstm_layer_fwd(x.to(cuda), W.to(cuda), b.to(cuda), U.to(cuda), 2, True)
+    hs, tape = Fn.lstm_layer_fwd(x.to(cuda), W.to(cuda), b.to(cuda), U.to(cuda), 2, True)
     rh, rg, rc = R.lstm_seq_fwd(x.double() @ W.double() + b.double(), U.double(), 2)
     _close(hs, rh, torch.float32)
-    _close(cs, rc, torch.float32)
+    dH = torch.randn(B, T, H, generator=g) * 0.3
+    dZ = Fn.lstm_layer_bwd(dH.to(cuda), tape, U.to(cuda), 2)
+    _close(dZ, R.lstm_seq_bwd(dH.double(), rg, rc, U.double(), 2), torch.float32)
+    xd = torch.randn(B, T, K, generator=g) * 0.3
+    hds, ttape = Fn.lstm_layer_tfwd(xd.to(cuda), W.to(cuda), tape, U.to(cuda), 2)
+    th, tz, tc = R.lstm_seq_tfwd(xd.double() @ W.double(), rg, rc, U.double(), 2)
+    _close(hds, th, torch.float32)
+    dHd = torch.randn(B, T, H, generator=g)
+    dZ2, dZd2 = Fn.lstm_layer_tbwd(dH.to(cuda), dHd.to(cuda), tape, ttape, U.to(cuda), 2)
+    rz, rzd = R.lstm_seq_tbwd(dH.double(), dHd.double(), rg, rc, tz, tc, U.double(), 2)
+    _close(dZ2, rz, torch.float32)
+    _close(dZd2, rzd, torch.float32)
 
 
 @pytest.mark.parametrize("B,T,K,tangent", [(70, 24, 32, False), (33, 12, 100, True), (1000, 24, 100, False),
