@@ -68,8 +68,8 @@ Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act) {
   GUARD(x);
   const int M = x.size(0), K = x.size(1), N = W.size(1);
   Tensor y = out_empty({M, N}, x.options());
-  if (dt_of(x) == hfrep::DT_BF16 && hfrep::skinny_supported(K, N))
-    hfrep::launch_skinny_fwd(x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
+  if (hfrep::skinny_supported(K, N))
+    hfrep::launch_skinny_fwd(dt_of(x), x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
                              y.data_ptr(), M, K, N, (int)act, cur_stream(x));
   else if (dt_of(x) == hfrep::DT_BF16 && hfrep::narrow_supported(K, N))
     hfrep::launch_narrow_fwd(x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
@@ -90,8 +90,8 @@ Tensor linear_dgrad(Tensor dz, Tensor W) {
   const int M = dz.size(0), K = dz.size(1), N = W.size(0);
   Tensor dx = out_empty({M, N}, dz.options());
   // dx = dz . W^T : W stored (N, K) row-major -> w_trans
-  if (dt_of(dz) == hfrep::DT_BF16 && hfrep::skinny_supported(N, K))
-    hfrep::launch_skinny_dgrad(dz.data_ptr(), W.data_ptr<float>(), dx.data_ptr(), M, N, K, cur_stream(dz));
+  if (hfrep::skinny_supported(N, K))
+    hfrep::launch_skinny_dgrad(dt_of(dz), dz.data_ptr(), W.data_ptr<float>(), dx.data_ptr(), M, N, K, cur_stream(dz));
   else if (dt_of(dz) == hfrep::DT_BF16 && N > 64)
     hfrep::launch_linear2(dz.data_ptr(), W.data_ptr<float>(), nullptr, dx.data_ptr(), M, N, K, 1, 0, cur_stream(dz));
   else
@@ -108,9 +108,9 @@ void linear_wgrad_(Tensor x, Tensor dz, Tensor gW, optional<Tensor> gb, int64_t 
   if (gb.has_value()) { CHECK_F32(*gb); TORCH_CHECK(gb->numel() == dz.size(1), "wgrad: gb size"); }
   GUARD(x);
   const int M = x.size(0), K = x.size(1), N = dz.size(1);
-  if (dt_of(x) == hfrep::DT_BF16 && shiftT == 0 && hfrep::skinny_supported(K, N)) {
+  if (shiftT == 0 && hfrep::skinny_supported(K, N)) {
     Tensor ws = out_empty({(int64_t)hfrep::skinny_wgrad_workspace_floats(M, K, N)}, x.options().dtype(at::kFloat));
-    hfrep::launch_skinny_wgrad(x.data_ptr(), dz.data_ptr(), gW.data_ptr<float>(),
+    hfrep::launch_skinny_wgrad(dt_of(x), x.data_ptr(), dz.data_ptr(), gW.data_ptr<float>(),
                                gb.has_value() ? gb->data_ptr<float>() : nullptr, M, K, N, ws.data_ptr<float>(),
                                cur_stream(x));
     return;

@@ -90,17 +90,17 @@ size_t lstm_wgrad3_workspace_floats(int K, int Hd, int N);
 bool launch_lstm_wgrad3(const void* X0, const void* H0, const void* D0, const void* X1, const void* H1, const void* D1,
                         float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s);
 
-// ---- skinny.hip (bf16, N <= 4 output columns, K % 8 == 0: the Flatten -> Dense(1) critic head) ----
+// ---- skinny.hip (bf16 / fp32, N <= 4 output columns, K % 8 == 0: the Flatten -> Dense(1) critic head) ----
 bool skinny_supported(int K, int N);
 bool narrow_supported(int K, int N);  // 4 < N <= 64, K <= 128 (bf16 forward only)
 void launch_narrow_fwd(const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
                        hipStream_t s);
-void launch_skinny_fwd(const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
+void launch_skinny_fwd(int dt, const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
                        hipStream_t s);
 size_t skinny_wgrad_workspace_floats(int M, int K, int N);
-void launch_skinny_wgrad(const void* x, const void* d, float* gW, float* gb, int M, int K, int N, float* ws,
+void launch_skinny_wgrad(int dt, const void* x, const void* d, float* gW, float* gb, int M, int K, int N, float* ws,
                          hipStream_t s);
-void launch_skinny_dgrad(const void* d, const float* W, void* dx, int M, int K, int N, hipStream_t s);
+void launch_skinny_dgrad(int dt, const void* d, const float* W, void* dx, int M, int K, int N, hipStream_t s);
 // a[0..na) += sum_z slab[z][0..na), b[0..nb) += sum_z slab[z][na..na+nb)  (fixed order; a/b may be null)
 void launch_split_reduce(const float* slab, float* a, float* b, int splits, int na, int nb, hipStream_t s);
 

@@ -1,4 +1,4 @@
-// Skinny GEMMs (bf16 activations, N <= 4 output columns, K % 8 == 0): the critic head
+// Skinny GEMMs (bf16 or fp32 activations, N <= 4 output columns, K % 8 == 0): the critic head
 // Flatten(T*H) -> Dense(1) of every WGAN family (reference GAN/MTSS_WGAN_GP.py build_critic).
 //
 // All three products of a Dense(1) layer are HBM-streaming with O(1) arithmetic per byte, so the
@@ -29,13 +29,40 @@ __device__ __forceinline__ void unpack8(const uint4& v, float (&f)[8]) {
 }
 __device__ __forceinline__ uint32_t pack2(float a, float b) { return pk2bf(a, b); }
 
+// 8 consecutive elements of a row: one 16-byte access in bf16, two in fp32
+template <typename T> struct Chunk8;
+template <> struct Chunk8<bf16_t> {
+  uint4 v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void zero() { v = make_uint4(0, 0, 0, 0); }
+  __device__ __forceinline__ void get(float (&f)[8]) const { unpack8(v, f); }
+  __device__ __forceinline__ static void store(bf16_t* p, const float (&o)[8]) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+  }
+};
+template <> struct Chunk8<float> {
+  float4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *reinterpret_cast<const float4*>(p);
+    b = *reinterpret_cast<const float4*>(p + 4);
+  }
+  __device__ __forceinline__ void zero() { a = b = make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ __forceinline__ void get(float (&f)[8]) const {
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&o)[8]) {
+    *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(o[4], o[5], o[6], o[7]);
+  }
+};
+
 constexpr int SK_ROWS = 4;  // rows per wave in flight (forward)
 
 }  // namespace
 
-template <int N>
-__global__ void __launch_bounds__(256) skinny_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W,
-                                                         const float* __restrict__ b, bf16_t* __restrict__ y, int M,
+template <int N, typename T>
+__global__ void __launch_bounds__(256) skinny_fwd_kernel(const T* __restrict__ x, const float* __restrict__ W,
+                                                         const float* __restrict__ b, T* __restrict__ y, int M,
                                                          int K, int act) {
   extern __shared__ float wsh[];  // [K][N]
   for (int i = threadIdx.x; i < K * N; i += 256) wsh[i] = W[i];
@@ -50,10 +77,12 @@ __global__ void __launch_bounds__(256) skinny_fwd_kernel(const bf16_t* __restric
 #pragma unroll
       for (int n = 0; n < N; ++n) acc[r][n] = 0.f;
     for (int c = lane; c < KC; c += 64) {
-      uint4 v[SK_ROWS];
+      Chunk8<T> v[SK_ROWS];
 #pragma unroll
-      for (int r = 0; r < SK_ROWS; ++r)
-        v[r] = (m0 + r < M) ? *reinterpret_cast<const uint4*>(x + (m0 + r) * K + 8 * c) : make_uint4(0, 0, 0, 0);
+      for (int r = 0; r < SK_ROWS; ++r) {
+        if (m0 + r < M) v[r].load(x + (m0 + r) * K + 8 * c);
+        else v[r].zero();
+      }
       float w[8][N];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -62,7 +91,7 @@ __global__ void __launch_bounds__(256) skinny_fwd_kernel(const bf16_t* __restric
 #pragma unroll
       for (int r = 0; r < SK_ROWS; ++r) {
         float f[8];
-        unpack8(v[r], f);
+        v[r].get(f);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
 #pragma unroll
@@ -74,13 +103,13 @@ __global__ void __launch_bounds__(256) skinny_fwd_kernel(const bf16_t* __restric
 #pragma unroll
       for (int n = 0; n < N; ++n) {
         const float s = wave_sum(acc[r][n]);
-        if (lane == 0 && m0 + r < M) y[(m0 + r) * N + n] = f2bf(act_f(act, s + (b ? b[n] : 0.f)));
+        if (lane == 0 && m0 + r < M) y[(m0 + r) * N + n] = Cvt<T>::from_f(act_f(act, s + (b ? b[n] : 0.f)));
       }
   }
 }
 
-template <int N>
-__global__ void __launch_bounds__(1024) skinny_wgrad_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ d,
+template <int N, typename T>
+__global__ void __launch_bounds__(1024) skinny_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ d,
                                                             float* __restrict__ slab, int M, int K, int rps) {
   const int c = threadIdx.x, KC = K / 8;
   const int z = blockIdx.x;
@@ -95,18 +124,19 @@ __global__ void __launch_bounds__(1024) skinny_wgrad_kernel(const bf16_t* __rest
   const bool own = c < KC;
   int m = mb;
   for (; m + 4 <= me; m += 4) {  // four rows in flight
-    uint4 v[4];
+    Chunk8<T> v[4];
     float dv[4][N];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      v[r] = own ? *reinterpret_cast<const uint4*>(x + (int64_t)(m + r) * K + 8 * c) : make_uint4(0, 0, 0, 0);
+      if (own) v[r].load(x + (int64_t)(m + r) * K + 8 * c);
+      else v[r].zero();
 #pragma unroll
-      for (int n = 0; n < N; ++n) dv[r][n] = bf2f(d[(int64_t)(m + r) * N + n]);
+      for (int n = 0; n < N; ++n) dv[r][n] = ld_f(d + (int64_t)(m + r) * N + n);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float f[8];
-      unpack8(v[r], f);
+      v[r].get(f);
 #pragma unroll
       for (int n = 0; n < N; ++n) {
         bacc[n] += dv[r][n];
@@ -116,12 +146,14 @@ __global__ void __launch_bounds__(1024) skinny_wgrad_kernel(const bf16_t* __rest
     }
   }
   for (; m < me; ++m) {
-    const uint4 v = own ? *reinterpret_cast<const uint4*>(x + (int64_t)m * K + 8 * c) : make_uint4(0, 0, 0, 0);
+    Chunk8<T> v;
+    if (own) v.load(x + (int64_t)m * K + 8 * c);
+    else v.zero();
     float f[8];
-    unpack8(v, f);
+    v.get(f);
 #pragma unroll
     for (int n = 0; n < N; ++n) {
-      const float dv = bf2f(d[(int64_t)m * N + n]);
+      const float dv = ld_f(d + (int64_t)m * N + n);
       bacc[n] += dv;
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j][n] = fmaf(f[j], dv, acc[j][n]);
@@ -174,9 +206,9 @@ __global__ void __launch_bounds__(1024) skinny_reduce_kernel(const float* __rest
   }
 }
 
-template <int N>
-__global__ void __launch_bounds__(256) skinny_dgrad_kernel(const bf16_t* __restrict__ d, const float* __restrict__ W,
-                                                           bf16_t* __restrict__ dx, int M, int K) {
+template <int N, typename T>
+__global__ void __launch_bounds__(256) skinny_dgrad_kernel(const T* __restrict__ d, const float* __restrict__ W,
+                                                           T* __restrict__ dx, int M, int K) {
   const int KC = K / 8;
   const int64_t total = (int64_t)M * KC;
   for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
@@ -184,7 +216,7 @@ __global__ void __launch_bounds__(256) skinny_dgrad_kernel(const bf16_t* __restr
     const int c = (int)(q - m * KC);
     float dv[N];
 #pragma unroll
-    for (int n = 0; n < N; ++n) dv[n] = bf2f(d[m * N + n]);
+    for (int n = 0; n < N; ++n) dv[n] = ld_f(d + m * N + n);
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -193,8 +225,7 @@ __global__ void __launch_bounds__(256) skinny_dgrad_kernel(const bf16_t* __restr
       for (int n = 0; n < N; ++n) s = fmaf(dv[n], W[(8 * c + j) * N + n], s);
       o[j] = s;
     }
-    *reinterpret_cast<uint4*>(dx + m * K + 8 * c) = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]),
-                                                                pack2(o[4], o[5]), pack2(o[6], o[7]));
+    Chunk8<T>::store(dx + m * K + 8 * c, o);
   }
 }
 
@@ -280,21 +311,25 @@ bool skinny_supported(int K, int N) {
   return N >= 1 && N <= 4 && K % 8 == 0 && K >= 8 && K / 8 <= 1024 && K * N <= 16384;  // W in <= 64 KB LDS
 }
 
-#define HFREP_SKINNY_N(N, KERNEL, ...)                                     \
+#define HFREP_SKINNY_N(N, KERNEL, T, ...)                                  \
   switch (N) {                                                             \
-    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;             \
-    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;             \
-    case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break;             \
-    default: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;            \
+    case 1: hipLaunchKernelGGL((KERNEL<1, T>), __VA_ARGS__); break;        \
+    case 2: hipLaunchKernelGGL((KERNEL<2, T>), __VA_ARGS__); break;        \
+    case 3: hipLaunchKernelGGL((KERNEL<3, T>), __VA_ARGS__); break;        \
+    default: hipLaunchKernelGGL((KERNEL<4, T>), __VA_ARGS__); break;       \
   }
 
-void launch_skinny_fwd(const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
+void launch_skinny_fwd(int dt, const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
                        hipStream_t s) {
   if (M <= 0) return;
   const int64_t groups = ((int64_t)M + 4 * SK_ROWS - 1) / (4 * SK_ROWS);
   const int grid = (int)std::min<int64_t>(groups, (int64_t)device_cu_count() * 8);
-  HFREP_SKINNY_N(N, skinny_fwd_kernel, dim3(grid), dim3(256), (size_t)K * N * sizeof(float), s, (const bf16_t*)x, W, b,
-                 (bf16_t*)y, M, K, act)
+  if (dt == DT_BF16)
+    HFREP_SKINNY_N(N, skinny_fwd_kernel, bf16_t, dim3(grid), dim3(256), (size_t)K * N * sizeof(float), s, (const bf16_t*)x,
+                   W, b, (bf16_t*)y, M, K, act)
+  else
+    HFREP_SKINNY_N(N, skinny_fwd_kernel, float, dim3(grid), dim3(256), (size_t)K * N * sizeof(float), s, (const float*)x,
+                   W, b, (float*)y, M, K, act)
 }
 
 size_t skinny_wgrad_workspace_floats(int M, int K, int N) {
@@ -302,14 +337,18 @@ size_t skinny_wgrad_workspace_floats(int M, int K, int N) {
   return (size_t)splits * (K + 1) * N;
 }
 
-void launch_skinny_wgrad(const void* x, const void* d, float* gW, float* gb, int M, int K, int N, float* ws,
+void launch_skinny_wgrad(int dt, const void* x, const void* d, float* gW, float* gb, int M, int K, int N, float* ws,
                          hipStream_t s) {
   if (M <= 0) return;
   const int splits = std::max(1, std::min(512, (M + 63) / 64));
   const int rps = (M + splits - 1) / splits;
   const int threads = ((K / 8 + 63) / 64) * 64;
-  HFREP_SKINNY_N(N, skinny_wgrad_kernel, dim3(splits), dim3(threads), 0, s, (const bf16_t*)x, (const bf16_t*)d, ws, M, K,
-                 rps)
+  if (dt == DT_BF16)
+    HFREP_SKINNY_N(N, skinny_wgrad_kernel, bf16_t, dim3(splits), dim3(threads), 0, s, (const bf16_t*)x, (const bf16_t*)d,
+                   ws, M, K, rps)
+  else
+    HFREP_SKINNY_N(N, skinny_wgrad_kernel, float, dim3(splits), dim3(threads), 0, s, (const float*)x, (const float*)d, ws,
+                   M, K, rps)
   const int total = (K + 1) * N;
   hipLaunchKernelGGL(skinny_reduce_kernel, dim3((total + 63) / 64), dim3(1024), 0, s, ws, gW, gb, splits, K * N, N);
 }
@@ -319,11 +358,14 @@ void launch_split_reduce(const float* slab, float* a, float* b, int splits, int 
   hipLaunchKernelGGL(skinny_reduce_kernel, dim3((total + 63) / 64), dim3(1024), 0, s, slab, a, b, splits, na, nb);
 }
 
-void launch_skinny_dgrad(const void* d, const float* W, void* dx, int M, int K, int N, hipStream_t s) {
+void launch_skinny_dgrad(int dt, const void* d, const float* W, void* dx, int M, int K, int N, hipStream_t s) {
   if (M <= 0) return;
   const int64_t total = (int64_t)M * (K / 8);
   const int grid = (int)std::min<int64_t>((total + 255) / 256, (int64_t)device_cu_count() * 16);
-  HFREP_SKINNY_N(N, skinny_dgrad_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)d, W, (bf16_t*)dx, M, K)
+  if (dt == DT_BF16)
+    HFREP_SKINNY_N(N, skinny_dgrad_kernel, bf16_t, dim3(grid), dim3(256), 0, s, (const bf16_t*)d, W, (bf16_t*)dx, M, K)
+  else
+    HFREP_SKINNY_N(N, skinny_dgrad_kernel, float, dim3(grid), dim3(256), 0, s, (const float*)d, W, (float*)dx, M, K)
 }
 
 }  // namespace hfrep

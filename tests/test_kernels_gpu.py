@@ -400,29 +400,32 @@ def test_lstm_wgrad_fused(cuda, B, T, K, tangent, impl):
     assert err < 1e-3 * sc(x, dZ), err
 
 
-@pytest.mark.parametrize("M,K,N", [(37, 2400, 1), (1000, 2400, 1), (513, 64, 3), (70, 8, 4), (4099, 800, 2)])
-def test_skinny_dense_ops(cuda, M, K, N):
-    """Flatten -> Dense(N <= 4) head kernels (csrc/skinny.hip): forward, input grad, weight+bias grad
-    vs fp64 products of the same bf16 inputs."""
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,K,N", [(37, 2400, 1), (1000, 2400, 1), (513, 64, 3), (70, 8, 4), (4099, 800, 2),
+                                   (70001, 2400, 1)])
+def test_skinny_dense_ops(cuda, dt, M, K, N):
+    """Flatten -> Dense(N <= 4) head kernels (csrc/skinny.hip, bf16 and fp32): forward, input grad,
+    weight+bias grad vs fp64 products of the same inputs."""
     from hfrep.ops import functional as Fn
 
     g = torch.Generator().manual_seed(40)
-    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    x = torch.randn(M, K, generator=g).to(dt)
     W = torch.randn(K, N, generator=g) * K ** -0.5
     b = torch.randn(N, generator=g)
     y = Fn.linear(x.to(cuda), W.to(cuda), b.to(cuda), 0)
     ry = x.double() @ W.double() + b.double()
-    _close(y, ry, torch.bfloat16, scale=(x.double().abs() @ W.double().abs()).max().item())
-    d = torch.randn(M, N, generator=g).to(torch.bfloat16)
+    _close(y, ry, dt, scale=(x.double().abs() @ W.double().abs()).max().item())
+    d = torch.randn(M, N, generator=g).to(dt)
     dx = Fn.linear_dgrad(d.to(cuda), W.to(cuda))
-    _close(dx, d.double() @ W.double().t(), torch.bfloat16)
+    _close(dx, d.double() @ W.double().t(), dt)
     gW0, gb0 = torch.randn(K, N, generator=g), torch.randn(N, generator=g)
     gW, gb = gW0.clone().to(cuda), gb0.clone().to(cuda)
     Fn.linear_wgrad_(x.to(cuda), d.to(cuda), gW, gb)
     rW = gW0.double() + x.double().t() @ d.double()
     rb = gb0.double() + d.double().sum(0)
-    assert (gW.cpu().double() - rW).abs().max().item() < 1e-3 * max(1.0, (x.double().abs().t() @ d.double().abs()).max().item())
-    assert (gb.cpu().double() - rb).abs().max().item() < 1e-3 * max(1.0, d.double().abs().sum(0).max().item())
+    tol = 1e-3 if dt == torch.bfloat16 else 2e-5
+    assert (gW.cpu().double() - rW).abs().max().item() < tol * max(1.0, (x.double().abs().t() @ d.double().abs()).max().item())
+    assert (gb.cpu().double() - rb).abs().max().item() < tol * max(1.0, d.double().abs().sum(0).max().item())
 
 
 @pytest.mark.parametrize("B,D", [(7, 768), (16384, 768), (33, 100)])
