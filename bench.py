@@ -28,6 +28,25 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
+# model -> (metric label, config description); the headline is the first one (BASELINE.json "metric")
+MODELS = {
+    "mtss_wgan_gp": ("seq/sec/node MTSS-WGAN-GP train (24x32 windows) at 1/2/4/8 GPUs; W-dist parity",
+                     "MTSS-WGAN-GP (G: LSTM100(sigmoid)-LN-LSTM100(sigmoid)-LReLU-LN-Dense32; "
+                     "C: LSTM100-LSTM100-Flatten-Dense1; GP lambda=10; n_critic=5; RMSprop 5e-5)"),
+    "wgan_gp": ("seq/sec/node WGAN-GP (MLP) train (24x32 windows)",
+                "WGAN-GP (G: Dense100(sigmoid)-LReLU-LN-Dense100(sigmoid)-LReLU-LN-Dense32; "
+                "C: Dense100-Dense100-Flatten-Dense1; GP lambda=10; n_critic=5; RMSprop 5e-5)"),
+    "gan": ("seq/sec/node vanilla GAN (MLP) train (24x32 windows)",
+            "GAN (G: Dense100(sigmoid)-LReLU-LN-Dense100(sigmoid)-LReLU-LN-Dense32; "
+            "D: Dense100-Dense100-Dense1(sigmoid) per step; BCE; Adam 2e-4 b1=0.5)"),
+    "mtss_gan": ("seq/sec/node MTSS-GAN (LSTM) train (24x32 windows)", "MTSS-GAN (LSTM G / LSTM D, BCE, Adam)"),
+    "mtss_wgan": ("seq/sec/node MTSS-WGAN (LSTM, clipped) train (24x32 windows)",
+                  "MTSS-WGAN (LSTM G / LSTM-LReLU-LN critic, clip 0.01, n_critic=5, RMSprop)"),
+    "conv_wgan_gp": ("seq/sec/node conv-critic WGAN-GP train (24x32 windows)",
+                     "LSTM G / causal Conv1D critic, GP lambda=10, n_critic=5"),
+}
+
+
 def _measure(args, dtype, rank, world, pg, dev):
     """Warm up, then time exactly args.steps training iterations at one compute dtype."""
     import numpy as np
@@ -37,9 +56,12 @@ def _measure(args, dtype, rank, world, pg, dev):
     from hfrep.data.windows import synthetic_windows
     from hfrep.train.gan_trainer import GANConfig, GANTrainer
 
+    from hfrep.models import gan as zoo
+
     T, F, B = args.window, args.features, args.batch_per_gpu
+    arch, loss = zoo.resolve(args.model)
     ds = synthetic_windows(args.dataset_windows, T, F, seed=1234)
-    cfg = GANConfig(arch="lstm", loss="wgan_gp", window=T, features=F, batch_size=B, dtype=dtype, seed=123)
+    cfg = GANConfig(arch=arch, loss=loss, window=T, features=F, batch_size=B, dtype=dtype, seed=123)
     tr = GANTrainer(cfg, ds, device=dev, process_group=pg, rank=rank, world=world)
     torch.cuda.reset_peak_memory_stats(dev)
 
@@ -98,6 +120,9 @@ def main():
     ap.add_argument("--dtype", default="both", choices=["both", "float32", "bfloat16"],
                     help="both (default): the reference-precision fp32 record, plus a bf16 sub-record timed the "
                          "same way right after it")
+    ap.add_argument("--model", default="mtss_wgan_gp", choices=sorted(MODELS),
+                    help="mtss_wgan_gp (default) is the BASELINE headline; gan / wgan_gp are BASELINE configs 3 / 4 "
+                         "(GAN.py, WGAN_GP.py MLP models) measured the same way")
     ap.add_argument("--dataset-windows", type=int, default=8192)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (e.g. for rocprof)")
     ap.add_argument("--trace-out", default="", help="after the timed steps: torch.profiler Chrome trace of "
@@ -122,7 +147,7 @@ def main():
     T, F, B = args.window, args.features, args.batch_per_gpu
     if rank == 0:
         rec = {
-            "metric": "seq/sec/node MTSS-WGAN-GP train (24x32 windows) at 1/2/4/8 GPUs; W-dist parity",
+            "metric": MODELS[args.model][0],
             "value": res["value"],
             "unit": "seq/s",
             "n_gpus": world,
@@ -137,8 +162,7 @@ def main():
             "dtype": "fp32" if primary == "float32" else "bf16",
             "data": "synthetic",
             "config": {
-                "model": "MTSS-WGAN-GP (G: LSTM100(sigmoid)-LN-LSTM100(sigmoid)-LReLU-LN-Dense32; "
-                         "C: LSTM100-LSTM100-Flatten-Dense1; GP lambda=10; n_critic=5; RMSprop 5e-5)",
+                "model": MODELS[args.model][1],
                 "global_batch": B * world,
                 "batch_per_gpu": B,
                 "seq_len": T,
@@ -148,7 +172,7 @@ def main():
             },
             "losses_finite": res["losses_finite"],
             # the W-dist half of the metric is a training-quality run, not a throughput step
-            "w_dist_parity": "profiles/r02_parity/README.md",
+            "w_dist_parity": "profiles/r02_parity/README.md" if args.model == "mtss_wgan_gp" else None,
             "peak_mem_gb_rank0": res["peak_mem_gb_rank0"],
         }
         if sub is not None:

@@ -509,6 +509,49 @@ Tensor layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, optiona
   return dx;
 }
 
+Tensor layernorm_tfwd(Tensor xd, Tensor xhat, Tensor rstd, Tensor gamma) {
+  CHECK_GPU(xd); CHECK_GPU(xhat); same_dt(xd, xhat); CHECK_F32(rstd); CHECK_F32(gamma);
+  const int D = xd.size(-1);
+  TORCH_CHECK(D <= 256 && gamma.numel() == D && xhat.numel() == xd.numel() && rstd.numel() * D == xd.numel(),
+              "layernorm_tfwd: D <= 256 and matching xd / xhat / rstd");
+  GUARD(xd);
+  xd = xd.contiguous();
+  Tensor yd = out_empty_like(xd);
+  hfrep::launch_layernorm_tfwd(dt_of(xd), xd.data_ptr(), xhat.data_ptr(), rstd.data_ptr<float>(),
+                               gamma.data_ptr<float>(), yd.data_ptr(), xd.numel() / D, D, cur_stream(xd));
+  return yd;
+}
+
+// (dx, dxd); need_dx == false returns two empty tensors and only accumulates ggamma / gbeta
+std::tuple<Tensor, Tensor> layernorm_tbwd_(optional<Tensor> dy, Tensor dyd, Tensor xd, Tensor xhat, Tensor rstd,
+                                           Tensor gamma, Tensor ggamma, Tensor gbeta, bool need_dx) {
+  CHECK_GPU(dyd); CHECK_GPU(xd); CHECK_GPU(xhat); same_dt(dyd, xd); same_dt(dyd, xhat);
+  CHECK_F32(rstd); CHECK_F32(gamma); CHECK_F32(ggamma); CHECK_F32(gbeta);
+  const int D = dyd.size(-1);
+  const int64_t n = dyd.numel();
+  TORCH_CHECK(D <= 256 && gamma.numel() == D && ggamma.numel() == D && gbeta.numel() == D && xd.numel() == n &&
+                  xhat.numel() == n && rstd.numel() * D == n,
+              "layernorm_tbwd: D <= 256 and matching operand sizes");
+  Tensor dyc;
+  if (dy.has_value()) {
+    CHECK_GPU(*dy); same_dt(*dy, dyd);
+    TORCH_CHECK(dy->numel() == n, "layernorm_tbwd: dy size");
+    dyc = dy->contiguous();
+  }
+  GUARD(dyd);
+  dyd = dyd.contiguous(); xd = xd.contiguous();
+  const int64_t rows = n / D;
+  Tensor dx = need_dx ? out_empty_like(dyd) : out_empty({0}, dyd.options());
+  Tensor dxd = need_dx ? out_empty_like(dyd) : out_empty({0}, dyd.options());
+  Tensor ws = out_empty({(int64_t)hfrep::layernorm_bwd_splits(rows) * 2 * D}, dyd.options().dtype(at::kFloat));
+  hfrep::launch_layernorm_tbwd(dt_of(dyd), dy.has_value() ? dyc.data_ptr() : nullptr, dyd.data_ptr(), xd.data_ptr(),
+                               xhat.data_ptr(), rstd.data_ptr<float>(), gamma.data_ptr<float>(),
+                               need_dx ? dx.data_ptr() : nullptr, need_dx ? dxd.data_ptr() : nullptr,
+                               ggamma.data_ptr<float>(), gbeta.data_ptr<float>(), ws.data_ptr<float>(), rows, D,
+                               cur_stream(dyd));
+  return {dx, dxd};
+}
+
 // ------------------------------------------------------------------------------------ conv1d (causal)
 Tensor im2col_causal(Tensor x, int64_t k, int64_t dil) {
   CHECK_GPU(x);
@@ -663,6 +706,9 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("layernorm_fwd(Tensor x, Tensor gamma, Tensor beta, float eps, bool save=True, float pre_lrelu=-1.0) -> "
         "(Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd_(Tensor dy, Tensor xhat, Tensor rstd, Tensor gamma, Tensor(a!)? ggamma, Tensor(b!)? gbeta) -> Tensor");
+  m.def("layernorm_tfwd(Tensor xd, Tensor xhat, Tensor rstd, Tensor gamma) -> Tensor");
+  m.def("layernorm_tbwd_(Tensor? dy, Tensor dyd, Tensor xd, Tensor xhat, Tensor rstd, Tensor gamma, "
+        "Tensor(a!) ggamma, Tensor(b!) gbeta, bool need_dx) -> (Tensor, Tensor)");
   m.def("gp_coef(Tensor g, float weight) -> (Tensor, Tensor)");
   m.def("gan_loss(Tensor p, int split, float la, float lb, int kind) -> (Tensor, Tensor)");
   m.def("im2col_causal(Tensor x, int k, int dil) -> Tensor");
@@ -699,6 +745,8 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("lstm2_tbwd", &lstm2_tbwd);
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("layernorm_bwd_", &layernorm_bwd_);
+  m.impl("layernorm_tfwd", &layernorm_tfwd);
+  m.impl("layernorm_tbwd_", &layernorm_tbwd_);
   m.impl("gp_coef", &gp_coef);
   m.impl("gan_loss", &gan_loss);
   m.impl("im2col_causal", &im2col_causal);

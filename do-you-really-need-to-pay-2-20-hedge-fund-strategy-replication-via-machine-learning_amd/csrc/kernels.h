@@ -119,6 +119,13 @@ void launch_layernorm_fwd(int dt, const void* x, const float* gamma, const float
 int layernorm_bwd_splits(int64_t rows);
 void launch_layernorm_bwd(int dt, const void* dy, const void* xhat, const float* rstd, const float* gamma,
                           void* dx, float* ggamma, float* gbeta, float* ws, int64_t rows, int D, hipStream_t s);
+// LayerNorm JVP (yd = gamma * xhat') and its reverse (dy may be null = zero primal seed; dx / dxd
+// both null = parameter gradients only); ggamma / gbeta accumulate through the same slab scheme
+void launch_layernorm_tfwd(int dt, const void* xd, const void* xhat, const float* rstd, const float* gamma, void* yd,
+                           int64_t rows, int D, hipStream_t s);
+void launch_layernorm_tbwd(int dt, const void* dy, const void* dyd, const void* xd, const void* xhat,
+                           const float* rstd, const float* gamma, void* dx, void* dxd, float* ggamma, float* gbeta,
+                           float* ws, int64_t rows, int D, hipStream_t s);
 // v = dGP/dg per row, pen += sum_b (1 - |g_b|)^2 / B  (rowpen: B floats of workspace)
 void launch_gan_loss(int dt, const void* p, int64_t n, int64_t split, float la, float lb, int kind, void* grad,
                      float* partial, float* out, hipStream_t s);

@@ -235,6 +235,160 @@ void launch_layernorm_bwd(int dt, const void* dy, const void* xhat, const float*
   if (slab) launch_split_reduce(slab, ggamma, gbeta, grid, D, D, s);
 }
 
+// ------------------------------------------------------------------ LayerNorm tangents (GP critics)
+// A gradient-penalty critic with LayerNorm (the lstm_critic_clip family) differentiates the LN's
+// Jacobian-vector product: the reference gets it from nested tf.GradientTape
+// (MTSS-GAN/mtss_gan.py:148-160); here it is two per-row kernels on the saved xhat / rstd.
+// Per row (r = rstd, mean over D):
+//   m = mean(xhat * xd),  xhatd = r (xd - mean(xd) - xhat m),  yd = gamma * xhatd
+// and for the reverse of (y, yd) with seeds (dy, dyd), g = gamma dy, h = gamma dyd,
+// S = sum(h xhat), P = sum(h xd):
+//   dxd = r (h - mean(h) - xhat S / D)
+//   G   = g - r m h - (r S / D) xd
+//   dx  = r (G - mean(G) - xhat mean(G xhat)) - r^2 xhat (P - D mean(xd) mean(h) - m S) / D
+//   dgamma += dy xhat + dyd xhatd,  dbeta += dy
+// mean(G) and mean(G xhat) expand into the seven raw row sums below, so every row is one read of
+// its four operands, one 7-way reduction and one write of dx / dxd.
+template <typename T>
+__global__ void __launch_bounds__(256) layernorm_tfwd_kernel(const T* __restrict__ xd, const T* __restrict__ xhat,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ gamma, T* __restrict__ yd,
+                                                             int64_t rows, int D) {
+  constexpr int MAXJ = 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float dv[MAXJ], hv[MAXJ], sd = 0.f, sxd = 0.f;
+#pragma unroll
+  for (int q = 0; q < MAXJ; ++q) {
+    const int j = lane + 64 * q;
+    dv[q] = j < D ? ld_f(xd + row * D + j) : 0.f;
+    hv[q] = j < D ? ld_f(xhat + row * D + j) : 0.f;
+    sd += dv[q];
+    sxd += dv[q] * hv[q];
+  }
+  const float mxd = wave_sum(sd) / D, m = wave_sum(sxd) / D, r = rstd[row];
+#pragma unroll
+  for (int q = 0; q < MAXJ; ++q) {
+    const int j = lane + 64 * q;
+    if (j < D) st_f(yd + row * D + j, gamma[j] * r * (dv[q] - mxd - hv[q] * m));
+  }
+}
+
+template <typename T, bool HAS_DY, bool NEED_DX>
+__global__ void __launch_bounds__(256) layernorm_tbwd_kernel(const T* __restrict__ dy, const T* __restrict__ dyd,
+                                                             const T* __restrict__ xd, const T* __restrict__ xhat,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ gamma, T* __restrict__ dx,
+                                                             T* __restrict__ dxd, float* __restrict__ slab,
+                                                             int64_t rows, int D) {
+  constexpr int MAXJ = 4;  // D <= 256
+  __shared__ float red_g[4 * MAXJ * 64];
+  __shared__ float red_b[4 * MAXJ * 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float pg[MAXJ] = {0.f, 0.f, 0.f, 0.f}, pb[MAXJ] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += wstride) {
+    const int64_t o = row * D;
+    float yv[MAXJ], ev[MAXJ], hv[MAXJ], dv[MAXJ], xv[MAXJ];
+    float s_d = 0.f, s_xd = 0.f, s_g = 0.f, s_gx = 0.f, s_h = 0.f, s_hx = 0.f, s_hd = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXJ; ++q) {
+      const int j = lane + 64 * q;
+      const bool on = j < D;
+      const float ga = on ? gamma[j] : 0.f;
+      yv[q] = (HAS_DY && on) ? ld_f(dy + o + j) : 0.f;
+      ev[q] = on ? ld_f(dyd + o + j) : 0.f;
+      hv[q] = ga * ev[q];  // h = gamma dyd
+      dv[q] = on ? ld_f(xd + o + j) : 0.f;
+      xv[q] = on ? ld_f(xhat + o + j) : 0.f;
+      const float g = ga * yv[q];
+      s_d += dv[q];
+      s_xd += xv[q] * dv[q];
+      s_g += g;
+      s_gx += g * xv[q];
+      s_h += hv[q];
+      s_hx += hv[q] * xv[q];
+      s_hd += hv[q] * dv[q];
+    }
+    const float invD = 1.f / D, r = rstd[row];
+    const float mxd = wave_sum(s_d) * invD, m = wave_sum(s_xd) * invD;
+    const float mh = wave_sum(s_h) * invD, S = wave_sum(s_hx), P = wave_sum(s_hd);
+    const float c = r * S * invD;  // coefficient of xd in G (and of xhat in dxd, divided by r)
+    float mG = 0.f, mGx = 0.f;
+    if constexpr (NEED_DX) {
+      mG = wave_sum(s_g) * invD - r * m * mh - c * mxd;
+      mGx = wave_sum(s_gx) * invD - 2.f * r * m * S * invD;
+    }
+    const float kr = r * r * (P - D * mxd * mh - m * S) * invD;
+#pragma unroll
+    for (int q = 0; q < MAXJ; ++q) {
+      const int j = lane + 64 * q;
+      if (j < D) {
+        const float ga = gamma[j];
+        const float xhd = r * (dv[q] - mxd - xv[q] * m);
+        pg[q] += (HAS_DY ? yv[q] * xv[q] : 0.f) + ev[q] * xhd;
+        pb[q] += yv[q];
+        if constexpr (NEED_DX) {
+          const float G = ga * yv[q] - r * m * hv[q] - c * dv[q];
+          st_f(dx + o + j, r * (G - mG - xv[q] * mGx) - kr * xv[q]);
+          st_f(dxd + o + j, r * (hv[q] - mh) - c * xv[q]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MAXJ; ++q) {
+    red_g[(wid * MAXJ + q) * 64 + lane] = pg[q];
+    red_b[(wid * MAXJ + q) * 64 + lane] = pb[q];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < D; j += 256) {
+    const int q = j / 64, l = j % 64;
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { a += red_g[(w * MAXJ + q) * 64 + l]; b += red_b[(w * MAXJ + q) * 64 + l]; }
+    slab[(size_t)blockIdx.x * 2 * D + j] = a;
+    slab[(size_t)blockIdx.x * 2 * D + D + j] = b;
+  }
+}
+
+void launch_layernorm_tfwd(int dt, const void* xd, const void* xhat, const float* rstd, const float* gamma, void* yd,
+                           int64_t rows, int D, hipStream_t s) {
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 1 << 30));
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(layernorm_tfwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)xd,
+                       (const bf16_t*)xhat, rstd, gamma, (bf16_t*)yd, rows, D);
+  else
+    hipLaunchKernelGGL(layernorm_tfwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)xd,
+                       (const float*)xhat, rstd, gamma, (float*)yd, rows, D);
+}
+
+template <typename T>
+static void tbwd_dispatch(const void* dy, const void* dyd, const void* xd, const void* xhat, const float* rstd,
+                          const float* gamma, void* dx, void* dxd, float* slab, int64_t rows, int D, int grid,
+                          hipStream_t s) {
+#define HFREP_LNT(HD, ND)                                                                                       \
+  hipLaunchKernelGGL((layernorm_tbwd_kernel<T, HD, ND>), dim3(grid), dim3(256), 0, s, (const T*)dy, (const T*)dyd, \
+                     (const T*)xd, (const T*)xhat, rstd, gamma, (T*)dx, (T*)dxd, slab, rows, D)
+  if (dy && dx) HFREP_LNT(true, true);
+  else if (dy) HFREP_LNT(true, false);
+  else if (dx) HFREP_LNT(false, true);
+  else HFREP_LNT(false, false);
+#undef HFREP_LNT
+}
+
+void launch_layernorm_tbwd(int dt, const void* dy, const void* dyd, const void* xd, const void* xhat,
+                           const float* rstd, const float* gamma, void* dx, void* dxd, float* ggamma, float* gbeta,
+                           float* ws, int64_t rows, int D, hipStream_t s) {
+  const int grid = layernorm_bwd_splits(rows);
+  if (dt == DT_BF16)
+    tbwd_dispatch<bf16_t>(dy, dyd, xd, xhat, rstd, gamma, dx, dxd, ws, rows, D, grid, s);
+  else
+    tbwd_dispatch<float>(dy, dyd, xd, xhat, rstd, gamma, dx, dxd, ws, rows, D, grid, s);
+  launch_split_reduce(ws, ggamma, gbeta, grid, D, D, s);
+}
+
 // ------------------------------------------------------------------ gradient penalty coefficient
 // One wave per sample row: the per-row penalty term goes to its own slot and a single-workgroup
 // reduce sums them (a per-row atomicAdd on one address serialised 16k adds: 212 us at B = 16384).

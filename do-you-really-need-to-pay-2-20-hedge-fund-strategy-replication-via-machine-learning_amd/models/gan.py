@@ -103,13 +103,17 @@ ZOO = {
                                   save_prefix="MTSS_GAN_GP", legacy_class="WGAN_GP"),
     ("conv", "wgan_gp"): ZooEntry(lstm_generator, conv_critic_gp, "wgan_gp", "rmsprop", 5e-5, 5, gp_weight=10.0,
                                   save_prefix="CONV_GAN_GP", legacy_class="CONV_WGAN_GP"),
+    # the MTSS-WGAN LayerNorm critic trained with the gradient penalty instead of clipping (a
+    # framework variant: exercises the LayerNorm tangent kernels in the reverse-over-tangent critic step)
+    ("lstm_ln", "wgan_gp"): ZooEntry(lstm_generator, lstm_critic_clip, "wgan_gp", "rmsprop", 5e-5, 5, gp_weight=10.0,
+                                     save_prefix="MTSS_LN_GAN_GP", legacy_class="MTSS_LN_WGAN_GP"),
 }
 
 LEGACY = {e.legacy_class: k for k, e in ZOO.items()}
 ALIASES = {
     "gan": ("mlp", "gan"), "wgan": ("mlp", "wgan"), "wgan_gp": ("mlp", "wgan_gp"),
     "mtss_gan": ("lstm", "gan"), "mtss_wgan": ("lstm", "wgan"), "mtss_wgan_gp": ("lstm", "wgan_gp"),
-    "conv_wgan_gp": ("conv", "wgan_gp"),
+    "conv_wgan_gp": ("conv", "wgan_gp"), "mtss_ln_wgan_gp": ("lstm_ln", "wgan_gp"),
 }
 
 

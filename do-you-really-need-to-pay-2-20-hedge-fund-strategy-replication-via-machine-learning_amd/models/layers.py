@@ -268,18 +268,15 @@ class LayerNormalization(Layer):
         dx = Fn.layer_norm_bwd_(dy, ctx["xhat"], ctx["rstd"], self.p("gamma"), gg, gb)
         return dx if need_dx else None
 
-    @staticmethod
-    def _input(ctx):
-        """The LN input; after a fused LReLU -> LN forward it is rebuilt from the LReLU tape."""
-        if ctx.get("x") is None and "x_pre" in ctx:
-            ctx = dict(ctx, x=R.leaky_relu(ctx["x_pre"], ctx["alpha"]))
-        return ctx
-
+    # tangent pass of a GP critic with LayerNorm (lstm_critic_clip + wgan_gp): closed-form JVP and
+    # reverse kernels on the saved xhat / rstd (works after a fused LReLU -> LN forward too, whose
+    # tape holds xhat / rstd but not the LN input)
     def etfwd(self, ctx, xd):
-        return super().etfwd(self._input(ctx), xd)
+        return Fn.layer_norm_tfwd(xd, ctx["xhat"], ctx["rstd"], self.p("gamma")), {"xd": xd}
 
     def etbwd(self, ctx, tctx, dy, dyd, need_dx):
-        return super().etbwd(self._input(ctx), tctx, dy, dyd, need_dx)
+        return Fn.layer_norm_tbwd_(dy, dyd, tctx["xd"], ctx["xhat"], ctx["rstd"], self.p("gamma"), self.g("gamma"),
+                                   self.g("beta"), need_dx)
 
 
 class LeakyReLU(Layer):

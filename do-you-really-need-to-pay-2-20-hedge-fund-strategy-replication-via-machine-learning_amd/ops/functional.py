@@ -181,6 +181,25 @@ def layer_norm_bwd_(dy, xhat, rstd, gamma, ggamma, gbeta):
     return dx
 
 
+def layer_norm_tfwd(xd, xhat, rstd, gamma):
+    """LayerNorm JVP from the saved forward (xhat, rstd): the GP critic's tangent pass."""
+    if _nat(xd):
+        return _ops().layernorm_tfwd(xd.contiguous(), xhat, rstd, gamma)
+    return R.layer_norm_tfwd(xd, xhat, rstd, gamma.to(xd.dtype))
+
+
+def layer_norm_tbwd_(dy, dyd, xd, xhat, rstd, gamma, ggamma, gbeta, need_dx: bool):
+    """Reverse of the LN forward + JVP; accumulates dgamma / dbeta, returns (dx, dxd) or (None, None)."""
+    if _nat(dyd):
+        dx, dxd = _ops().layernorm_tbwd_(dy.contiguous() if dy is not None else None, dyd.contiguous(), xd, xhat,
+                                         rstd, gamma, ggamma, gbeta, bool(need_dx))
+        return (dx, dxd) if need_dx else (None, None)
+    dx, dxd, dg, db = R.layer_norm_tbwd(dy, dyd, xd, xhat, rstd, gamma.to(dyd.dtype))
+    ggamma.add_(dg.to(ggamma.dtype))
+    gbeta.add_(db.to(gbeta.dtype))
+    return (dx, dxd) if need_dx else (None, None)
+
+
 # ---------------------------------------------------------------------------------------
 # temporal conv helpers (im2col on the feature axis)
 # ---------------------------------------------------------------------------------------

@@ -357,3 +357,37 @@ def layer_norm_bwd(dy: torch.Tensor, xhat: torch.Tensor, rstd: torch.Tensor, gam
     dx = rstd * (g - g.mean(dim=-1, keepdim=True) - xhat * (g * xhat).mean(dim=-1, keepdim=True))
     red = tuple(range(dy.dim() - 1))
     return dx, (dy * xhat).sum(dim=red), dy.sum(dim=red)
+
+
+def layer_norm_tfwd(xd: torch.Tensor, xhat: torch.Tensor, rstd: torch.Tensor, gamma):
+    """JVP of LayerNorm w.r.t. its input: gamma * r (xd - mean(xd) - xhat mean(xhat xd))."""
+    m = (xhat * xd).mean(dim=-1, keepdim=True)
+    return gamma * (rstd * (xd - xd.mean(dim=-1, keepdim=True) - xhat * m))
+
+
+def layer_norm_tbwd(dy, dyd: torch.Tensor, xd: torch.Tensor, xhat: torch.Tensor, rstd: torch.Tensor, gamma):
+    """Reverse of (y, yd) = (LN(x), JVP(x; xd)) with seeds (dy, dyd); dy None = zero.
+
+    Returns (dx, dxd, dgamma, dbeta); the closed form the native kernel evaluates (csrc/misc.hip).
+    """
+    D = xhat.shape[-1]
+    r = rstd
+    mxd = xd.mean(dim=-1, keepdim=True)
+    m = (xhat * xd).mean(dim=-1, keepdim=True)
+    xhatd = r * (xd - mxd - xhat * m)
+    h = dyd * gamma
+    mh = h.mean(dim=-1, keepdim=True)
+    S = (h * xhat).sum(dim=-1, keepdim=True)
+    P = (h * xd).sum(dim=-1, keepdim=True)
+    dxd = r * (h - mh - xhat * S / D)
+    g = dy * gamma if dy is not None else torch.zeros_like(h)
+    G = g - r * m * h - (r * S / D) * xd
+    dx = r * (G - G.mean(dim=-1, keepdim=True) - xhat * (G * xhat).mean(dim=-1, keepdim=True)) \
+        - r * r * xhat * (P - D * mxd * mh - m * S) / D
+    red = tuple(range(dyd.dim() - 1))
+    dgamma = (dyd * xhatd).sum(dim=red)
+    dbeta = torch.zeros_like(dgamma)
+    if dy is not None:
+        dgamma = dgamma + (dy * xhat).sum(dim=red)
+        dbeta = dy.sum(dim=red)
+    return dx, dxd, dgamma, dbeta

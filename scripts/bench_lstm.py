@@ -36,11 +36,13 @@ def main():
     ap.add_argument("--act", type=int, default=2)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="fwd,tfwd,bwd,tbwd,bwd_dx,tbwd_dx,dgrad")
+    ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "float32"])
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, T, K, H = a.batch, a.T, a.K, 100
     g = torch.Generator(device=dev).manual_seed(0)
-    mk = lambda *s, sc=0.5: (torch.randn(*s, device=dev, generator=g) * sc).to(torch.bfloat16)
+    dt = getattr(torch, a.dtype)
+    mk = lambda *s, sc=0.5: (torch.randn(*s, device=dev, generator=g) * sc).to(dt)
     x, xd = mk(B, T, K), mk(B, T, K)
     W = torch.randn(K, 4 * H, device=dev, generator=g) * 0.1
     U = torch.randn(H, 4 * H, device=dev, generator=g) * 0.1
@@ -49,6 +51,7 @@ def main():
     hs, tape = Fn.lstm_layer_fwd(x, W, b, U, a.act, True)
     hds, ttape = Fn.lstm_layer_tfwd(xd, W, tape, U, a.act)
     dZ_ = Fn.lstm_layer_bwd(dH, tape, U, a.act)
+    gW, gU, gb = torch.zeros(K, 4 * H, device=dev), torch.zeros(H, 4 * H, device=dev), torch.zeros(4 * H, device=dev)
     ops = {
         "fwd": lambda: Fn.lstm_layer_fwd(x, W, b, U, a.act, True),
         "fwd_notape": lambda: Fn.lstm_layer_fwd(x, W, b, U, a.act, False),
@@ -58,10 +61,12 @@ def main():
         "bwd_dx": lambda: Fn.lstm_layer_bwd(dH, tape, U, a.act, W=W),
         "tbwd_dx": lambda: Fn.lstm_layer_tbwd(dH, dHd, tape, ttape, U, a.act, W=W),
         "dgrad": lambda: Fn.linear_dgrad(dZ_, W),
+        "wgrad": lambda: Fn.lstm_wgrad_(x, hs, dZ_, gW, gU, gb),
+        "wgrad_tan": lambda: Fn.lstm_wgrad_(x, hs, dZ_, gW, gU, gb, xd, hds, dZ_),
     }
     for name in a.only.split(","):
         ms = timeit(ops[name], a.iters)
-        print(json.dumps({"op": name, "B": B, "T": T, "K": K, "ms": round(ms, 4),
+        print(json.dumps({"op": name, "dtype": a.dtype, "B": B, "T": T, "K": K, "ms": round(ms, 4),
                           "us_per_step": round(ms * 1e3 / T, 2)}), flush=True)
 
 

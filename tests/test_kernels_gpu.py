@@ -157,6 +157,46 @@ def test_layernorm(cuda, dt, D):
     _close(gb, rdb, dt, scale=dy.double().abs().sum((0, 1)).max().item())
 
 
+@pytest.mark.parametrize("D", [100, 35, 256])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_layernorm_tangent(cuda, dt, D):
+    """LN JVP + its reverse (the GP critic's LayerNorm) vs torch.func over the fp64 LN: the
+    closed form in csrc/misc.hip against nested autodiff, with and without a primal seed."""
+    g = torch.Generator().manual_seed(17)
+    x = (torch.randn(29, 13, D, generator=g) * 2 + 0.5).double()
+    xd = torch.randn(29, 13, D, generator=g).double()
+    gamma, beta = torch.randn(D, generator=g).double(), torch.randn(D, generator=g).double()
+    dy, dyd = torch.randn(29, 13, D, generator=g).double(), torch.randn(29, 13, D, generator=g).double()
+    _, xhat, rstd = _ops().layernorm_fwd(x.to(dt).to(cuda), gamma.float().to(cuda), beta.float().to(cuda), 1e-3)
+    xq = x.to(dt).double()  # the kernel's input as rounded to dt
+    yd = _ops().layernorm_tfwd(xd.to(dt).to(cuda), xhat, rstd, gamma.float().to(cuda))
+
+    def ln(q, ga, be):
+        return R.layer_norm(q, ga, be, 1e-3)
+
+    for with_dy in (True, False):
+        xs, xds = xq.clone().requires_grad_(True), xd.to(dt).double().requires_grad_(True)
+        gs, bs = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+        y, ryd = torch.func.jvp(lambda q: ln(q, gs, bs), (xs,), (xds,))
+        seeds = [dy.to(dt).double() if with_dy else torch.zeros_like(dy), dyd.to(dt).double()]
+        rdx, rdxd, rdg, rdb = torch.autograd.grad([y, ryd], [xs, xds, gs, bs], seeds)
+        if with_dy:
+            _close(yd, ryd.detach(), dt)
+        gg, gb = torch.zeros(D, device=cuda), torch.zeros(D, device=cuda)
+        dx, dxd = _ops().layernorm_tbwd_(dy.to(dt).to(cuda) if with_dy else None, dyd.to(dt).to(cuda),
+                                         xd.to(dt).to(cuda), xhat, rstd, gamma.float().to(cuda), gg, gb, True)
+        _close(dx, rdx, dt)
+        _close(dxd, rdxd, dt)
+        _close(gg, rdg, dt, scale=(dyd.abs() * 4).sum((0, 1)).max().item())
+        _close(gb, rdb, dt, scale=dy.abs().sum((0, 1)).max().item())
+        # parameter-gradient-only form: same dgamma / dbeta, nothing written for dx / dxd
+        gg2, gb2 = torch.zeros(D, device=cuda), torch.zeros(D, device=cuda)
+        e1, e2 = _ops().layernorm_tbwd_(dy.to(dt).to(cuda) if with_dy else None, dyd.to(dt).to(cuda),
+                                        xd.to(dt).to(cuda), xhat, rstd, gamma.float().to(cuda), gg2, gb2, False)
+        assert e1.numel() == 0 and e2.numel() == 0
+        assert torch.equal(gg2, gg) and torch.equal(gb2, gb)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_gp_coef_and_interpolate(cuda, dt):
     g = torch.Generator().manual_seed(8)
@@ -221,7 +261,7 @@ def test_optimizers_match_cpu(cuda):
 
 
 @pytest.mark.parametrize("key", [("lstm", "wgan_gp"), ("mlp", "wgan_gp"), ("lstm", "wgan"), ("mlp", "gan"),
-                                 ("lstm", "gan"), ("conv", "wgan_gp")])
+                                 ("lstm", "gan"), ("conv", "wgan_gp"), ("lstm_ln", "wgan_gp")])
 def test_trainer_gradients_gpu_vs_cpu(cuda, key):
     """The full explicit critic/generator gradient programs on GPU (native kernels) vs CPU fp64."""
     from hfrep.train.gan_trainer import GANConfig, GANTrainer
@@ -333,7 +373,8 @@ BF16_GLOBAL, BF16_BLOCK = 1.5e-2, 5e-2
 
 @pytest.mark.parametrize("key,T,F,B,lrelu", [(("lstm", "wgan_gp"), 24, 32, 64, False), (("lstm", "wgan"), 24, 32, 64, False),
                                              (("lstm", "wgan_gp"), 24, 32, 256 * 32 + 70, False),
-                                             (("lstm", "wgan_gp"), 168, 36, 40, True)])
+                                             (("lstm", "wgan_gp"), 168, 36, 40, True),
+                                             (("lstm_ln", "wgan_gp"), 24, 32, 64, False)])
 def test_trainer_gradients_bf16_fused(cuda, key, T, F, B, lrelu):
     """bf16 training step (fused LSTM kernels) vs the fp64 CPU engine: norm-relative error of the
     whole gradient and of every parameter block.  Cases: the bench shape at small B, a multi-pass
@@ -696,3 +737,17 @@ def test_lstmf_wgrad_fused(cuda, B, T, K, tangent):
     _close(gW, rW, torch.float32, scale=sW)
     _close(gU, rU, torch.float32, scale=sU)
     _close(gb, rb, torch.float32, scale=D.abs().sum(0).max().item())
+
+
+def test_gan_eval_device_path(cuda):
+    """GANEval(..., device='cuda'): FID covariances through the native wgrad kernel and the MMD
+    sample means on the GPU agree with the fp64 CPU reference path."""
+    from hfrep.eval.gan_eval import GANEval
+
+    rs = np.random.RandomState(3)
+    real, fake = rs.rand(4000, 24, 32), rs.rand(4000, 24, 32) * 0.9 + 0.05
+    cpu = GANEval(real, fake, real, ["f"], ["m"])
+    gpu = GANEval(real, fake, real, ["f"], ["m"], device=cuda)
+    for name in ("FID", "linear_MMD", "gaussian_MMD", "poly_MMD"):
+        a, b = getattr(gpu, name)(), getattr(cpu, name)()
+        assert abs(a - b) <= 1e-4 * max(abs(b), 1e-3), (name, a, b)
