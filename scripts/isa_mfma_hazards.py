@@ -122,3 +122,30 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def war_census(code, labels, horizon=24):
+    """MFMA source operands (A, B and a SrcC that is not the destination) overwritten soon after
+    the MFMA by a non-MFMA instruction: {(opcode of writer, operand kind): [wait states]}."""
+    out = defaultdict(list)
+    for i, (op, ops, text) in enumerate(code):
+        if not op.startswith("v_mfma") or len(ops) < 4:
+            continue
+        srcs = {"A": regs(ops[1]), "B": regs(ops[2]), "C": regs(ops[3]) - regs(ops[0])}
+        j, ws = i + 1, 0
+        while j < len(code) and ws <= horizon:
+            opj, opsj, tj = code[j]
+            if opj == "s_nop":
+                ws += int(opsj[0], 0) + 1
+                j += 1
+                continue
+            if opj.startswith(("s_branch", "s_cbranch", "s_endpgm")):
+                break
+            if opsj and not opj.startswith(("v_mfma", "buffer_store", "ds_write", "global_store", "s_")):
+                w = regs(opsj[0])
+                for kind, rs in srcs.items():
+                    if rs and w & rs:
+                        out[(opj, kind)].append((ws, i, j))
+            ws += 1
+            j += 1
+    return out
