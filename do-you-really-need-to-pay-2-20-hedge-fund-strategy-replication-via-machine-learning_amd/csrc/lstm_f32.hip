@@ -31,7 +31,9 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
 #include <mutex>
+#include <type_traits>
 #include <set>
 
 namespace hfrep {
@@ -552,6 +554,177 @@ lstmf_bwd_kernel(const float* __restrict__ dH, const float* __restrict__ tape, c
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// BPTT with a role split and a row-half pipeline (8 waves, two per SIMD).
+//
+// lstmf_bwd_kernel runs the step's MFMA phase (dh_rec = dz_{t+1} U^T) and its VALU phase (the cell
+// adjoints) back to back in the same four waves, so the matrix pipe idles through every VALU phase:
+// 400 MFMAs = 12.8 k cycles of pipe time per wave and step against ~24 k measured.  A single wave
+// cannot overlap them (in-order issue; the scheduler keeps the cell math in clumps between MFMA
+// runs), so here the roles go to different waves that share a SIMD:
+//   * waves 0..3 (MFMA role): U^T fragments in AGPRs (the same 2 column tiles per wave as before)
+//     and nothing else; A(m, t) = rows m of dh_rec(t) -> the dh tile;
+//   * waves 4..7 (cell role): the cell state, tape loads and dZ stores of units 28 w' .. 28 w' + 27;
+//     B(m, t) = the cell adjoints of rows m, which overwrite rows m of the dz tile with dz_t.
+// The two 16-row halves of a tile are independent recurrences (the A operand of row r is
+// dz_{t+1}[r]), so one role works on one half while the other role works on the other half:
+//   P1(t): B(0, t) || A(1, t)      P2(t): B(1, t) || A(0, t - 1)
+// with one barrier after each.  The hardware interleaves the two waves of a SIMD, so the cell math
+// issues while the matrix pipe runs.  Register budget: the MFMA role ~230 (200 AGPRs of U^T), the
+// cell role ~150, two waves per SIMD.  dZ rows of a half leave during the half-phase after the one
+// that completed them (the tile rows are stable for exactly that phase).  The dz / dh tiles start at
+// zero (dz_T = 0, dh_rec(T - 1) = 0), so the first P1 and the last P2 need no special case
+// (A(0, -1) is computed into dh rows 0 and never read).
+template <int ACT>
+__global__ void __launch_bounds__(512, 1)
+lstmf_bwdp_kernel(const float* __restrict__ dH, const float* __restrict__ tape, const float* __restrict__ U,
+                  float* __restrict__ dZ, int B, int Tn) {
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  float* zt = fsm;                  // dz tile [32][BZ_LR]: [q][u'] per row
+  float* ht = zt + 32 * BZ_LR;      // dh_rec tile [32][BH_LR]
+  float* trash = ht + 32 * BH_LR;   // [4 * BZ_KQ] written by padding cells, never read
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = wv & 3;             // wave index within the role
+  const int q = lane & 3, g = lane >> 4, j4 = (lane & 15) >> 2, c16 = lane & 15;
+  const int nrb = (B + 31) / 32;
+  if (wv < 4) {
+    // ---------------- MFMA role ----------------
+    float ut[2][FH];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int j = 16 * (2 * w + e) + c16;
+      const bool ok = j < FH;
+#pragma unroll
+      for (int k = 0; k < FH; ++k) {
+        const float v = U[(ok ? j : 0) * FG + g * FH + k];
+        ut[e][k] = ok ? v : 0.f;  // (arch VGPRs: at two waves per SIMD the role fits in 256)
+      }
+    }
+    // rows of half M of dh_rec = dz[rows M] U^T -> the dh tile
+    auto half_a = [&](auto MA_) {
+      constexpr int M = decltype(MA_)::value;
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      const float* ar = zt + (16 * M + c16) * BZ_LR + g * BZ_KQ;
+#pragma unroll
+      for (int jj = 0; jj < FH / 4; ++jj) {
+        const f32x4 a4 = *reinterpret_cast<const f32x4*>(ar + 4 * jj);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          acc[0] = mma4(a4[s], ut[0][4 * jj + s], acc[0]);
+          acc[1] = mma4(a4[s], ut[1][4 * jj + s], acc[1]);
+        }
+        if ((jj & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int col = 16 * (2 * w + e) + c16;
+        if (2 * w + e < 7) {  // (wave 3's second tile is past the 112-unit tile: uniform skip)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ht[(16 * M + 4 * g + i) * BH_LR + col] = acc[e][i];
+        }
+      }
+    };
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      for (int i = tid; i < 32 * BZ_LR; i += 512) zt[i] = 0.f;  // dz_T = 0
+      for (int i = tid; i < 32 * BH_LR; i += 512) ht[i] = 0.f;  // dh_rec(T - 1) = 0
+      __syncthreads();
+      for (int t = Tn - 1; t >= 0; --t) {
+        half_a(std::integral_constant<int, 1>{});  // P1(t): A(1, t)
+        lds_barrier();
+        half_a(std::integral_constant<int, 0>{});  // P2(t): A(0, t - 1)
+        lds_barrier();
+      }
+      __syncthreads();
+    }
+  } else {
+    // ---------------- cell role ----------------
+    const int ct = tid - 256;
+    const int ub = FUW * w + j4;
+    const int hr = (4 * g + q) * BH_LR + ub, zw = (4 * g + q) * BZ_LR + ub;
+    // dZ store share: threads 0..199 of the role own chunk ct % 100 of rows 2 k + ct / 100 (k < 16)
+    const int srr = ct / 100, sch = ct - 100 * srr, sqq = sch / 25, sc = sch - 25 * sqq;
+    const int slo = (srr & 1) * BZ_LR + sqq * BZ_KQ + 4 * sc;
+    const int sgo = ct < 200 ? (srr * Tn * FG + sqq * FH + 4 * sc) * 4 : kOOB;
+    const int tl = ftape_lane(w, lane), tcl = ftape_cell(w, lane);
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      const int row0 = rb * 32;
+      const rsrc_t rdh = ftile_rsrc(dH, row0, B, Tn, FH), rt = ftape_rsrc(tape, rb, nrb, Tn);
+      const rsrc_t rz = ftile_rsrc(dZ, row0, B, Tn, FG);
+      const int nr = min(32, B - row0);
+      int vp1[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) vp1[m] = ((16 * m + 4 * g + q) * Tn * FH + ub) * 4;
+      float dc[2][FNT], tc[2][FNT];
+      f32x4 tg[2][FNT];
+      float tcp[2][FNT], tdh[2][FNT];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < FNT; ++n) {
+          const bool tok = !(w == 3 && n >= 4);
+          const int T1 = Tn - 1;
+          dc[m][n] = 0.f;
+          tc[m][n] = ld1(rt, tok ? tcl + T1 * FT_STEP * 4 + ftape_slot(m, n) : kOOB, 0);  // c_{T-1}
+          bwdf_tape_load(tg[m][n], tcp[m][n], tdh[m][n], rt, rdh, tl + T1 * FT_STEP * 4 + ftape_slot(m, n),
+                         tcl + (T1 - 1) * FT_STEP * 4 + ftape_slot(m, n), vp1[m] + T1 * FH * 4 + 16 * n, tok, T1 > 0);
+        }
+      for (int i = tid; i < 32 * BZ_LR; i += 512) zt[i] = 0.f;
+      for (int i = tid; i < 32 * BH_LR; i += 512) ht[i] = 0.f;
+      __syncthreads();
+      // rows of half M of the dz tile (dz at step ts) -> dZ[:, ts, :]
+      auto store_half = [&](auto M_, int ts) {
+        constexpr int M = decltype(M_)::value;
+#pragma unroll
+        for (int k = 8 * M; k < 8 * M + 8; ++k) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(zt + slo + 2 * k * BZ_LR);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rz, 2 * k + srr < nr ? sgo : kOOB,
+                                                 (2 * k * Tn + ts) * FG * 4, 0);
+        }
+      };
+      // cell adjoints of row half M at step t; each cell then issues step t - 1's tape loads
+      auto half_b = [&](auto M_, int t) {
+        constexpr int m = decltype(M_)::value;
+#pragma unroll
+        for (int n = 0; n < FNT; ++n) {
+          const bool tok = !(w == 3 && n >= 4);
+          const float ig = tg[m][n][0], fg = tg[m][n][1], gg = tg[m][n][2], og = tg[m][n][3];
+          const float dht = tdh[m][n] + ht[hr + 16 * m * BH_LR + 4 * n];
+          const float ca = act_f(ACT, tc[m][n]);
+          const float dov = dht * ca;
+          const float dct = dc[m][n] + dht * og * act_dy(ACT, ca);
+          dc[m][n] = tok ? dct * fg : 0.f;
+          float z4[4];
+          z4[0] = dct * gg * ig * (1.f - ig);
+          z4[1] = dct * tcp[m][n] * fg * (1.f - fg);
+          z4[2] = dct * ig * act_dy(ACT, gg);
+          z4[3] = dov * og * (1.f - og);
+          float* zd = tok ? zt + zw + 16 * m * BZ_LR + 4 * n : trash;  // padding cells: trash row
+#pragma unroll
+          for (int k = 0; k < 4; ++k) zd[k * BZ_KQ] = z4[k];
+          tc[m][n] = tcp[m][n];  // c_{t-1} is the next step's c
+          const int tp = t > 0 ? t - 1 : 0;
+          bwdf_tape_load(tg[m][n], tcp[m][n], tdh[m][n], rt, rdh, tl + tp * FT_STEP * 4 + ftape_slot(m, n),
+                         tcl + (tp - 1) * FT_STEP * 4 + ftape_slot(m, n), vp1[m] + tp * FH * 4 + 16 * n,
+                         tok && t > 0, tp > 0);
+        }
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      for (int t = Tn - 1; t >= 0; --t) {
+        if (t < Tn - 1) store_half(I1{}, t + 1);  // rows 16..31 of dz_{t+1}: stable until P2(t)
+        half_b(I0{}, t);                          // P1(t): B(0, t)
+        lds_barrier();
+        store_half(I0{}, t);                      // rows 0..15 of dz_t: stable until P1(t - 1)
+        half_b(I1{}, t);                          // P2(t): B(1, t)
+        lds_barrier();
+      }
+      store_half(I1{}, 0);
+      __syncthreads();  // (the tiles are re-zeroed for the next row block)
+    }
+  }
+}
+
 // ==========================================================================================
 // tangent reverse (fp32): (dZ, dZdot) of the reverse-over-tangent pass (ops/reference.py
 // lstm_seq_tbwd) from the primal and tangent tapes of lstmf_fwd<TAPE> / lstmf_fwd<TAN>
@@ -931,11 +1104,16 @@ bool launch_lstmf_tfwd(const float* xd, const float* W, const float* U, const fl
 
 template <int ACT>
 void bwdf_launch(const float* dH, const float* tape, const float* U, float* dZ, int B, int Tn, hipStream_t s) {
-  auto k = lstmf_bwd_kernel<ACT>;
+  // HFREP_LSTMF_BWD=1: the unpipelined two-phase kernel (A / B comparison); default: row-half pipelined
+  static const int ver = [] {
+    const char* e = getenv("HFREP_LSTMF_BWD");
+    return e ? atoi(e) : 2;
+  }();
+  auto k = ver == 1 ? lstmf_bwd_kernel<ACT> : lstmf_bwdp_kernel<ACT>;
   allow_lds(reinterpret_cast<const void*>(k));
   const int nrb = (B + 31) / 32, cus = device_cu_count();
-  const size_t sm = (size_t)(32 * BZ_LR + 32 * BH_LR) * 4;
-  hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(256), sm, s, dH, tape, U, dZ, B, Tn);
+  const size_t sm = (size_t)(32 * BZ_LR + 32 * BH_LR + 4 * BZ_KQ) * 4;
+  hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(ver == 1 ? 256 : 512), sm, s, dH, tape, U, dZ, B, Tn);
 }
 bool launch_lstmf_bwd(const float* dH, const float* tape, const float* U, float* dZ, int B, int Tn, int H, int act,
                       hipStream_t s) {
