@@ -90,11 +90,17 @@ class _LegacyGAN:
     build_discriminator = build_critic
 
     def train(self, epochs, batch_size=128, sample_interval=50, save_dir: str | None = "./trained_generator",
-              verbose: bool = True, log_every: int = 1):
+              verbose: bool = True, log_every: int = 1, graph: bool | None = None):
+        """The reference ``train``; on a GPU the step replays from a hipGraph unless ``graph=False``
+        or HFREP_GRAPH=0 (at the reference's batch 32 the step is launch-bound: graph replay is what
+        makes it fast, profiles/r01_parity)."""
         if batch_size != self._trainer.cfg.batch_size:
             self._make(batch_size)
         self._trainer.cfg.log_every = log_every
-        hist = self._trainer.train(epochs, verbose=verbose)
+        if graph is None:
+            graph = (self.device.type == "cuda" and os.environ.get("HFREP_GRAPH", "1") != "0"
+                     and self._trainer.rng.native)
+        hist = self._trainer.train(epochs, verbose=verbose, graph=graph)
         self.history = hist
         if save_dir:
             os.makedirs(save_dir, exist_ok=True)
@@ -143,8 +149,10 @@ def script_main(cls, epochs: int = 5000, batch_size: int = 32):
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--save-dir", default="./trained_generator")
     ap.add_argument("--log-every", type=int, default=100)
+    ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay (GPU)")
     a = ap.parse_args()
     ds = reference_dataset()
     model = cls(ds, dtype=a.dtype)
-    model.train(epochs=a.epochs, batch_size=a.batch_size, save_dir=a.save_dir, log_every=a.log_every)
+    model.train(epochs=a.epochs, batch_size=a.batch_size, save_dir=a.save_dir, log_every=a.log_every,
+                graph=False if a.no_graph else None)
     print(f"saved {model.saved_path}")

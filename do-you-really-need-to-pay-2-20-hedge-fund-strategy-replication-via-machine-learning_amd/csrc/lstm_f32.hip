@@ -888,6 +888,210 @@ lstmf_tbwd_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, c
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// tangent reverse with the role split of lstmf_bwdp_kernel: 32-row tiles whose 16-row halves are
+// pipelined (P1(t): cells of rows 0-15 || MFMAs of rows 16-31; P2(t): cells of rows 16-31 ||
+// MFMAs of rows 0-15 of the previous step), MFMA waves 0..3 (U^T in VGPRs, both adjoint streams:
+// 400 MFMAs per half-phase) and cell waves 4..7.  The cell waves carry 4 values per cell for both
+// halves (c, cdot and the two adjoint carries) and ONE set of step loads (gates, zdot, c_{t-1},
+// cdot_{t-1}, dH, dHd: 12 per cell): the set for the other half is issued right after a half's
+// cells, and lands while the MFMA waves finish the half-phase.
+template <int ACT>
+__global__ void __launch_bounds__(512, 1)
+lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, const float* __restrict__ tape,
+                   const float* __restrict__ ttape, const float* __restrict__ U, float* __restrict__ dZ,
+                   float* __restrict__ dZd, int B, int Tn) {
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  float* zt = fsm;                   // dz tile     [32][BZ_LR]
+  float* zdt = zt + 32 * BZ_LR;      // dzdot tile  [32][BZ_LR]
+  float* ht = zdt + 32 * BZ_LR;      // dz U^T      [32][BH_LR]
+  float* hdt = ht + 32 * BH_LR;      // dzdot U^T   [32][BH_LR]
+  float* trash = hdt + 32 * BH_LR;   // [4 * BZ_KQ] padding-cell writes
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = wv & 3;
+  const int q = lane & 3, g = lane >> 4, j4 = (lane & 15) >> 2, c16 = lane & 15;
+  const int nrb = (B + 31) / 32;
+  if (wv < 4) {
+    // ---------------- MFMA role ----------------
+    float ut[2][FH];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int j = 16 * (2 * w + e) + c16;
+      const bool ok = j < FH;
+#pragma unroll
+      for (int k = 0; k < FH; ++k) {
+        const float v = U[(ok ? j : 0) * FG + g * FH + k];
+        ut[e][k] = ok ? v : 0.f;
+      }
+    }
+    // rows of half M of (dz, dzdot) U^T, one adjoint stream after the other (8 accumulator
+    // registers live: U^T takes 200 of the role's 256 VGPRs)
+    auto half_a = [&](auto MA_) {
+      constexpr int M = decltype(MA_)::value;
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        const float* ar = (st ? zdt : zt) + (16 * M + c16) * BZ_LR + g * BZ_KQ;
+#pragma unroll
+        for (int jj = 0; jj < FH / 4; ++jj) {
+          const f32x4 a4 = *reinterpret_cast<const f32x4*>(ar + 4 * jj);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            acc[0] = mma4(a4[s], ut[0][4 * jj + s], acc[0]);
+            acc[1] = mma4(a4[s], ut[1][4 * jj + s], acc[1]);
+          }
+          if ((jj & 1) == 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        float* hd = st ? hdt : ht;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int col = 16 * (2 * w + e) + c16;
+          if (2 * w + e < 7) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) hd[(16 * M + 4 * g + i) * BH_LR + col] = acc[e][i];
+          }
+        }
+      }
+    };
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      for (int i = tid; i < 2 * 32 * (BZ_LR + BH_LR); i += 512) zt[i] = 0.f;  // all four tiles
+      __syncthreads();
+      for (int t = Tn - 1; t >= 0; --t) {
+        half_a(std::integral_constant<int, 1>{});
+        lds_barrier();
+        half_a(std::integral_constant<int, 0>{});
+        lds_barrier();
+      }
+      __syncthreads();
+    }
+  } else {
+    // ---------------- cell role ----------------
+    const int ct = tid - 256;
+    const int ub = FUW * w + j4;
+    const int hr = (4 * g + q) * BH_LR + ub, zw = (4 * g + q) * BZ_LR + ub;
+    const int srr = ct / 100, sch = ct - 100 * srr, sqq = sch / 25, sc = sch - 25 * sqq;
+    const int slo = (srr & 1) * BZ_LR + sqq * BZ_KQ + 4 * sc;
+    const int sgo = ct < 200 ? (srr * Tn * FG + sqq * FH + 4 * sc) * 4 : kOOB;
+    const int tl = ftape_lane(w, lane), tcl = ftape_cell(w, lane);
+    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      const int row0 = rb * 32;
+      const rsrc_t rdh = ftile_rsrc(dH, row0, B, Tn, FH), rdhd = ftile_rsrc(dHd, row0, B, Tn, FH);
+      const rsrc_t rt = ftape_rsrc(tape, rb, nrb, Tn), rtt = ftape_rsrc(ttape, rb, nrb, Tn);
+      const rsrc_t rz = ftile_rsrc(dZ, row0, B, Tn, FG), rzd = ftile_rsrc(dZd, row0, B, Tn, FG);
+      const int nr = min(32, B - row0);
+      int vp1[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) vp1[m] = ((16 * m + 4 * g + q) * Tn * FH + ub) * 4;
+      float tc[2][FNT], tcd[2][FNT], acn[2][FNT], acdn[2][FNT];
+      f32x4 tg[FNT], tz[FNT];
+      float tcp[FNT], tcdp[FNT], tdh[FNT], tdhd[FNT];
+      // the step loads of half M at step tt (one register set, reused by the two halves in turn)
+      auto load_half = [&](auto M_, int tt, bool on) {
+        constexpr int m = decltype(M_)::value;
+#pragma unroll
+        for (int n = 0; n < FNT; ++n) {
+          const bool tok = on && !(w == 3 && n >= 4);
+          const int og = tl + tt * FT_STEP * 4 + ftape_slot(m, n), ocp = tcl + (tt - 1) * FT_STEP * 4 + ftape_slot(m, n);
+          tg[n] = ld4(rt, tok ? og : kOOB);
+          tz[n] = ld4(rtt, tok ? og : kOOB);
+          tcp[n] = ld1(rt, (tok && tt > 0) ? ocp : kOOB, 0);
+          tcdp[n] = ld1(rtt, (tok && tt > 0) ? ocp : kOOB, 0);
+          tdh[n] = ld1(rdh, tok ? vp1[m] + tt * FH * 4 + 16 * n : kOOB, 0);
+          tdhd[n] = ld1(rdhd, tok ? vp1[m] + tt * FH * 4 + 16 * n : kOOB, 0);
+        }
+      };
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < FNT; ++n) {
+          const bool tok = !(w == 3 && n >= 4);
+          const int oc = tcl + (Tn - 1) * FT_STEP * 4 + ftape_slot(m, n);
+          acn[m][n] = 0.f;
+          acdn[m][n] = 0.f;
+          tc[m][n] = ld1(rt, tok ? oc : kOOB, 0);
+          tcd[m][n] = ld1(rtt, tok ? oc : kOOB, 0);
+        }
+      load_half(std::integral_constant<int, 0>{}, Tn - 1, true);
+      for (int i = tid; i < 2 * 32 * (BZ_LR + BH_LR); i += 512) zt[i] = 0.f;
+      __syncthreads();
+      auto store_half = [&](auto M_, int ts) {
+        constexpr int M = decltype(M_)::value;
+#pragma unroll
+        for (int k = 8 * M; k < 8 * M + 8; ++k) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(zt + slo + 2 * k * BZ_LR);
+          const f32x4 vd = *reinterpret_cast<const f32x4*>(zdt + slo + 2 * k * BZ_LR);
+          const int go = 2 * k + srr < nr ? sgo : kOOB, so = (2 * k * Tn + ts) * FG * 4;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rz, go, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, vd), rzd, go, so, 0);
+          if (k & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      auto half_b = [&](auto M_) {
+        constexpr int m = decltype(M_)::value;
+#pragma unroll
+        for (int n = 0; n < FNT; ++n) {
+          const bool tok = !(w == 3 && n >= 4);
+          const float i_ = tg[n][0], f_ = tg[n][1], g_ = tg[n][2], o_ = tg[n][3];
+          const float zdi = tz[n][0], zdf = tz[n][1], zdg = tz[n][2], zdo = tz[n][3];
+          const float c = tc[m][n], cd = tcd[m][n], cp = tcp[n], cdp = tcdp[n];
+          const float si = i_ * (1.f - i_), sf = f_ * (1.f - f_), so = o_ * (1.f - o_), sg = act_dy(ACT, g_);
+          const float idot = si * zdi, fdot = sf * zdf, gdot = sg * zdg, odot = so * zdo;
+          const float ca = act_f(ACT, c), d1 = act_dy(ACT, ca), d2 = act_d2y(ACT, ca);
+          const int hi = hr + 16 * m * BH_LR + 4 * n;
+          const float a_h = tdh[n] + ht[hi], a_hd = tdhd[n] + hdt[hi];
+          const float a_od = a_hd * ca;
+          const float a_o = a_h * ca + a_hd * d1 * cd;
+          const float a_cd = acdn[m][n] + a_hd * o_ * d1;
+          const float a_c = acn[m][n] + a_h * o_ * d1 + a_hd * (odot * d1 + o_ * d2 * cd);
+          const float a_fd = a_cd * cp, a_id = a_cd * g_, a_gd = a_cd * i_;
+          const float a_f = a_c * cp + a_cd * cdp;
+          const float a_i = a_c * g_ + a_cd * gdot;
+          const float a_g = a_c * i_ + a_cd * idot;
+          acn[m][n] = tok ? a_c * f_ + a_cd * fdot : 0.f;
+          acdn[m][n] = tok ? a_cd * f_ : 0.f;
+          const float s2i = si * (1.f - 2.f * i_), s2f = sf * (1.f - 2.f * f_), s2o = so * (1.f - 2.f * o_);
+          const float s2g = act_d2y(ACT, g_);
+          float zd4[4], z4[4];
+          zd4[0] = a_id * si; zd4[1] = a_fd * sf; zd4[2] = a_gd * sg; zd4[3] = a_od * so;
+          z4[0] = a_i * si + a_id * s2i * zdi;
+          z4[1] = a_f * sf + a_fd * s2f * zdf;
+          z4[2] = a_g * sg + a_gd * s2g * zdg;
+          z4[3] = a_o * so + a_od * s2o * zdo;
+          const int zo = zw + 16 * m * BZ_LR + 4 * n;
+          float* zp = tok ? zt + zo : trash;
+          float* zdp = tok ? zdt + zo : trash;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            zp[k * BZ_KQ] = z4[k];
+            zdp[k * BZ_KQ] = zd4[k];
+          }
+          tc[m][n] = cp;
+          tcd[m][n] = cdp;
+          __builtin_amdgcn_sched_barrier(0);  // one cell's temporaries at a time
+        }
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      for (int t = Tn - 1; t >= 0; --t) {
+        if (t < Tn - 1) store_half(I1{}, t + 1);
+        half_b(I0{});                             // P1(t): B(0, t)
+        __builtin_amdgcn_sched_barrier(0);        //   (the load set is free only after the cells)
+        load_half(I1{}, t, true);                 //   then half 1's loads for P2(t)
+        lds_barrier();
+        store_half(I0{}, t);
+        half_b(I1{});                             // P2(t): B(1, t)
+        __builtin_amdgcn_sched_barrier(0);
+        load_half(I0{}, t > 0 ? t - 1 : 0, t > 0);  //   then half 0's loads for P1(t - 1)
+        lds_barrier();
+      }
+      store_half(I1{}, 0);
+      __syncthreads();
+    }
+  }
+}
+
 // ==========================================================================================
 // fused fp32 LSTM weight gradients
 // ==========================================================================================
@@ -1129,12 +1333,25 @@ bool launch_lstmf_bwd(const float* dH, const float* tape, const float* U, float*
 template <int ACT>
 void tbwdf_launch(const float* dH, const float* dHd, const float* tape, const float* ttape, const float* U, float* dZ,
                   float* dZd, int B, int Tn, hipStream_t s) {
-  auto k = lstmf_tbwd_kernel<ACT>;
-  allow_lds(reinterpret_cast<const void*>(k));
+  // HFREP_LSTMF_TBWD=1: the 16-row two-phase kernel (A / B comparison); default: role split
+  static const int ver = [] {
+    const char* e = getenv("HFREP_LSTMF_TBWD");
+    return e ? atoi(e) : 2;
+  }();
   const int cus = device_cu_count();
-  const size_t sm = (size_t)(2 * 16 * BZ_LR + 2 * 16 * BH_LR) * 4;
-  const int nt16 = (B + 15) / 16;
-  hipLaunchKernelGGL(k, dim3(nt16 < cus ? nt16 : cus), dim3(256), sm, s, dH, dHd, tape, ttape, U, dZ, dZd, B, Tn);
+  if (ver == 1) {
+    auto k = lstmf_tbwd_kernel<ACT>;
+    allow_lds(reinterpret_cast<const void*>(k));
+    const size_t sm = (size_t)(2 * 16 * BZ_LR + 2 * 16 * BH_LR) * 4;
+    const int nt16 = (B + 15) / 16;
+    hipLaunchKernelGGL(k, dim3(nt16 < cus ? nt16 : cus), dim3(256), sm, s, dH, dHd, tape, ttape, U, dZ, dZd, B, Tn);
+    return;
+  }
+  auto k = lstmf_tbwdp_kernel<ACT>;
+  allow_lds(reinterpret_cast<const void*>(k));
+  const size_t sm = (size_t)(2 * 32 * BZ_LR + 2 * 32 * BH_LR + 4 * BZ_KQ) * 4;
+  const int nrb = (B + 31) / 32;
+  hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(512), sm, s, dH, dHd, tape, ttape, U, dZ, dZd, B, Tn);
 }
 bool launch_lstmf_tbwd(const float* dH, const float* dHd, const float* tape, const float* ttape, const float* U, float* dZ,
                        float* dZd, int B, int Tn, int H, int act, hipStream_t s) {

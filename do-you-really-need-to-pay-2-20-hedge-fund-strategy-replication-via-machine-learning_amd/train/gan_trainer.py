@@ -248,12 +248,19 @@ class GANTrainer:
         nc = 2 if self.cfg.loss == "gan" else self.n_critic
         return nc * B + B
 
-    def train(self, epochs: int | None = None, log=None, verbose: bool = True):
+    def train(self, epochs: int | None = None, log=None, verbose: bool = True, graph: bool = False):
+        """``epochs`` reference iterations.  ``graph=True`` replays the step from a captured hipGraph
+        after two eager warmup steps (train/runner.py GraphedStep: bitwise identical to eager)."""
         epochs = self.cfg.epochs if epochs is None else epochs
         t0 = time.time()
         hist = []
+        step = self.train_step
+        if graph:
+            from .runner import GraphedStep
+
+            step = GraphedStep(self)
         for ep in range(epochs):
-            self.train_step()
+            step()
             if (ep + 1) % self.cfg.log_every == 0 or ep == epochs - 1:
                 rec = self.losses()
                 rec["elapsed_s"] = time.time() - t0

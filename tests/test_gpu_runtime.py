@@ -135,3 +135,19 @@ def test_poisoned_outputs_all_written(cuda, key, dtype):
             assert bool(torch.isfinite(m.flat).all()), m.model_name
     finally:
         ops.set_debug_poison(prev)
+
+
+def test_legacy_script_train_uses_graph(cuda, tmp_path):
+    """The reference entry point (GAN/MTSS_WGAN_GP.py -> compat.legacy_gan WGAN_GP.train) replays
+    the step from a hipGraph on the GPU; the result is bitwise the eager run's."""
+    from hfrep.compat.legacy_gan import WGAN_GP
+
+    ds = np.random.RandomState(0).rand(64, 12, 8).astype(np.float32)
+    a, b = WGAN_GP(ds, device=cuda), WGAN_GP(ds, device=cuda)
+    with torch.no_grad():
+        b.generator.flat.copy_(a.generator.flat)
+        b.critic.flat.copy_(a.critic.flat)
+    ha = a.train(epochs=6, batch_size=16, save_dir=None, verbose=False, log_every=3)
+    hb = b.train(epochs=6, batch_size=16, save_dir=None, verbose=False, log_every=3, graph=False)
+    assert torch.equal(a.generator.flat, b.generator.flat) and torch.equal(a.critic.flat, b.critic.flat)
+    assert [r["d_loss"] for r in ha] == [r["d_loss"] for r in hb]
