@@ -604,6 +604,14 @@ def test_lstm2_head_adjoint_in_kernel(cuda):
             # bf16 differences that the recurrence carries back, so compare at bf16 tolerance)
             for a, c in zip(t1, t2):
                 _close(a, c.double(), torch.bfloat16)
+    # the native op itself can never reach the DX + generated-head instantiation: with W it
+    # materialises the head adjoint (bindings.cpp lstm2_tbwd) -> bitwise the tensor-fed launch
+    ops = _ops()
+    o1 = ops.lstm2_tbwd(None, None, tape, ttape, U, act, W, d, dd, w.reshape(-1))
+    o2 = ops.lstm2_tbwd(dHm, dHdm, tape, ttape, U, act, W)
+    assert all(torch.equal(a, c) for a, c in zip(o1, o2))
+    o3 = ops.lstm2_tbwd(None, None, tape, ttape, U, act, W, d, dd, w.reshape(-1))
+    assert all(torch.equal(a, c) for a, c in zip(o1, o3))
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
