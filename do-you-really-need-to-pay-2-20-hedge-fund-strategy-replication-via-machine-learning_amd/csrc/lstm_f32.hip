@@ -986,19 +986,24 @@ lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, 
       float tc[2][FNT], tcd[2][FNT], acn[2][FNT], acdn[2][FNT];
       f32x4 tg[FNT], tz[FNT];
       float tcp[FNT], tcdp[FNT], tdh[FNT], tdhd[FNT];
-      // the step loads of half M at step tt (one register set, reused by the two halves in turn)
+      // the step loads of half M at step tt (one register set, reused by the two halves in turn).
+      // The per-lane part of every address is one of four VGPRs (tl, tcl, vp1[m]); the cell's slot
+      // and the step go into the uniform soffset, so no per-cell offset registers are hoisted
+      // (out-of-range lanes: voffset kOOB, which the range check drops whatever the soffset)
       auto load_half = [&](auto M_, int tt, bool on) {
         constexpr int m = decltype(M_)::value;
+        const int tp = tt > 0 ? tt - 1 : 0;
 #pragma unroll
         for (int n = 0; n < FNT; ++n) {
           const bool tok = on && !(w == 3 && n >= 4);
-          const int og = tl + tt * FT_STEP * 4 + ftape_slot(m, n), ocp = tcl + (tt - 1) * FT_STEP * 4 + ftape_slot(m, n);
-          tg[n] = ld4(rt, tok ? og : kOOB);
-          tz[n] = ld4(rtt, tok ? og : kOOB);
-          tcp[n] = ld1(rt, (tok && tt > 0) ? ocp : kOOB, 0);
-          tcdp[n] = ld1(rtt, (tok && tt > 0) ? ocp : kOOB, 0);
-          tdh[n] = ld1(rdh, tok ? vp1[m] + tt * FH * 4 + 16 * n : kOOB, 0);
-          tdhd[n] = ld1(rdhd, tok ? vp1[m] + tt * FH * 4 + 16 * n : kOOB, 0);
+          const int sg = tt * FT_STEP * 4 + ftape_slot(m, n), sc = tp * FT_STEP * 4 + ftape_slot(m, n);
+          const int sd = tt * FH * 4 + 16 * n;
+          tg[n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rt, tok ? tl : kOOB, sg, 0));
+          tz[n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rtt, tok ? tl : kOOB, sg, 0));
+          tcp[n] = ld1(rt, (tok && tt > 0) ? tcl : kOOB, sc);
+          tcdp[n] = ld1(rtt, (tok && tt > 0) ? tcl : kOOB, sc);
+          tdh[n] = ld1(rdh, tok ? vp1[m] : kOOB, sd);
+          tdhd[n] = ld1(rdhd, tok ? vp1[m] : kOOB, sd);
         }
       };
 #pragma unroll
