@@ -23,6 +23,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -311,9 +312,11 @@ def cmd_replicate(a) -> int:
         xe = ye = None
         if a.augment:
             xe, ye = generated_augmentation(np.load(a.augment, allow_pickle=False), c)
+        t0 = time.perf_counter()
         sw = latent_sweep(c, latents=latents, window=a.window, x_extra=xe, y_extra=ye, verbose=True, device=dev,
                           dtype=dt, seed=a.seed)
         res["ae_sweep"] = {"device": str(dev), "dtype": a.dtype, "seed": a.seed, "augmented": bool(a.augment),
+                           "elapsed_s": round(time.perf_counter() - t0, 3),
                            "metrics": sw.metrics.to_dict(orient="index"),
                            "sharpe_ante": sw.sharpe_ante.to_dict(orient="index"),
                            "turnover": sw.turnover.to_dict(orient="index"),
