@@ -64,26 +64,32 @@ class AETrainer:
         hist = {"loss": [], "val_loss": []}
         best, wait = np.inf, 0
         enc, dec = self.model.parts()
+        # one host <-> device round trip per epoch: the epoch's batch order goes to the device in
+        # one copy, the loss is accumulated there (float64, batch order: the same sum as the
+        # host-side one), and the training and validation losses come back together for the
+        # EarlyStopping decision (which is per epoch in Keras too)
         for ep in range(epochs):
             order = rs.permutation(split) if shuffle else np.arange(split)
-            tot, cnt = 0.0, 0
-            losses = []
+            order_t = torch.as_tensor(order, device=self.device)
+            tot = torch.zeros((), dtype=torch.float64, device=self.device)
             for s in range(0, split, batch_size):
-                idx = torch.as_tensor(order[s:s + batch_size], device=self.device)
+                idx = order_t[s:s + batch_size]
                 xb = xt.index_select(0, idx)
                 loss = self.model.loss_and_grads(xb)
                 # Keras applies ONE optimizer step per batch to all variables (one iteration tick)
                 self.opt.apply_group([enc.flat, dec.flat])
                 enc.zero_grad()
                 dec.zero_grad()
-                losses.append((loss, len(idx)))
-            tot = sum(float(l) * c for l, c in losses)
-            cnt = sum(c for _, c in losses)
-            hist["loss"].append(tot / cnt)
+                tot = tot + loss.double() * idx.numel()
+            vl_t = None
             if xv is not None:
                 with torch.no_grad():
                     pv = self.model.predict(xv)
-                    vl = float(((pv.double() - xv.double()) ** 2).mean())
+                    vl_t = ((pv.double() - xv.double()) ** 2).mean()
+            pair = torch.stack([tot, vl_t if vl_t is not None else tot]).cpu().tolist()
+            hist["loss"].append(pair[0] / split)
+            if xv is not None:
+                vl = pair[1]
                 hist["val_loss"].append(vl)
                 if verbose:
                     print(f"epoch {ep + 1}: loss {hist['loss'][-1]:.6f} val_loss {vl:.6f}")
