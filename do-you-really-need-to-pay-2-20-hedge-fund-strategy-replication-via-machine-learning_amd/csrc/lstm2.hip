@@ -1197,7 +1197,13 @@ struct Tile8w {
 template <int H>
 struct Tb4Geo {
   // the gate axis as full 32-wide k-steps + a 16-wide tail: G = 400 -> 12 x 32 + 16, no padding
-  static constexpr int G = 4 * H, NK = KSplit<G>::NF, KP = KSplit<G>::KP, LG = KP + 8, LH = ((H + 3) / 4) * 4 + 4;
+  // dz tile row stride: the smallest LG >= KP with (LG / 2) % 64 == 8 dwords, which makes the MFMA
+  // A-operand ds_read_b128 (lane l: row l & 15, k-group l >> 4) conflict-free in all four lane
+  // groups (scripted bank model, CDNA4 b128 lane groups); KP + 8 (408 at H = 100) was 2-way
+  // conflicted in every group (~1.5 conflict cycles per LDS instruction, profiles/r01_fwd5)
+  static constexpr int lg_stride(int kp) { return kp + ((16 - kp % 128) + 128) % 128; }
+  static constexpr int G = 4 * H, NK = KSplit<G>::NF, KP = KSplit<G>::KP, LG = lg_stride(KP), LH = ((H + 3) / 4) * 4 + 4;
+  static_assert((LG / 2) % 64 == 8 && LG >= KP, "dz tile stride");
   static constexpr bool TAIL = KSplit<G>::TAIL;
   static constexpr int NCW = (H + 15) / 16;  // compute waves
   static_assert(NCW <= 7, "tbwd4: H <= 112 (7 compute waves + 1 data wave)");
