@@ -333,6 +333,20 @@ std::tuple<Tensor, Tensor> lstmf_tbwd(optional<Tensor> dH, optional<Tensor> dHd,
   return {dZ, dZd};
 }
 
+Tensor lstmf_dgrad(Tensor dz, Tensor W) {
+  CHECK_F32(dz); CHECK_F32(W);
+  TORCH_CHECK(dz.dim() == 2 && dz.is_contiguous() && W.dim() == 2 && W.is_contiguous() && W.size(1) == dz.size(1),
+              "lstmf_dgrad: dz (M, N) and W (KO, N), contiguous");
+  TORCH_CHECK(hfrep::lstmf_dgrad_supported(dz.size(1), W.size(0)), "lstmf_dgrad: N must be 400 and KO <= 112");
+  GUARD(dz);
+  Tensor x = out_empty({dz.size(0), W.size(0)}, dz.options());
+  if (dz.size(0) == 0) return x;
+  const bool ok = hfrep::launch_lstmf_dgrad(dz.data_ptr<float>(), W.data_ptr<float>(), x.data_ptr<float>(), dz.size(0),
+                                            dz.size(1), W.size(0), cur_stream(dz));
+  TORCH_CHECK(ok, "lstmf_dgrad: launch failed");
+  return x;
+}
+
 // ------------------------------------------------------------------------------------ LSTM v2 (bf16 fused)
 void check_lstm2(const Tensor& x, const Tensor& U, int64_t H) {
   TORCH_CHECK(x.scalar_type() == at::kBFloat16, "lstm2 kernels are bf16-only");
@@ -695,6 +709,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstmf_bwd(Tensor? dH, Tensor tape, Tensor U, int act, int B, int T) -> Tensor");
   m.def("lstmf_tbwd(Tensor? dH, Tensor? dHd, Tensor tape, Tensor ttape, Tensor U, int act, int B, int T) -> (Tensor, Tensor)");
   m.def("lstmf_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int act) -> (Tensor, Tensor)");
+  m.def("lstmf_dgrad(Tensor dz, Tensor W) -> Tensor");
   m.def("lstm2_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
   m.def("lstm2_bwd(Tensor? dH, Tensor tape, Tensor U, int act, Tensor? W=None, bool need_dz=True, Tensor? head_d=None, "
         "Tensor? head_w=None) -> (Tensor, Tensor)");
@@ -736,6 +751,7 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("lstmf_tfwd", &lstmf_tfwd);
   m.impl("lstmf_bwd", &lstmf_bwd);
   m.impl("lstmf_tbwd", &lstmf_tbwd);
+  m.impl("lstmf_dgrad", &lstmf_dgrad);
   m.impl("lstm_bwd", &lstm_bwd);
   m.impl("lstm_tfwd", &lstm_tfwd);
   m.impl("lstm_tbwd", &lstm_tbwd);

@@ -61,6 +61,9 @@ bool lstmf_wgrad_supported(int K, int H, int N);
 size_t lstmf_wgrad_workspace_floats(int M, int K);
 bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
                         float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s);
+// fp32 input gradient X (M, KO) = D (M, N) W^T, W (KO, N) row-major; N = 400, KO <= 112
+bool lstmf_dgrad_supported(int N, int KO);
+bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s);
 
 // ---- gemm.hip ----
 // C[M,N] = act(A[M,K] . op(W) + bias);  op(W) = W (K,N) or W^T when w_trans (W stored (N,K)).

@@ -1247,6 +1247,118 @@ lstmf_wgrad_kernel(const float* __restrict__ X, const float* __restrict__ Hs, co
 }
 
 // ==========================================================================================
+// fp32 input gradient dX = dZ W^T   (dZ: M x 400, W: KO x 400 row-major, dX: M x KO, KO <= 16 NT)
+// ==========================================================================================
+// hipBLASLt ran this product at 59 % (KO = 100) / 41 % (KO = 32) of the fp32 MFMA pipe on the
+// 6.3 M-row calls of the B = 262k step (profiles/r02_final/kernel_summary_B262144_fp32.txt,
+// MT112x256x32 / MT32x256x32), 11 % of the fp32 step.
+//
+// One persistent workgroup per CU, 4 waves (one per SIMD), each workgroup a contiguous range of
+// 16-row chunks.  Wave w owns the k-slice [100 w, 100 w + 100) of the 400-long reduction for ALL NT
+// output tiles: its W^T fragments (NT x 25 k-steps) live in registers and its A operand comes
+// straight from HBM into registers — every dZ byte is loaded once, by one lane, no LDS staging.
+// k is permuted inside the slice (k-step 4 q + j of lane group g reads k = 16 q + 4 g + j; step 24
+// reads k = 96 + g), so a lane's four consecutive k-steps are one contiguous dwordx4 (the sum over
+// k is order-free; A and B use the same map).  The four waves' partial tiles meet in LDS: chunk
+// c's accumulators (two alternating register sets) are written during chunk c + 1's MFMAs and
+// summed in fixed wave order during chunk c + 2's, so one barrier per chunk is the only stall.
+constexpr int DG_KS = 25;
+template <int NT>
+__global__ void __launch_bounds__(256, 1)
+lstmf_dgrad_kernel(const float* __restrict__ D, const float* __restrict__ W, float* __restrict__ X, int M, int KO,
+                   int rows_per_wg) {
+  __shared__ __attribute__((aligned(16))) f32x4 part[2][4][NT][64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int mb = blockIdx.x * rows_per_wg, nrows = min(M, mb + rows_per_wg) - mb;
+  if (nrows <= 0) return;  // uniform over the workgroup
+  const int kb = 100 * w;
+
+  float bw[NT][DG_KS];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int col = 16 * n + c16;
+#pragma unroll
+    for (int s = 0; s < DG_KS; ++s) {
+      const int k = s < 24 ? kb + 16 * (s >> 2) + 4 * g + (s & 3) : kb + 96 + g;
+      bw[n][s] = col < KO ? W[col * FG + k] : 0.f;
+    }
+  }
+  const rsrc_t rd = make_rsrc(D + (size_t)mb * FG, nrows * FG * 4);
+  const rsrc_t rx = make_rsrc(X + (size_t)mb * KO, nrows * KO * 4);
+  const int nch = (nrows + 15) / 16;
+
+  f32x4 a0[6], a1[6], acc0[NT], acc1[NT];
+  float s0 = 0.f, s1 = 0.f;
+  auto load = [&](f32x4 (&a)[6], float& a_s, int r0) {
+    const int vo = ((r0 + c16) * FG + kb + 4 * g) * 4;  // rows past the range read zeros
+#pragma unroll
+    for (int q = 0; q < 6; ++q) a[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, vo + 64 * q, 0, 0));
+    a_s = ld1(rd, vo + (96 - 3 * g) * 4, 0);
+  };
+  auto mm = [&](f32x4 (&acc)[NT], const f32x4 (&a)[6], int q0, int q1) {
+#pragma unroll
+    for (int q = q0; q < q1; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = mma4(a[q][j], bw[n][4 * q + j], acc[n]);
+  };
+  auto put = [&](const f32x4 (&acc)[NT], int slot) {
+#pragma unroll
+    for (int n = 0; n < NT; ++n) part[slot][w][n][lane] = acc[n];
+  };
+  // branch-free (a fixed number of stores on every path keeps the vmcnt waits of the MFMA operand
+  // loads exact); invalid lanes / chunks store to kOOB
+  auto reduce = [&](int slot, int r0, bool on) {
+#pragma unroll
+    for (int e = 0; e < (NT * 64 + 255) / 256; ++e) {
+      const int idx = tid + 256 * e, ok = on && idx < NT * 64, ix = idx < NT * 64 ? idx : 0;
+      const int n = ix >> 6, ln = ix & 63, col = 16 * n + (ln & 15), row = r0 + 4 * (ln >> 4);
+      const f32x4 v = ((part[slot][0][n][ln] + part[slot][1][n][ln]) + part[slot][2][n][ln]) + part[slot][3][n][ln];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st1(v[i], rx, ok && col < KO ? ((row + i) * KO + col) * 4 : kOOB, 0);
+    }
+  };
+  // chunk c: chunk c - 2's partials are reduced and stored FIRST (vmcnt is in order over loads and
+  // stores: stores issued after the next chunk's loads would be waited for with them), then the
+  // next chunk's A operands are loaded, then the MFMAs run into cur with chunk c - 1's
+  // accumulators (prev) written to LDS under them
+  auto chunk = [&](f32x4 (&cur)[NT], const f32x4 (&prev)[NT], const f32x4 (&a)[6], float a_s, f32x4 (&an)[6],
+                   float& an_s, int c) {
+    reduce(c & 1, 16 * (c - 2), c >= 2);
+    load(an, an_s, 16 * (c + 1));  // past the end: out of range, zeros
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs (the scheduler sinks them)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) cur[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mm(cur, a, 0, 2);
+    if (c >= 1) put(prev, (c - 1) & 1);
+    mm(cur, a, 2, 6);
+#pragma unroll
+    for (int n = 0; n < NT; ++n) cur[n] = mma4(a_s, bw[n][24], cur[n]);
+    __syncthreads();
+  };
+
+  // unrolled by two so the A-operand and accumulator sets alternate without register copies
+  load(a0, s0, 0);
+  int c = 0;
+  for (; c + 2 <= nch; c += 2) {
+    chunk(acc0, acc1, a0, s0, a1, s1, c);
+    chunk(acc1, acc0, a1, s1, a0, s0, c + 1);
+  }
+  if (c < nch) chunk(acc0, acc1, a0, s0, a1, s1, c++);
+  // drain (c == nch): the last chunk's accumulators, then the last two reductions
+  if (c & 1)
+    put(acc0, (c - 1) & 1);
+  else
+    put(acc1, (c - 1) & 1);
+  reduce(c & 1, 16 * (c - 2), c >= 2);
+  __syncthreads();
+  reduce((c - 1) & 1, 16 * (c - 1), true);
+}
+
+// ==========================================================================================
 // host side
 // ==========================================================================================
 namespace {
@@ -1389,6 +1501,30 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
     default: hipLaunchKernelGGL(lstmf_wgrad_kernel<100>, dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
   }
   launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s);
+  return true;
+}
+
+bool lstmf_dgrad_supported(int N, int KO) { return N == FG && KO >= 1 && KO <= 16 * FNT; }
+
+bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s) {
+  if (!lstmf_dgrad_supported(N, KO) || M <= 0) return false;
+  // one workgroup per CU (two for NT <= 3: HBM-bound there, and the registers allow a second one
+  // in flight); more only if a workgroup's dZ range would pass 2 GB (32-bit buffer offsets)
+  const int chunks = (M + 15) / 16, cus = device_cu_count() * (KO <= 48 ? 2 : 1);
+  int grid = chunks < cus ? chunks : cus;
+  const int min_grid = (int)(((long long)M * FG * 4 + (1ll << 31) - 1) / (1ll << 31));
+  if (grid < min_grid) grid = min_grid;
+  const int rpw = (chunks + grid - 1) / grid * 16;
+  const int z = (M + rpw - 1) / rpw;
+  switch ((KO + 15) / 16) {
+    case 1: hipLaunchKernelGGL(lstmf_dgrad_kernel<1>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
+    case 2: hipLaunchKernelGGL(lstmf_dgrad_kernel<2>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
+    case 3: hipLaunchKernelGGL(lstmf_dgrad_kernel<3>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
+    case 4: hipLaunchKernelGGL(lstmf_dgrad_kernel<4>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
+    case 5: hipLaunchKernelGGL(lstmf_dgrad_kernel<5>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
+    case 6: hipLaunchKernelGGL(lstmf_dgrad_kernel<6>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
+    default: hipLaunchKernelGGL(lstmf_dgrad_kernel<7>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
+  }
   return true;
 }
 

@@ -59,8 +59,16 @@ def linear(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: int) -
     return R.apply_act(y, act)
 
 
+# fp32 dZ (.., 400) @ W^T with W (K <= 112, 400): the LSTM layers' input gradient, on the
+# register-resident k-split kernel of csrc/lstm_f32.hip (HFREP_LSTMF_DGRAD=0: hipBLASLt, A/B only)
+_LSTMF_DGRAD = os.environ.get("HFREP_LSTMF_DGRAD", "1") != "0"
+
+
 def linear_dgrad(dz: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     """dz @ W^T (input gradient)."""
+    if (_LSTMF_DGRAD and dz.dtype == torch.float32 and W.dtype == torch.float32 and dz.shape[-1] == 400
+            and W.shape[0] <= 112 and _nat(dz)):
+        return _ops().lstmf_dgrad(_2d(dz.contiguous()), W.contiguous()).reshape(*dz.shape[:-1], W.shape[0])
     if _nat(dz) and W.shape[1] > 4 and _blas_fp32(dz, dz.numel() // dz.shape[-1]):
         return torch.mm(_2d(dz.contiguous()), W.t()).reshape(*dz.shape[:-1], W.shape[0])
     if _nat(dz):

@@ -747,6 +747,21 @@ def test_lstmf_wgrad_fused(cuda, B, T, K, tangent):
     _close(gb, rb, torch.float32, scale=D.abs().sum(0).max().item())
 
 
+@pytest.mark.parametrize("M,KO", [(1, 100), (17, 32), (1000, 100), (4099, 36), (20000, 100), (333, 7), (100000, 112)])
+def test_lstmf_dgrad(cuda, M, KO):
+    """fp32 LSTM input gradient dZ W^T (register-resident k-split kernel) vs fp64, bitwise
+    run-to-run, including partial row chunks and column tiles."""
+    from hfrep.ops import _native
+
+    g = torch.Generator().manual_seed(29)
+    dz, W = torch.randn(M, 400, generator=g), torch.randn(KO, 400, generator=g) * 0.1
+    out = _native.native().lstmf_dgrad(dz.to(cuda), W.to(cuda))
+    ref = dz.double() @ W.double().t()
+    _close(out, ref, torch.float32, scale=(dz.abs().double() @ W.abs().double().t()).max().item())
+    again = _native.native().lstmf_dgrad(dz.to(cuda), W.to(cuda))
+    assert torch.equal(out, again)
+
+
 def test_gan_eval_device_path(cuda):
     """GANEval(..., device='cuda'): FID covariances through the native wgrad kernel and the MMD
     sample means on the GPU agree with the fp64 CPU reference path."""
