@@ -173,6 +173,16 @@ __device__ __forceinline__ f32x4 ld4(rsrc_t r, int voff) {
 __device__ __forceinline__ void st4(f32x4 v, rsrc_t r, int voff) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), r, voff, 0, 0);
 }
+// 16-byte store at byte offset voff + uoff (uoff uniform) with soffset 0.  A buffer store of more
+// than 8 bytes whose data VGPRs the next VALU instruction overwrites needs one wait state, and the
+// compiler only inserts it when soffset is NOT a register: with the uniform step offset in soffset
+// the BPTT's dZ stores wrote the next value for a few 16-byte chunks per 10^5 rows (rows 14 / 15
+// of a 32-row block, r02: scripts/dbg_large_bwd.py, scripts/isa_store_hazard.py)
+__device__ __forceinline__ void st16(f32x4 v, rsrc_t r, bool ok, int voff, int uoff) {
+  // (unsigned: voff may already be kOOB; the sum stays past every descriptor's size)
+  const int off = (int)((unsigned)voff + (unsigned)uoff);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), r, ok ? off : kOOB, 0, 0);
+}
 
 }  // namespace
 
@@ -417,10 +427,7 @@ struct BwdfStore {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(zt + lo + 2 * k * BZ_LR);
-      // (16-byte store with soffset != 0 and data overwritten right after: the data VGPRs are the
-      // ds_read result, not re-written by VALU before the store retires its operands)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rz, 2 * k + rr < nr ? go : kOOB,
-                                             (2 * k * Tn + t) * FG * 4, 0);
+      st16(v, rz, 2 * k + rr < nr, go, (2 * k * Tn + t) * FG * 4);
     }
   }
 };
@@ -433,8 +440,7 @@ __device__ __forceinline__ void bwdf_store16(const float* zt, rsrc_t rz, int Tn,
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(zt + lo + 2 * k * BZ_LR);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rz, 2 * k + rr < nr ? go : kOOB,
-                                           (2 * k * Tn + t) * FG * 4, 0);
+    st16(v, rz, 2 * k + rr < nr, go, (2 * k * Tn + t) * FG * 4);
   }
 }
 
@@ -678,8 +684,7 @@ lstmf_bwdp_kernel(const float* __restrict__ dH, const float* __restrict__ tape, 
 #pragma unroll
         for (int k = 8 * M; k < 8 * M + 8; ++k) {
           const f32x4 v = *reinterpret_cast<const f32x4*>(zt + slo + 2 * k * BZ_LR);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rz, 2 * k + srr < nr ? sgo : kOOB,
-                                                 (2 * k * Tn + ts) * FG * 4, 0);
+          st16(v, rz, 2 * k + srr < nr, sgo, (2 * k * Tn + ts) * FG * 4);
         }
       };
       // cell adjoints of row half M at step t; each cell then issues step t - 1's tape loads
@@ -1026,9 +1031,10 @@ lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, 
         for (int k = 8 * M; k < 8 * M + 8; ++k) {
           const f32x4 v = *reinterpret_cast<const f32x4*>(zt + slo + 2 * k * BZ_LR);
           const f32x4 vd = *reinterpret_cast<const f32x4*>(zdt + slo + 2 * k * BZ_LR);
-          const int go = 2 * k + srr < nr ? sgo : kOOB, so = (2 * k * Tn + ts) * FG * 4;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rz, go, so, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, vd), rzd, go, so, 0);
+          const bool ok = 2 * k + srr < nr;
+          const int so = (2 * k * Tn + ts) * FG * 4;
+          st16(v, rz, ok, sgo, so);
+          st16(vd, rzd, ok, sgo, so);
           if (k & 1) __builtin_amdgcn_sched_barrier(0);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -1150,26 +1156,31 @@ lstmf_wgrad_kernel(const float* __restrict__ X, const float* __restrict__ Hs, co
     const float* Xs = seg ? Xd : X;
     const float* Hq = seg ? Hds : Hs;
     const float* Dq = seg ? Dd : D;
-    const rsrc_t rx = make_rsrc(Xs, M * KX * 4), rh = make_rsrc(Hq, M * FH * 4), rd = make_rsrc(Dq, M * FG * 4);
+    // descriptors based at this workgroup's first row (row mb - 1 for the shifted H): the byte
+    // offsets stay 32-bit however large M is (a whole-tensor base overflowed past 1.34 M rows of dZ)
+    const int hb = mb > 0 ? mb - 1 : 0, nr = me > mb ? me - mb : 0;
+    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * KX, nr * KX * 4);
+    const rsrc_t rh = make_rsrc(Hq + (size_t)hb * FH, (nr ? me - hb : 0) * FH * 4);
+    const rsrc_t rd = make_rsrc(Dq + (size_t)mb * FG, nr * FG * 4);
     auto load = [&](int m0) {
 #pragma unroll
       for (int j = 0; j < WG::JX; ++j) {
         const int e = tid + 512 * j, r = e / (KX / 4), c = e - r * (KX / 4);
         const bool ok = e < WG::NX4 && m0 + r < me;
-        vx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? ((m0 + r) * KX + 4 * c) * 4 : kOOB, 0, 0));
+        vx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? ((m0 - mb + r) * KX + 4 * c) * 4 : kOOB, 0, 0));
       }
 #pragma unroll
       for (int j = 0; j < WG::JH; ++j) {
         const int e = tid + 512 * j, r = e / (FH / 4), c = e - r * (FH / 4);
         const int m = m0 + r;
         const bool ok = e < WG::NH4 && m < me && (m % Tn) != 0;  // h_{-1} = 0 at t = 0
-        vh[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, ok ? ((m - 1) * FH + 4 * c) * 4 : kOOB, 0, 0));
+        vh[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, ok ? ((m - 1 - hb) * FH + 4 * c) * 4 : kOOB, 0, 0));
       }
 #pragma unroll
       for (int j = 0; j < WG::JD; ++j) {
         const int e = tid + 512 * j, r = e / (FG / 4), c = e - r * (FG / 4);
         const bool ok = e < WG::ND4 && m0 + r < me;
-        vd[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, ok ? ((m0 + r) * FG + 4 * c) * 4 : kOOB, 0, 0));
+        vd[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, ok ? ((m0 - mb + r) * FG + 4 * c) * 4 : kOOB, 0, 0));
       }
     };
     auto to_lds = [&](int buf) {

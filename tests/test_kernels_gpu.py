@@ -747,6 +747,33 @@ def test_lstmf_wgrad_fused(cuda, B, T, K, tangent):
     _close(gb, rb, torch.float32, scale=D.abs().sum(0).max().item())
 
 
+@pytest.mark.parametrize("K,tangent", [(100, False), (32, True)])
+def test_lstmf_wgrad_large_m(cuda, K, tangent):
+    """fp32 fused weight gradient past 4 GiB of dZ (M = 3 M rows: a whole-tensor buffer descriptor
+    wrapped its 32-bit size there and read zeros for the later rows) vs an fp64 GPU reference."""
+    from hfrep.ops import functional as Fn
+
+    B, T, H, N = 120000, 25, 100, 400
+    g = torch.Generator(device=cuda).manual_seed(31)
+    rn = lambda *s: torch.randn(*s, device=cuda, generator=g)  # noqa: E731
+    x, hs, dz = rn(B, T, K), rn(B, T, H), rn(B, T, N)
+    xd, hds, dzd = (rn(B, T, K), rn(B, T, H), rn(B, T, N)) if tangent else (None, None, None)
+    gW, gU, gb = (torch.zeros(K, N, device=cuda), torch.zeros(H, N, device=cuda), torch.zeros(N, device=cuda))
+    Fn.lstm_wgrad_(x, hs, dz, gW, gU, gb, xd, hds, dzd)
+    rW = torch.zeros(K, N, dtype=torch.float64, device=cuda)
+    rU = torch.zeros(H, N, dtype=torch.float64, device=cuda)
+    for xx, hh, dd in ((x, hs, dz), (xd, hds, dzd)) if tangent else ((x, hs, dz),):
+        D = dd.double().reshape(-1, N)
+        rW += xx.double().reshape(-1, K).t() @ D
+        rU += R.shift_prev(hh.double()).reshape(-1, H).t() @ D
+    rb = dz.double().reshape(-1, N).sum(0)
+    # random-sign sums of 3 M products: scale by the root-sum-square, not the absolute sum
+    tol = 2e-5 * (B * T) ** 0.5 * (2 if tangent else 1)
+    for got, ref in ((gW, rW), (gU, rU), (gb, rb)):
+        err = (got.double() - ref).abs().max().item()
+        assert err < tol, (err, tol)
+
+
 @pytest.mark.parametrize("M,KO", [(1, 100), (17, 32), (1000, 100), (4099, 36), (20000, 100), (333, 7), (100000, 112)])
 def test_lstmf_dgrad(cuda, M, KO):
     """fp32 LSTM input gradient dZ W^T (register-resident k-split kernel) vs fp64, bitwise
@@ -774,3 +801,56 @@ def test_gan_eval_device_path(cuda):
     for name in ("FID", "linear_MMD", "gaussian_MMD", "poly_MMD"):
         a, b = getattr(gpu, name)(), getattr(cpu, name)()
         assert abs(a - b) <= 1e-4 * max(abs(b), 1e-3), (name, a, b)
+
+
+def _block_rel(model, a, b):
+    """{keras weight name: relative L2 error} of two flat gradients of ``model``."""
+    out = {}
+    for lay in model.layers:
+        for sp in lay.specs:
+            n = int(np.prod(sp.shape))
+            x, y = a[sp.offset:sp.offset + n], b[sp.offset:sp.offset + n]
+            out[sp.keras] = ((x - y).norm() / max(y.norm().item(), 1e-30)).item()
+    return out
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("B", [16384, 262144])
+def test_bench_scale_gradients_are_slice_averages(cuda, dtype, B):
+    """At the bench batch (B = 262,144: dZ of the critic's W terms is 20 GB) the critic GP and the
+    generator gradients equal the average of the gradients of four row slices: every row's
+    contribution is computed identically, only the reduction order differs.  Catches any kernel
+    whose addressing breaks past 2 / 4 GiB (the fp32 weight gradient did, before r02)."""
+    from hfrep.train.gan_trainer import GANConfig, GANTrainer
+
+    T, F, S = 24, 32, 4
+    ds = np.random.RandomState(0).rand(64, T, F).astype(np.float32)
+    tr = GANTrainer(GANConfig(arch="lstm", loss="wgan_gp", window=T, features=F, batch_size=B, dtype=dtype), ds,
+                    device=cuda)
+    dt = torch.float32 if dtype == "float32" else torch.bfloat16
+    g = torch.Generator(device=cuda).manual_seed(41)
+    real = torch.rand(B, T, F, device=cuda, generator=g).to(dt)
+    noise = torch.randn(B, T, F, device=cuda, generator=g).to(dt)
+    alpha = torch.rand(B, device=cuda, generator=g)
+    tol = 1e-4 if dtype == "float32" else 1e-3
+    sl = lambda t, i: t[i * (B // S):(i + 1) * (B // S)].contiguous()  # noqa: E731
+
+    def grads(model, fn, *args):
+        if model.flat.grad is not None:
+            model.flat.grad.zero_()
+        fn(*args)
+        torch.cuda.synchronize()
+        return model.flat.grad.double().clone()
+
+    with torch.no_grad():
+        fake = tr.generator.predict(noise)
+        full = grads(tr.critic, tr.critic_gp_grads, real, fake, alpha)
+        avg = sum(grads(tr.critic, tr.critic_gp_grads, sl(real, i), sl(fake, i), sl(alpha, i)) for i in range(S)) / S
+        rel = ((full - avg).norm() / avg.norm()).item()
+        assert torch.isfinite(full).all() and rel < tol, (f"critic: full-batch vs slice-average rel {rel:.2e}",
+                                                          _block_rel(tr.critic, full, avg))
+        full = grads(tr.generator, tr.generator_grads, noise)
+        avg = sum(grads(tr.generator, tr.generator_grads, sl(noise, i)) for i in range(S)) / S
+        rel = ((full - avg).norm() / avg.norm()).item()
+        assert torch.isfinite(full).all() and rel < tol, (f"generator: full-batch vs slice-average rel {rel:.2e}",
+                                                          _block_rel(tr.generator, full, avg))
