@@ -147,11 +147,12 @@ void lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<
   const void* D1 = tangent ? dZd->data_ptr() : nullptr;
   float* gbp = gb.has_value() ? gb->data_ptr<float>() : nullptr;
   if (f32) {
-    Tensor ws = out_empty({(int64_t)hfrep::lstmf_wgrad_workspace_floats(M, K)}, x.options());
+    // impl (fp32): 0 = default, 1 = exact-fp32 MFMA kernel, 2 = three-term bf16 split kernel
+    Tensor ws = out_empty({(int64_t)hfrep::lstmf_wgrad_workspace_floats(M, K, (int)impl)}, x.options());
     hfrep::launch_lstmf_wgrad(x.data_ptr<float>(), hs.data_ptr<float>(), dZ.data_ptr<float>(),
                               tangent ? xd->data_ptr<float>() : nullptr, tangent ? hds->data_ptr<float>() : nullptr,
                               tangent ? dZd->data_ptr<float>() : nullptr, gW.data_ptr<float>(), gU.data_ptr<float>(), gbp,
-                              M, K, Tn, ws.data_ptr<float>(), cur_stream(x));
+                              M, K, Tn, ws.data_ptr<float>(), cur_stream(x), (int)impl);
     return;
   }
   // impl: 0 = auto (LDS-DMA streaming v3 where supported), 2 = force v2 (tests / A-B)

@@ -58,9 +58,11 @@ bool launch_lstmf_tbwd(const float* dH, const float* dHd, const float* tape, con
 // gU += Hprev^T dZ (+ Hdprev^T dZd), gb += colsum dZ, through per-workgroup slabs in ws
 // (lstmf_wgrad_workspace_floats) and one fixed-order reduce
 bool lstmf_wgrad_supported(int K, int H, int N);
-size_t lstmf_wgrad_workspace_floats(int M, int K);
+// impl: 0 = default (HFREP_LSTMF_WGRAD, else the split for K <= 36 and exact for K = 100), 1 = exact-fp32
+// MFMA, 2 = the three-term bf16 split
+size_t lstmf_wgrad_workspace_floats(int M, int K, int impl = 0);
 bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
-                        float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s);
+                        float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl = 0);
 // fp32 input gradient X (M, KO) = D (M, N) W^T, W (KO, N) row-major; N = 400, KO <= 112
 bool lstmf_dgrad_supported(int N, int KO);
 bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s);

@@ -170,6 +170,9 @@ __device__ __forceinline__ constexpr int ftape_slot(int m, int n) { return (m * 
 __device__ __forceinline__ f32x4 ld4(rsrc_t r, int voff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
 }
+__device__ __forceinline__ f32x4 ld4s(rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
 __device__ __forceinline__ void st4(f32x4 v, rsrc_t r, int voff) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), r, voff, 0, 0);
 }
@@ -1257,6 +1260,291 @@ lstmf_wgrad_kernel(const float* __restrict__ X, const float* __restrict__ Hs, co
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// fp32 weight gradient on the bf16 matrix pipe: three-term split, six products
+// ------------------------------------------------------------------------------------------
+// lstmf_wgrad_kernel above runs at ~83 % of the fp32 MFMA rate (64 FLOP/clk/SIMD), which is 1/16 of
+// the bf16 rate.  Here every fp32 operand a is split EXACTLY into three bf16 terms by truncation,
+// a = h + m + l (h = top 8 significand bits, m = the next 8, l = the last 8: the two subtractions
+// are exact), and C += A^T D is accumulated as hh + hm + mh + mm + hl + lh on
+// v_mfma_f32_16x16x32_bf16 (bf16 x bf16 products are exact in fp32, accumulation in fp32).  The
+// dropped terms ml, lm, ll are <= 2^-24 |a b| -- the rounding error of one fp32 product -- so the
+// result matches the exact-fp32 kernel to fp32 reduction noise (test_lstmf_wgrad_split_*), at 6/16
+// of its matrix-pipe time.
+//
+// Work split: a workgroup PAIR shares a row range z and splits the 400 gate columns (jh = 0: columns
+// 0..207, jh = 1: 208..399 + a zero tile); the pair sits on one XCD (blocks b and b + 8), so the A
+// rows [x | h_{t-1} | 1] both read come from the same L2.  Per 32-row chunk the workgroup stages the
+// three bf16 planes of A (32 x 208) and of its D half (32 x 208) in LDS, double-buffered (2 x 78 KB):
+// the next chunk's fp32 rows are loaded into registers before the MFMAs and split into the other
+// buffer after them, one barrier per chunk.  MFMA operands come from ds_read_b64_tr_b16 (row-major
+// image, hardware transpose: lane 4q + p of a 16-lane group addresses row q, columns 4p..4p+3).
+// 8 waves: wave w owns i-tiles [0, 7) or [7, NI) (w >> 2) times a group of 4 / 3 / 3 / 3 local
+// j-tiles (reversed for w >= 4 so each SIMD's two waves carry ~equal MFMA counts); its B fragments
+// (all three planes of its <= 4 j-tiles) stay in registers for the chunk, the A fragments stream.
+constexpr int WS_C = 208, WS_ROWB = WS_C * 2, WS_PLANE = 32 * WS_ROWB;  // bytes: one bf16 plane image
+constexpr int WS_IMG = 3 * WS_PLANE;                                    // three planes
+constexpr int WS_BUF = 2 * WS_IMG;                                      // A image + D image
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+template <int KX>
+struct WSGeo {
+  static constexpr int KR = KX + FH + 1;          // rows of the output slab (bias row last)
+  static constexpr int NI = (KR + 15) / 16;       // i-tiles
+  static constexpr int NI0 = (NI + 1) / 2;        // i-tiles of waves 0..3
+  static constexpr int JX = (32 * KX / 4 + 511) / 512, JH = (32 * FH / 4 + 511) / 512;  // float4 slots per thread
+  static constexpr int JD = (32 * 52 + 511) / 512;  // D slots: 52 float4 per row (jh = 1 uses 48)
+  static_assert(KX % 4 == 0 && 16 * NI <= WS_C, "wgrad split: K");
+};
+
+// three bf16 planes of four fp32 values, packed two per dword
+__device__ __forceinline__ void split3(const f32x4 v, uint32_t (&p)[3][2]) {
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    uint32_t hb[2], mb[2], lb[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float a = v[2 * e + k];
+      const uint32_t u = __builtin_bit_cast(uint32_t, a), h = u & 0xffff0000u;
+      const float r1 = a - __builtin_bit_cast(float, h);
+      const uint32_t u1 = __builtin_bit_cast(uint32_t, r1), m = u1 & 0xffff0000u;
+      const float r2 = r1 - __builtin_bit_cast(float, m);
+      hb[k] = h;
+      mb[k] = m;
+      lb[k] = __builtin_bit_cast(uint32_t, r2);
+    }
+    // high halves of (x1, x0) -> x0 in the low 16 bits, x1 in the high 16 bits
+    p[0][e] = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
+    p[1][e] = __builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u);
+    p[2][e] = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
+  }
+}
+
+// one 16x16x32 operand (8 bf16) of plane image `img` (byte offset in LDS) at column block c0:
+// two transposed reads (rows 8 G + q and 8 G + 4 + q of this lane's group G)
+__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int lane_off, int c0) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + lane_off + c0 * 2));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + lane_off + 4 * WS_ROWB + c0 * 2));
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+__device__ __forceinline__ f32x4 mma32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// one chunk's products for NIV i-tiles x NJV j-tiles of a wave (acc[ii][jj], ii < NIV, jj < NJV):
+// two passes over the i-tiles, each with the three B planes of (up to) two j-tiles in registers and
+// the A fragments streamed one i-tile ahead.  Each tile's six products go to a fresh accumulator
+// that is added to the running sum in VALU fp32 (round to nearest): chaining them straight into the
+// running sum on the matrix pipe drifted (3 M rows: 0.043 vs 0.014 for the exact kernel, consistent
+// with a biased rounding of the MFMA's C addition).
+template <int NIV, int NJV, int NA, int NB>
+__device__ __forceinline__ void ws_chunk(f32x4 (&acc)[NA][NB], const char* A_, const char* D_, int tr_off, int i0, int j0) {
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+    constexpr int dummy = 0;
+    (void)dummy;
+    const int nb = NJV - 2 * jp < 2 ? NJV - 2 * jp : 2;  // compile-time after unrolling
+    bf16x8 bfr[2][3];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (jj < nb) bfr[jj][q] = tr_frag(D_ + q * WS_PLANE, tr_off, 16 * (j0 + 2 * jp + jj));
+    bf16x8 af[2][3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) af[0][q] = tr_frag(A_ + q * WS_PLANE, tr_off, 16 * i0);
+#pragma unroll
+    for (int ii = 0; ii < NIV; ++ii) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (ii + 1 < NIV) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) af[(ii + 1) & 1][q] = tr_frag(A_ + q * WS_PLANE, tr_off, 16 * (i0 + ii + 1));
+      }
+      const bf16x8(&a3)[3] = af[ii & 1];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        if (jj < nb) {
+          f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
+          t = mma32(a3[2], bfr[jj][0], t);  // lh
+          t = mma32(a3[0], bfr[jj][2], t);  // hl
+          t = mma32(a3[1], bfr[jj][1], t);  // mm
+          t = mma32(a3[1], bfr[jj][0], t);  // mh
+          t = mma32(a3[0], bfr[jj][1], t);  // hm
+          t = mma32(a3[0], bfr[jj][0], t);  // hh
+          acc[ii][2 * jp + jj] += t;
+        }
+      }
+    }
+  }
+}
+
+template <int KX>
+__global__ void __launch_bounds__(512, 1)
+lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ Hs, const float* __restrict__ D,
+                         const float* __restrict__ Xd, const float* __restrict__ Hds, const float* __restrict__ Dd,
+                         float* __restrict__ slab, int M, int Tn, int rows_per_z, int Z) {
+  using G = WSGeo<KX>;
+  constexpr int NI = G::NI, NI0 = G::NI0, JX = G::JX, JH = G::JH, JD = G::JD;
+  extern __shared__ __attribute__((aligned(16))) char wsm[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // block -> (row range z, column half jh); with Z % 8 == 0 the pair shares an XCD
+  int z, jh;
+  if (Z % 8 == 0) {
+    const int slot = blockIdx.x >> 3;
+    jh = slot & 1;
+    z = (slot >> 1) * 8 + (blockIdx.x & 7);
+  } else {
+    jh = blockIdx.x & 1;
+    z = blockIdx.x >> 1;
+  }
+  const int mb = z * rows_per_z, me = min(M, mb + rows_per_z);
+  const int jbase = 208 * jh, nd4 = jh ? 48 : 52;  // D columns of this half, float4 per row
+
+  // wave tiles
+  const int ig = w >> 2, jg = ig ? 3 - (w & 3) : (w & 3);
+  const int i0 = ig ? NI0 : 0, ni = ig ? NI - NI0 : NI0;
+  const int j0 = jg == 0 ? 0 : 1 + 3 * jg, nj = jg == 0 ? 4 : 3;
+
+  // zero both buffers (pad columns, the zero j-tile of jh = 1), then the bias column (A, plane h)
+  for (int i = tid; i < 2 * WS_BUF / 16; i += 512) reinterpret_cast<uint4*>(wsm)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+
+  f32x4 acc[NI0][4];
+#pragma unroll
+  for (int a = 0; a < NI0; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // this lane's transposed-read base: row 8 G + q, column 4 p (bytes)
+  const int tr_off = (8 * (lane >> 4) + ((lane & 15) >> 2)) * WS_ROWB + 8 * (lane & 3);
+
+  // per-thread float4 slots of a 32-row chunk: X (JX), H (JH), D (JD); element e = tid + 512 j of the
+  // chunk's row-major image.  Their offsets are recomputed per chunk from an opaque copy of tid (a few
+  // VALU) instead of being held in ~20 loop-invariant registers next to the accumulators.
+  const int step32 = 32 % Tn;
+  f32x4 vx[JX], vh[JH], vd[JD];
+  for (int seg = 0; seg < (Xd ? 2 : 1); ++seg) {
+    const float* Xs = seg ? Xd : X;
+    const float* Hq = seg ? Hds : Hs;
+    const float* Dq = seg ? Dd : D;
+    // the H descriptor starts at row mb - 1 (row -1 for mb = 0, whose h_{-1} is never addressed: the
+    // t = 0 rows are masked) so every voffset is >= 0 -- the range check is on voffset alone, and a
+    // negative voffset with a compensating soffset reads zeros
+    const int nr = me > mb ? me - mb : 0;
+    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * KX, nr * KX * 4);
+    const rsrc_t rh = make_rsrc(Hq + ((ptrdiff_t)mb - 1) * FH, (nr ? nr + 1 : 0) * FH * 4);
+    const rsrc_t rd = make_rsrc(Dq + (size_t)mb * FG, nr * FG * 4);
+    // t = (row) mod Tn of this thread's H slots at the current chunk (h_{-1} = 0 rows)
+    int tm[JH];
+#pragma unroll
+    for (int j = 0; j < JH; ++j) tm[j] = (mb + min((tid + 512 * j) / (FH / 4), 31)) % Tn;
+    auto opaque_tid = [&]() {
+      int t = tid;
+      asm volatile("" : "+v"(t));
+      return t;
+    };
+    auto load = [&](int m0) {  // rows past me: voffset out of range, zeros
+      const int lim = me - m0, t0 = opaque_tid();
+#pragma unroll
+      for (int j = 0; j < JX; ++j) {
+        const int e = t0 + 512 * j, r = e / (KX / 4), c4 = e - r * (KX / 4);
+        const bool ok = e < 32 * KX / 4 && r < lim;
+        vx[j] = ld4s(rx, ok ? (r * KX + 4 * c4) * 4 : kOOB, (m0 - mb) * KX * 4);
+      }
+#pragma unroll
+      for (int j = 0; j < JH; ++j) {
+        const int e = t0 + 512 * j, r = e / (FH / 4), c4 = e - r * (FH / 4);
+        const bool ok = e < 32 * FH / 4 && r < lim && tm[j] != 0;
+        vh[j] = ld4s(rh, ok ? (r * FH + 4 * c4) * 4 : kOOB, (m0 - mb) * FH * 4);
+      }
+#pragma unroll
+      for (int j = 0; j < JD; ++j) {
+        const int e = t0 + 512 * j, r = e / 52, c4 = e - r * 52;
+        const bool ok = e < 32 * 52 && c4 < nd4 && r < lim;
+        vd[j] = ld4s(rd, ok ? (r * FG + jbase + 4 * c4) * 4 : kOOB, (m0 - mb) * FG * 4);
+      }
+#pragma unroll
+      for (int j = 0; j < JH; ++j) {
+        tm[j] += step32;
+        if (tm[j] >= Tn) tm[j] -= Tn;
+      }
+    };
+    auto put = [&](char* dst, bool ok, const f32x4& v) {
+      if (ok) {
+        uint32_t p[3][2];
+        split3(v, p);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(dst + q * WS_PLANE) = make_uint2(p[q][0], p[q][1]);
+      }
+    };
+    auto stage = [&](int buf) {
+      char* base = wsm + buf * WS_BUF;
+      const int t0 = opaque_tid();
+#pragma unroll
+      for (int j = 0; j < JX; ++j) {
+        const int e = t0 + 512 * j, r = e / (KX / 4), c4 = e - r * (KX / 4);
+        put(base + r * WS_ROWB + 8 * c4, e < 32 * KX / 4, vx[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < JH; ++j) {
+        const int e = t0 + 512 * j, r = e / (FH / 4), c4 = e - r * (FH / 4);
+        put(base + r * WS_ROWB + 2 * KX + 8 * c4, e < 32 * FH / 4, vh[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < JD; ++j) {
+        const int e = t0 + 512 * j, r = e / 52, c4 = e - r * 52;
+        put(base + WS_IMG + r * WS_ROWB + 8 * c4, e < 32 * 52 && c4 < nd4, vd[j]);
+      }
+    };
+    // bias column (column KR - 1 of A): 1 in plane h for the primal segment, 0 for the tangent one
+    if (tid < 64) {
+      const int buf = tid >> 5, r = tid & 31;
+      *reinterpret_cast<uint16_t*>(wsm + buf * WS_BUF + r * WS_ROWB + (G::KR - 1) * 2) = seg ? 0 : 0x3f80;
+    }
+    const int nch = nr > 0 ? (nr + 31) / 32 : 0;
+    if (nch > 0) {
+      load(mb);
+      stage(0);
+    }
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      const bool more = c + 1 < nch;
+      if (more) load(mb + 32 * (c + 1));
+      const char* A_ = wsm + (c & 1) * WS_BUF;
+      const char* D_ = A_ + WS_IMG;
+      // straight-line MFMA code per (i-tiles, j-tiles) shape: with wave-uniform branches between an
+      // MFMA and the VALU read of its result the compiler did not count the wait states across the
+      // branch (2 instead of >= 7: stale sums)
+      switch (ni * 8 + nj) {
+        case NI0 * 8 + 4: ws_chunk<NI0, 4>(acc, A_, D_, tr_off, i0, j0); break;
+        case NI0 * 8 + 3: ws_chunk<NI0, 3>(acc, A_, D_, tr_off, i0, j0); break;
+        case (NI - NI0) * 8 + 4: ws_chunk<NI - NI0, 4>(acc, A_, D_, tr_off, i0, j0); break;
+        default: ws_chunk<NI - NI0, 3>(acc, A_, D_, tr_off, i0, j0); break;
+      }
+      if (more) stage((c + 1) & 1);
+      __syncthreads();
+    }
+    __syncthreads();  // (the bias column of both buffers is rewritten for the next segment)
+  }
+  // slab store: C[16 (i0 + ii) + 4 g + r][jbase + 16 (j0 + jj) + c16]
+  float* out = slab + (size_t)z * G::KR * FG;
+  const int g = lane >> 4, c16 = lane & 15;
+#pragma unroll
+  for (int ii = 0; ii < NI0; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+      if (ii < ni && jj < nj) {
+        const int col = jbase + 16 * (j0 + jj) + c16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 16 * (i0 + ii) + 4 * g + r;
+          if (i < G::KR && col < FG) out[(size_t)i * FG + col] = acc[ii][jj][r];
+        }
+      }
+}
+
 // ==========================================================================================
 // fp32 input gradient dX = dZ W^T   (dZ: M x 400, W: KO x 400 row-major, dX: M x KO, KO <= 16 NT)
 // ==========================================================================================
@@ -1498,11 +1786,51 @@ static int wgradf_grid(int M) {
   return chunks < cus ? chunks : cus;
 }
 bool lstmf_wgrad_supported(int K, int H, int N) { return H == FH && N == FG && (K == 32 || K == 36 || K == 100); }
-size_t lstmf_wgrad_workspace_floats(int M, int K) { return (size_t)wgradf_grid(M) * (K + FH + 1) * FG; }
+
+// HFREP_LSTMF_WGRAD=1 / 2: force the exact-fp32 MFMA kernel / the three-term bf16 split; default (0):
+// the split for K <= 36 (12.1 -> 10.8 ms at 12.6 M rows), the exact kernel for K = 100, where the split
+// kernel's 28-tile waves spill (36.5 vs 16.4 ms; profiles/r02_hazard/wgrad_split_vs_exact_v1.jsonl)
+static int wgradf_version() {
+  static const int v = [] {
+    const char* e = getenv("HFREP_LSTMF_WGRAD");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+// split kernel: Z row ranges x 2 column halves, one workgroup per CU
+static int wgrads_z(int M) {
+  const int chunks = (M + 31) / 32, half = device_cu_count() / 2;
+  return chunks < half ? chunks : half;
+}
+static int wgradf_pick(int impl, int K) {
+  const int v = impl == 1 || impl == 2 ? impl : wgradf_version();
+  return v ? v : (K <= 36 ? 2 : 1);
+}
+size_t lstmf_wgrad_workspace_floats(int M, int K, int impl) {
+  const int z = wgradf_pick(impl, K) == 1 ? wgradf_grid(M) : wgrads_z(M);
+  return (size_t)z * (K + FH + 1) * FG;
+}
 
 bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
-                        float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s) {
+                        float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl) {
   if (!lstmf_wgrad_supported(K, FH, FG) || M <= 0) return false;
+  if (wgradf_pick(impl, K) != 1) {
+    const int z0 = wgrads_z(M);
+    const int rpz = ((M + z0 - 1) / z0 + 31) / 32 * 32;
+    const int z = (M + rpz - 1) / rpz;
+    const size_t sm = 2 * WS_BUF;
+    auto go = [&](auto k) {
+      allow_lds(reinterpret_cast<const void*>(k));
+      hipLaunchKernelGGL(k, dim3(2 * z), dim3(512), sm, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpz, z);
+    };
+    switch (K) {
+      case 32: go(lstmf_wgrad_split_kernel<32>); break;
+      case 36: go(lstmf_wgrad_split_kernel<36>); break;
+      default: go(lstmf_wgrad_split_kernel<100>); break;
+    }
+    launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s);
+    return true;
+  }
   const int grid = wgradf_grid(M);
   const int rpw = ((M + grid - 1) / grid + WF_R - 1) / WF_R * WF_R;
   const int z = (M + rpw - 1) / rpw;

@@ -374,8 +374,10 @@ def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None, impl: int = 
     """All weight gradients of one LSTM layer: gW += X^T dZ (+ Xd^T dZd), gU += H_{t-1}^T dZ (+ ...),
     gb += sum(dZ).  bf16 GPU: ONE fused launch (csrc/wgrad3.hip LDS-DMA streaming kernel where the
     shape is supported, csrc/gemm2.hip otherwise; ``impl=2`` forces the latter); fp32 GPU at the
-    model widths: ONE fused launch of csrc/lstm_f32.hip lstmf_wgrad_kernel; otherwise per-product
-    calls."""
+    model widths: ONE fused launch of csrc/lstm_f32.hip -- lstmf_wgrad_split_kernel (fp32 operands
+    split exactly into three bf16 terms, six products on the bf16 matrix pipe; default for K <= 36,
+    ``impl=2``) or the exact-fp32 MFMA kernel lstmf_wgrad_kernel (default for K = 100, ``impl=1``);
+    otherwise per-product calls."""
     f32 = (dZ.dtype == torch.float32 and _LSTMF and x.shape[-1] in (32, 36, 100) and hs.shape[-1] == 100
            and dZ.shape[-1] == 400)
     if (dZ.dtype == torch.bfloat16 or f32) and _nat(dZ):
