@@ -334,7 +334,7 @@ std::tuple<Tensor, Tensor> lstmf_tbwd(optional<Tensor> dH, optional<Tensor> dHd,
   return {dZ, dZd};
 }
 
-Tensor lstmf_dgrad(Tensor dz, Tensor W) {
+Tensor lstmf_dgrad(Tensor dz, Tensor W, int64_t impl) {
   CHECK_F32(dz); CHECK_F32(W);
   TORCH_CHECK(dz.dim() == 2 && dz.is_contiguous() && W.dim() == 2 && W.is_contiguous() && W.size(1) == dz.size(1),
               "lstmf_dgrad: dz (M, N) and W (KO, N), contiguous");
@@ -343,7 +343,7 @@ Tensor lstmf_dgrad(Tensor dz, Tensor W) {
   Tensor x = out_empty({dz.size(0), W.size(0)}, dz.options());
   if (dz.size(0) == 0) return x;
   const bool ok = hfrep::launch_lstmf_dgrad(dz.data_ptr<float>(), W.data_ptr<float>(), x.data_ptr<float>(), dz.size(0),
-                                            dz.size(1), W.size(0), cur_stream(dz));
+                                            dz.size(1), W.size(0), cur_stream(dz), (int)impl);
   TORCH_CHECK(ok, "lstmf_dgrad: launch failed");
   return x;
 }
@@ -710,7 +710,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstmf_bwd(Tensor? dH, Tensor tape, Tensor U, int act, int B, int T) -> Tensor");
   m.def("lstmf_tbwd(Tensor? dH, Tensor? dHd, Tensor tape, Tensor ttape, Tensor U, int act, int B, int T) -> (Tensor, Tensor)");
   m.def("lstmf_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int act) -> (Tensor, Tensor)");
-  m.def("lstmf_dgrad(Tensor dz, Tensor W) -> Tensor");
+  m.def("lstmf_dgrad(Tensor dz, Tensor W, int impl=0) -> Tensor");
   m.def("lstm2_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
   m.def("lstm2_bwd(Tensor? dH, Tensor tape, Tensor U, int act, Tensor? W=None, bool need_dz=True, Tensor? head_d=None, "
         "Tensor? head_w=None) -> (Tensor, Tensor)");

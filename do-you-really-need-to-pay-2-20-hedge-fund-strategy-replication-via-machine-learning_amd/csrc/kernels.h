@@ -65,7 +65,8 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
                         float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl = 0);
 // fp32 input gradient X (M, KO) = D (M, N) W^T, W (KO, N) row-major; N = 400, KO <= 112
 bool lstmf_dgrad_supported(int N, int KO);
-bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s);
+// impl: 0 = default (HFREP_LSTMF_DGRAD_IMPL, else the exact-fp32 MFMA kernel), 1 = exact, 2 = three-term bf16 split
+bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl = 0);
 
 // ---- gemm.hip ----
 // C[M,N] = act(A[M,K] . op(W) + bias);  op(W) = W (K,N) or W^T when w_trans (W stored (N,K)).

@@ -1545,6 +1545,118 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
       }
 }
 
+// ------------------------------------------------------------------------------------------
+// fp32 input gradient on the bf16 matrix pipe: dX = dZ W^T with the exact three-term split
+// ------------------------------------------------------------------------------------------
+// Same split as lstmf_wgrad_split_kernel (a = h + m + l by truncation, six products
+// lh + hl + mm + mh + hm + hh on v_mfma_f32_16x16x32_bf16, dropped terms <= 2^-24 of each product).
+// The reduction (k = 400 gate columns) is 13 k-steps of 32 (k 400..415 zero); 8 waves, wave w owns
+// k-steps w and w + 8 (waves 5..7 only w), so its W^T fragments -- all three planes, every output
+// tile: 2 x NT x 3 x 4 VGPRs -- stay in registers for the whole kernel.  Per 16-row tile every lane
+// loads its 8 contiguous dZ values per k-step straight from HBM (one tile ahead) and splits them in
+// registers; the waves' partial tiles meet in LDS (double-buffered, one barrier per tile) and are
+// summed in fixed wave order.  Each partial is at most 12 MFMAs from zero, so the MFMA's own C
+// accumulation is used (no long-running sum here).  Straight-line MFMA -> LDS-store code per wave
+// kind (two k-steps or one): no branch between an MFMA and the read of its result.
+constexpr int DS_KS = 13;
+template <int NT, int NKS>
+__device__ __forceinline__ void dgs_tile(f32x4* part, const bf16x8 (&bw)[2][NT][3], const f32x4 (&ra)[2][2],
+                                         int lane) {
+  f32x4 acc[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    uint32_t p0[3][2], p1[3][2];
+    split3(ra[s][0], p0);
+    split3(ra[s][1], p1);
+    bf16x8 a[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      a[q] = __builtin_bit_cast(bf16x8, make_uint4(p0[q][0], p0[q][1], p1[q][0], p1[q][1]));
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      f32x4 t = acc[n];
+      t = mma32(a[2], bw[s][n][0], t);  // lh
+      t = mma32(a[0], bw[s][n][2], t);  // hl
+      t = mma32(a[1], bw[s][n][1], t);  // mm
+      t = mma32(a[1], bw[s][n][0], t);  // mh
+      t = mma32(a[0], bw[s][n][1], t);  // hm
+      acc[n] = mma32(a[0], bw[s][n][0], t);  // hh
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NT; ++n) part[n * 64 + lane] = acc[n];
+}
+
+template <int NT>
+__global__ void __launch_bounds__(512, 1)
+lstmf_dgrad_split_kernel(const float* __restrict__ D, const float* __restrict__ W, float* __restrict__ X, int M, int KO,
+                         int rows_per_wg) {
+  extern __shared__ __attribute__((aligned(16))) f32x4 dpart[];  // [2][8 waves][NT][64 lanes]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int mb = blockIdx.x * rows_per_wg, nrows = min(M, mb + rows_per_wg) - mb;
+  if (nrows <= 0) return;  // uniform over the workgroup
+  const int nks = w + 8 < DS_KS ? 2 : 1;
+  // W^T fragments (B operand: lane holds k = 32 ks + 8 g .. + 7 of output column 16 n + c16), split
+  bf16x8 bw[2][NT][3];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int ks = w + 8 * s, col = 16 * n + c16, k0 = 32 * ks + 8 * g;
+      f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
+      if (ks < DS_KS && col < KO && k0 < FG) {
+        v0 = *reinterpret_cast<const f32x4*>(W + (size_t)col * FG + k0);
+        v1 = *reinterpret_cast<const f32x4*>(W + (size_t)col * FG + k0 + 4);
+      }
+      uint32_t p0[3][2], p1[3][2];
+      split3(v0, p0);
+      split3(v1, p1);
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        bw[s][n][q] = __builtin_bit_cast(bf16x8, make_uint4(p0[q][0], p0[q][1], p1[q][0], p1[q][1]));
+    }
+  const rsrc_t rd = make_rsrc(D + (size_t)mb * FG, nrows * FG * 4);
+  const rsrc_t rx = make_rsrc(X + (size_t)mb * KO, nrows * KO * 4);
+  const int nt16 = (nrows + 15) / 16;
+  // this lane's A operand: row r0 + c16, k = 32 ks + 8 g .. + 7 (k >= 400: zeros)
+  auto load = [&](f32x4 (&ra)[2][2], int r0) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ks = w + 8 * s, k0 = 32 * ks + 8 * g;
+      const bool ok = ks < DS_KS && k0 < FG && r0 + c16 < nrows;
+      const int vo = ok ? ((r0 + c16) * FG + k0) * 4 : kOOB;
+      ra[s][0] = ld4(rd, vo);
+      ra[s][1] = ld4(rd, ok ? vo + 16 : kOOB);
+    }
+  };
+  f32x4 ra[2][2][2];
+  load(ra[0], 0);
+  for (int c = 0; c < nt16; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nt16) load(ra[cur ^ 1], 16 * (c + 1));
+    f32x4* part = dpart + ((cur * 8 + w) * NT) * 64;
+    if (nks == 2)
+      dgs_tile<NT, 2>(part, bw, ra[cur], lane);
+    else
+      dgs_tile<NT, 1>(part, bw, ra[cur], lane);
+    __syncthreads();
+    // fixed-order sum of the 8 waves' partials; thread e owns (n, lane') = (e >> 6, e & 63)
+    const f32x4* pb = dpart + (cur * 8) * NT * 64;
+    for (int e = tid; e < NT * 64; e += 512) {
+      f32x4 v = pb[e];
+#pragma unroll
+      for (int ww = 1; ww < 8; ++ww) v += pb[ww * NT * 64 + e];
+      const int n = e >> 6, ln = e & 63, col = 16 * n + (ln & 15), row = 16 * c + 4 * (ln >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st1(v[i], rx, col < KO && row + i < nrows ? ((row + i) * KO + col) * 4 : kOOB, 0);
+    }
+  }
+}
+
 // ==========================================================================================
 // fp32 input gradient dX = dZ W^T   (dZ: M x 400, W: KO x 400 row-major, dX: M x KO, KO <= 16 NT)
 // ==========================================================================================
@@ -1789,7 +1901,7 @@ bool lstmf_wgrad_supported(int K, int H, int N) { return H == FH && N == FG && (
 
 // HFREP_LSTMF_WGRAD=1 / 2: force the exact-fp32 MFMA kernel / the three-term bf16 split; default (0):
 // the split for K <= 36 (12.1 -> 10.8 ms at 12.6 M rows), the exact kernel for K = 100, where the split
-// kernel's 28-tile waves spill (36.5 vs 16.4 ms; profiles/r02_hazard/wgrad_split_vs_exact_v1.jsonl)
+// kernel's 28-tile waves spill (36.5 vs 16.4 ms; profiles/r02_split/wgrad_split_vs_exact_v1.jsonl)
 static int wgradf_version() {
   static const int v = [] {
     const char* e = getenv("HFREP_LSTMF_WGRAD");
@@ -1845,8 +1957,42 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
 
 bool lstmf_dgrad_supported(int N, int KO) { return N == FG && KO >= 1 && KO <= 16 * FNT; }
 
-bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s) {
+// HFREP_LSTMF_DGRAD_IMPL=2: the three-term bf16 split kernel; default 1: the exact-fp32 MFMA kernel
+// (the split one measured slower: 5.76 vs 4.69 ms at 6.3 M rows, KO = 100; 3.56 vs 2.28 at KO = 32 --
+// 16-row tiles with a barrier and an 8-wave reduction each do not hide the dZ stream;
+// profiles/r02_split/dgrad_split_vs_exact.jsonl)
+static int dgradf_version() {
+  static const int v = [] {
+    const char* e = getenv("HFREP_LSTMF_DGRAD_IMPL");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl) {
   if (!lstmf_dgrad_supported(N, KO) || M <= 0) return false;
+  if ((impl == 1 || impl == 2 ? impl : dgradf_version()) == 2) {
+    const int chunks = (M + 15) / 16, cus = device_cu_count();
+    int grid = chunks < cus ? chunks : cus;
+    const int min_grid = (int)(((long long)M * FG * 4 + (1ll << 31) - 1) / (1ll << 31));
+    if (grid < min_grid) grid = min_grid;
+    const int rpw = (chunks + grid - 1) / grid * 16;
+    const int z = (M + rpw - 1) / rpw;
+    auto go = [&](auto k, int nt) {
+      allow_lds(reinterpret_cast<const void*>(k));
+      hipLaunchKernelGGL(k, dim3(z), dim3(512), (size_t)2 * 8 * nt * 64 * 16, s, D, W, X, M, KO, rpw);
+    };
+    switch ((KO + 15) / 16) {
+      case 1: go(lstmf_dgrad_split_kernel<1>, 1); break;
+      case 2: go(lstmf_dgrad_split_kernel<2>, 2); break;
+      case 3: go(lstmf_dgrad_split_kernel<3>, 3); break;
+      case 4: go(lstmf_dgrad_split_kernel<4>, 4); break;
+      case 5: go(lstmf_dgrad_split_kernel<5>, 5); break;
+      case 6: go(lstmf_dgrad_split_kernel<6>, 6); break;
+      default: go(lstmf_dgrad_split_kernel<7>, 7); break;
+    }
+    return true;
+  }
   // one workgroup per CU (two for NT <= 3: HBM-bound there, and the registers allow a second one
   // in flight); more only if a workgroup's dZ range would pass 2 GB (32-bit buffer offsets)
   const int chunks = (M + 15) / 16, cus = device_cu_count() * (KO <= 48 ? 2 : 1);

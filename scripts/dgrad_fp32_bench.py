@@ -35,13 +35,16 @@ def main():
         for KO in (100, 32):
             W = torch.randn(KO, 400, device=dev, generator=g) * 0.1
             fl = 2.0 * M * 400 * KO
-            t_n = timeit(lambda: ops.lstmf_dgrad(dz, W))
+            t_n = timeit(lambda: ops.lstmf_dgrad(dz, W, 1))
+            t_s = timeit(lambda: ops.lstmf_dgrad(dz, W, 2))
             t_t = timeit(lambda: torch.mm(dz, W.t()))
-            diff = (ops.lstmf_dgrad(dz, W) - torch.mm(dz, W.t())).abs().max().item()
+            diff = (ops.lstmf_dgrad(dz, W, 1) - torch.mm(dz, W.t())).abs().max().item()
+            diff_s = (ops.lstmf_dgrad(dz, W, 2) - ops.lstmf_dgrad(dz, W, 1)).abs().max().item()
             print(json.dumps({"op": "lstmf_dgrad", "M": M, "KO": KO, "native_ms": round(t_n, 3),
-                              "hipblaslt_ms": round(t_t, 3), "native_tf": round(fl / t_n / 1e9, 1),
-                              "hipblaslt_tf": round(fl / t_t / 1e9, 1),
-                              "native_GBs": round(M * 400 * 4 / t_n / 1e6, 0), "maxdiff": diff}), flush=True)
+                              "split_ms": round(t_s, 3), "hipblaslt_ms": round(t_t, 3),
+                              "native_tf": round(fl / t_n / 1e9, 1), "split_tf": round(fl / t_s / 1e9, 1),
+                              "hipblaslt_tf": round(fl / t_t / 1e9, 1), "split_GBs": round(M * 400 * 4 / t_s / 1e6, 0),
+                              "maxdiff": diff, "split_vs_exact_maxdiff": diff_s}), flush=True)
         del dz
         torch.cuda.empty_cache()
 

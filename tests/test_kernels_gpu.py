@@ -813,17 +813,23 @@ def test_lstmf_wgrad_large_m(cuda, K, tangent):
 
 @pytest.mark.parametrize("M,KO", [(1, 100), (17, 32), (1000, 100), (4099, 36), (20000, 100), (333, 7), (100000, 112)])
 def test_lstmf_dgrad(cuda, M, KO):
-    """fp32 LSTM input gradient dZ W^T (register-resident k-split kernel) vs fp64, bitwise
-    run-to-run, including partial row chunks and column tiles."""
+    """fp32 LSTM input gradient dZ W^T, the exact-fp32 kernel and the three-term bf16 split kernel,
+    vs fp64, bitwise run-to-run, including partial row chunks and column tiles."""
     from hfrep.ops import _native
 
     g = torch.Generator().manual_seed(29)
     dz, W = torch.randn(M, 400, generator=g), torch.randn(KO, 400, generator=g) * 0.1
-    out = _native.native().lstmf_dgrad(dz.to(cuda), W.to(cuda))
     ref = dz.double() @ W.double().t()
-    _close(out, ref, torch.float32, scale=(dz.abs().double() @ W.abs().double().t()).max().item())
-    again = _native.native().lstmf_dgrad(dz.to(cuda), W.to(cuda))
-    assert torch.equal(out, again)
+    scale = (dz.abs().double() @ W.abs().double().t()).max().item()
+    errs = {}
+    for impl in (1, 2):  # exact-fp32 MFMA kernel, three-term bf16 split kernel (the default)
+        out = _native.native().lstmf_dgrad(dz.to(cuda), W.to(cuda), impl)
+        _close(out, ref, torch.float32, scale=scale)
+        again = _native.native().lstmf_dgrad(dz.to(cuda), W.to(cuda), impl)
+        assert torch.equal(out, again)
+        errs[impl] = (out.double().cpu() - ref).abs().max().item()
+    # the split's dropped terms are <= 2^-24 of each product: within 2x the exact kernel's error
+    assert errs[2] <= 2 * errs[1] + 1e-6 * scale, errs
 
 
 def test_gan_eval_device_path(cuda):
