@@ -10,7 +10,10 @@ the whole-job aggregate over all ranks.
 Model: the reference architecture at the north-star shape — generator LSTM(100, sigmoid) -> LN ->
 LSTM(100, sigmoid) -> LeakyReLU -> LN -> Dense(32); critic LSTM(100) -> LSTM(100) -> Flatten ->
 Dense(1); random init; synthetic return windows (no dataset/network on the box); compute dtype
-fp32 (the reference's Keras float32; exact-f32 MFMA) for the headline record, and a bf16 sub-record
+fp32 (the reference's Keras float32: fp32 storage and accumulation, products on the exact-f32 MFMA
+except the first LSTM layer's weight gradient, which splits each fp32 operand exactly into three
+bf16 terms -- six products, error at the fp32 rounding level, tests/test_kernels_gpu.py
+test_lstmf_wgrad_split_vs_exact) for the headline record, and a bf16 sub-record
 (bf16 MFMA with fp32 accumulation, fp32 master weights / optimizer) of the same config.
 
 Usage:
