@@ -260,16 +260,21 @@ def test_optimizers_match_cpu(cuda):
         assert og.iterations.item() == 4
 
 
-@pytest.mark.parametrize("key", [("lstm", "wgan_gp"), ("mlp", "wgan_gp"), ("lstm", "wgan"), ("mlp", "gan"),
-                                 ("lstm", "gan"), ("conv", "wgan_gp"), ("lstm_ln", "wgan_gp")])
-def test_trainer_gradients_gpu_vs_cpu(cuda, key):
-    """The full explicit critic/generator gradient programs on GPU (native kernels) vs CPU fp64."""
+@pytest.mark.parametrize("key,T,F,lrelu", [(("lstm", "wgan_gp"), 24, 32, False), (("mlp", "wgan_gp"), 24, 32, False),
+                                           (("lstm", "wgan"), 24, 32, False), (("mlp", "gan"), 24, 32, False),
+                                           (("lstm", "gan"), 24, 32, False), (("conv", "wgan_gp"), 24, 32, False),
+                                           (("lstm_ln", "wgan_gp"), 24, 32, False),
+                                           (("lstm", "wgan_gp"), 168, 36, True)])
+def test_trainer_gradients_gpu_vs_cpu(cuda, key, T, F, lrelu):
+    """The full explicit critic/generator gradient programs on GPU (native fp32 kernels) vs CPU fp64,
+    incl. the production generator shape (T = 168, F = 36, LeakyReLU after the first LSTM)."""
     from hfrep.train.gan_trainer import GANConfig, GANTrainer
 
-    T, F, B = 24, 32, 48
+    B = 48
     ds = np.random.RandomState(0).rand(64, T, F).astype(np.float32)
-    cfg_g = GANConfig(arch=key[0], loss=key[1], window=T, features=F, batch_size=B, dtype="float32")
-    cfg_c = GANConfig(arch=key[0], loss=key[1], window=T, features=F, batch_size=B, dtype="float64")
+    kw = dict(arch=key[0], loss=key[1], window=T, features=F, batch_size=B, lrelu_after_first=lrelu)
+    cfg_g = GANConfig(dtype="float32", **kw)
+    cfg_c = GANConfig(dtype="float64", **kw)
     tg = GANTrainer(cfg_g, ds, device=cuda)
     tc = GANTrainer(cfg_c, ds, param_dtype=torch.float64)
     with torch.no_grad():
@@ -888,6 +893,8 @@ def test_bench_scale_gradients_are_slice_averages(cuda, dtype, B):
     with torch.no_grad():
         fake = tr.generator.predict(noise)
         full = grads(tr.critic, tr.critic_gp_grads, real, fake, alpha)
+        # run-to-run bitwise at the full batch (the store-data hazard made reruns differ at 2 x 262k rows)
+        assert torch.equal(full, grads(tr.critic, tr.critic_gp_grads, real, fake, alpha)), "critic rerun differs"
         avg = sum(grads(tr.critic, tr.critic_gp_grads, sl(real, i), sl(fake, i), sl(alpha, i)) for i in range(S)) / S
         rel = ((full - avg).norm() / avg.norm()).item()
         assert torch.isfinite(full).all() and rel < tol, (f"critic: full-batch vs slice-average rel {rel:.2e}",
