@@ -160,8 +160,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            # fp32 = the reference's precision (Keras float32): exact-f32 MFMA (v_mfma_f32_16x16x4_f32),
-            # fp32 activations, tapes, gradients and optimizer state
+            # fp32 = the reference's precision (Keras float32): fp32 activations, tapes, gradients and
+            # optimizer state; products on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32) except the
+            # K <= 36 LSTM weight gradient (exact three-term bf16 split, fp32-rounding-level error)
             "dtype": "fp32" if primary == "float32" else "bf16",
             "data": "synthetic",
             "config": {
