@@ -1272,21 +1272,28 @@ lstmf_wgrad_kernel(const float* __restrict__ X, const float* __restrict__ Hs, co
 // result matches the exact-fp32 kernel to fp32 reduction noise (test_lstmf_wgrad_split_*), at 6/16
 // of its matrix-pipe time.
 //
-// Work split: a workgroup PAIR shares a row range z and splits the 400 gate columns (jh = 0: columns
-// 0..207, jh = 1: 208..399 + a zero tile); the pair sits on one XCD (blocks b and b + 8), so the A
-// rows [x | h_{t-1} | 1] both read come from the same L2.  Per 32-row chunk the workgroup stages the
-// three bf16 planes of A (32 x 208) and of its D half (32 x 208) in LDS, double-buffered (2 x 78 KB):
-// the next chunk's fp32 rows are loaded into registers before the MFMAs and split into the other
-// buffer after them, one barrier per chunk.  MFMA operands come from ds_read_b64_tr_b16 (row-major
-// image, hardware transpose: lane 4q + p of a 16-lane group addresses row q, columns 4p..4p+3).
-// 8 waves: wave w owns i-tiles [0, 7) or [7, NI) (w >> 2) times a group of 4 / 3 / 3 / 3 local
-// j-tiles (reversed for w >= 4 so each SIMD's two waves carry ~equal MFMA counts); its B fragments
-// (all three planes of its <= 4 j-tiles) stay in registers for the chunk, the A fragments stream.
-constexpr int WS_C = 208, WS_ROWB = WS_C * 2, WS_PLANE = 32 * WS_ROWB;  // bytes: one bf16 plane image
-constexpr int WS_IMG = 3 * WS_PLANE;                                    // three planes
-constexpr int WS_BUF = 2 * WS_IMG;                                      // A image + D image
+// Work split: a workgroup PAIR shares a row range z and splits the 400 gate columns in two parts of
+// 208 (13 j-tiles; the second part 192 + 1 zero tile); the pair sits on one XCD (blocks b, b + 8), so
+// the A rows [x | h_{t-1} | 1] both read come from the same L2.  Per 32-row chunk the workgroup
+// stages the three bf16 planes of A (32 x 208) and of its D part (32 x 208) in LDS, double-buffered
+// (2 x 78 KB): the next chunk's fp32 rows are loaded into registers before the MFMAs
+// and split into the other buffer after them, one barrier per chunk.  MFMA operands come from
+// ds_read_b64_tr_b16 (row-major image, hardware transpose: lane 4q + p of a 16-lane group addresses
+// row q, columns 4p..4p+3).  8 waves: wave w owns i-tiles [0, NI0) or [NI0, NI) (w >> 2) times a
+// group of 4 / 3 / 3 / 3 local j-tiles (reversed for w >= 4 so each SIMD's two waves carry ~equal
+// MFMA counts); its B fragments (all three planes of its <= 3 j-tiles) stay in registers for the
+// chunk, the A fragments stream: every operand is read from LDS once per wave.  (A three-part
+// column split was measured slower: profiles/r02_split.)
+constexpr int WS_CA = 208, WS_CD = 208;                   // image columns (A, D part)
+constexpr int WS_ROWA = WS_CA * 2, WS_ROWD = WS_CD * 2;   // bytes per image row
+constexpr int WS_PLA = 32 * WS_ROWA, WS_PLD = 32 * WS_ROWD;  // bytes per plane
+constexpr int WS_IMGD = 3 * WS_PLA;                       // D image offset in a buffer
+constexpr int WS_BUF = 3 * WS_PLA + 3 * WS_PLD;           // one buffer: A + D images (79,872 B)
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) char lds_char;
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 template <int KX>
 struct WSGeo {
@@ -1294,8 +1301,8 @@ struct WSGeo {
   static constexpr int NI = (KR + 15) / 16;       // i-tiles
   static constexpr int NI0 = (NI + 1) / 2;        // i-tiles of waves 0..3
   static constexpr int JX = (32 * KX / 4 + 511) / 512, JH = (32 * FH / 4 + 511) / 512;  // float4 slots per thread
-  static constexpr int JD = (32 * 52 + 511) / 512;  // D slots: 52 float4 per row (jh = 1 uses 48)
-  static_assert(KX % 4 == 0 && 16 * NI <= WS_C, "wgrad split: K");
+  static constexpr int JD = (32 * 52 + 511) / 512;  // D slots: 52 float4 per row (the second part uses 48)
+  static_assert(KX % 4 == 0 && 16 * NI <= WS_CA, "wgrad split: K");
 };
 
 // three bf16 planes of four fp32 values, packed two per dword
@@ -1321,60 +1328,56 @@ __device__ __forceinline__ void split3(const f32x4 v, uint32_t (&p)[3][2]) {
   }
 }
 
-// one 16x16x32 operand (8 bf16) of plane image `img` (byte offset in LDS) at column block c0:
-// two transposed reads (rows 8 G + q and 8 G + 4 + q of this lane's group G)
-__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int lane_off, int c0) {
-  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + lane_off + c0 * 2));
-  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + lane_off + 4 * WS_ROWB + c0 * 2));
+// one 16x16x32 operand (8 bf16) of a plane image (row stride ROWB) at column block c0: two
+// transposed reads (rows 8 G + q and 8 G + 4 + q of this lane's group G); lane_off = the lane's
+// (8 G + q) ROWB + 8 p
+template <int ROWB>
+__device__ __forceinline__ bf16x8 tr_frag(const lds_char* img, int lane_off, int c0) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + lane_off + c0 * 2));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + lane_off + 4 * ROWB + c0 * 2));
   return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 __device__ __forceinline__ f32x4 mma32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// one chunk's products for NIV i-tiles x NJV j-tiles of a wave (acc[ii][jj], ii < NIV, jj < NJV):
-// two passes over the i-tiles, each with the three B planes of (up to) two j-tiles in registers and
-// the A fragments streamed one i-tile ahead.  Each tile's six products go to a fresh accumulator
-// that is added to the running sum in VALU fp32 (round to nearest): chaining them straight into the
-// running sum on the matrix pipe drifted (3 M rows: 0.043 vs 0.014 for the exact kernel, consistent
-// with a biased rounding of the MFMA's C addition).
+// one chunk's products for NIV i-tiles x NJV j-tiles of a wave (acc[ii][jj]): the B planes of the
+// NJV j-tiles in registers, the A fragments one i-tile ahead.  Each tile's six products go to a
+// fresh accumulator that is added to the running sum in VALU fp32 (round to nearest): chaining them
+// straight into the running sum on the matrix pipe drifted (3 M rows: 0.043 vs 0.014 for the exact
+// kernel, consistent with a biased rounding of the MFMA's C addition).  Straight-line code (one
+// instantiation per wave shape): with a wave-uniform branch between an MFMA and the VALU read of its
+// result the compiler did not count the wait states across the branch (2 instead of >= 7).
 template <int NIV, int NJV, int NA, int NB>
-__device__ __forceinline__ void ws_chunk(f32x4 (&acc)[NA][NB], const char* A_, const char* D_, int tr_off, int i0, int j0) {
+__device__ __forceinline__ void ws_chunk(f32x4 (&acc)[NA][NB], const lds_char* A_, const lds_char* D_, int tro_a,
+                                         int tro_d, int i0, int j0) {
+  bf16x8 bfr[NJV][3];
 #pragma unroll
-  for (int jp = 0; jp < 2; ++jp) {
-    constexpr int dummy = 0;
-    (void)dummy;
-    const int nb = NJV - 2 * jp < 2 ? NJV - 2 * jp : 2;  // compile-time after unrolling
-    bf16x8 bfr[2][3];
+  for (int jj = 0; jj < NJV; ++jj)
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj)
+    for (int q = 0; q < 3; ++q) bfr[jj][q] = tr_frag<WS_ROWD>(D_ + q * WS_PLD, tro_d, 16 * (j0 + jj));
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
-        if (jj < nb) bfr[jj][q] = tr_frag(D_ + q * WS_PLANE, tr_off, 16 * (j0 + 2 * jp + jj));
-    bf16x8 af[2][3];
+  for (int ii = 0; ii < NIV; ++ii) {
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 a3[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) af[0][q] = tr_frag(A_ + q * WS_PLANE, tr_off, 16 * i0);
+    for (int q = 0; q < 3; ++q) a3[q] = tr_frag<WS_ROWA>(A_ + q * WS_PLA, tro_a, 16 * (i0 + ii));
+    // j-tiles in pairs: two fresh accumulators in flight, added after both chains
 #pragma unroll
-    for (int ii = 0; ii < NIV; ++ii) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (ii + 1 < NIV) {
+    for (int j2 = 0; j2 < NJV; j2 += 2) {
+      f32x4 t[2];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) af[(ii + 1) & 1][q] = tr_frag(A_ + q * WS_PLANE, tr_off, 16 * (i0 + ii + 1));
+      for (int jj = j2; jj < j2 + 2 && jj < NJV; ++jj) {
+        f32x4& u = t[jj - j2];
+        u = mma32(a3[2], bfr[jj][0], f32x4{0.f, 0.f, 0.f, 0.f});  // lh
+        u = mma32(a3[0], bfr[jj][2], u);                        // hl
+        u = mma32(a3[1], bfr[jj][1], u);                        // mm
+        u = mma32(a3[1], bfr[jj][0], u);                        // mh
+        u = mma32(a3[0], bfr[jj][1], u);                        // hm
+        u = mma32(a3[0], bfr[jj][0], u);                        // hh
       }
-      const bf16x8(&a3)[3] = af[ii & 1];
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        if (jj < nb) {
-          f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
-          t = mma32(a3[2], bfr[jj][0], t);  // lh
-          t = mma32(a3[0], bfr[jj][2], t);  // hl
-          t = mma32(a3[1], bfr[jj][1], t);  // mm
-          t = mma32(a3[1], bfr[jj][0], t);  // mh
-          t = mma32(a3[0], bfr[jj][1], t);  // hm
-          t = mma32(a3[0], bfr[jj][0], t);  // hh
-          acc[ii][2 * jp + jj] += t;
-        }
-      }
+      for (int jj = j2; jj < j2 + 2 && jj < NJV; ++jj) acc[ii][jj] += t[jj - j2];
     }
   }
 }
@@ -1386,10 +1389,11 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
                          float* __restrict__ slab, int M, int Tn, int rows_per_z, int Z) {
   using G = WSGeo<KX>;
   constexpr int NI = G::NI, NI0 = G::NI0, JX = G::JX, JH = G::JH, JD = G::JD;
-  extern __shared__ __attribute__((aligned(16))) char wsm[];
+  extern __shared__ __attribute__((aligned(16))) char wsm_[];
+  lds_char* wsm = (lds_char*)wsm_;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // block -> (row range z, column half jh); with Z % 8 == 0 the pair shares an XCD
+  // block -> (row range z, column part jh); with Z % 8 == 0 the pair shares an XCD
   int z, jh;
   if (Z % 8 == 0) {
     const int slot = blockIdx.x >> 3;
@@ -1400,15 +1404,15 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
     z = blockIdx.x >> 1;
   }
   const int mb = z * rows_per_z, me = min(M, mb + rows_per_z);
-  const int jbase = 208 * jh, nd4 = jh ? 48 : 52;  // D columns of this half, float4 per row
+  const int jbase = WS_CD * jh, nd4 = jh ? 48 : 52;  // D columns of this part, float4 per row
 
-  // wave tiles
+  // wave tiles: i-half ig, j-group jg (4 / 3 / 3 / 3 of the 13 local j-tiles)
   const int ig = w >> 2, jg = ig ? 3 - (w & 3) : (w & 3);
   const int i0 = ig ? NI0 : 0, ni = ig ? NI - NI0 : NI0;
   const int j0 = jg == 0 ? 0 : 1 + 3 * jg, nj = jg == 0 ? 4 : 3;
 
-  // zero both buffers (pad columns, the zero j-tile of jh = 1), then the bias column (A, plane h)
-  for (int i = tid; i < 2 * WS_BUF / 16; i += 512) reinterpret_cast<uint4*>(wsm)[i] = make_uint4(0, 0, 0, 0);
+  // zero both buffers (pad columns, zero j-tiles of the last part)
+  for (int i = tid; i < 2 * WS_BUF / 16; i += 512) reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(wsm)[i] = u32x4_t{0, 0, 0, 0};
   __syncthreads();
 
   f32x4 acc[NI0][4];
@@ -1417,13 +1421,38 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // this lane's transposed-read base: row 8 G + q, column 4 p (bytes)
-  const int tr_off = (8 * (lane >> 4) + ((lane & 15) >> 2)) * WS_ROWB + 8 * (lane & 3);
+  // this lane's transposed-read bases: row 8 G + q, column 4 p (bytes)
+  const int trr = 8 * (lane >> 4) + ((lane & 15) >> 2);
+  const int tro_a = trr * WS_ROWA + 8 * (lane & 3), tro_d = trr * WS_ROWD + 8 * (lane & 3);
 
-  // per-thread float4 slots of a 32-row chunk: X (JX), H (JH), D (JD); element e = tid + 512 j of the
-  // chunk's row-major image.  Their offsets are recomputed per chunk from an opaque copy of tid (a few
-  // VALU) instead of being held in ~20 loop-invariant registers next to the accumulators.
+  // per-thread float4 slots of a 32-row chunk: X (JX), H (JH), D (JD); element e = tid + 512 j:
+  // byte offset in the chunk frame (kOOB: none), LDS byte offset (-1: none), H-slot row
+  int gx[JX], lx[JX], gh[JH], lh[JH], rhr[JH], gd[JD], ld_[JD], rd_[JD];
+#pragma unroll
+  for (int j = 0; j < JX; ++j) {
+    const int e = tid + 512 * j, r = e / (KX / 4), c4 = e - r * (KX / 4);
+    const bool ok = e < 32 * KX / 4;
+    gx[j] = ok ? (r * KX + 4 * c4) * 4 : kOOB;
+    lx[j] = ok ? r * WS_ROWA + 8 * c4 : -1;
+  }
+#pragma unroll
+  for (int j = 0; j < JH; ++j) {
+    const int e = tid + 512 * j, r = e / (FH / 4), c4 = e - r * (FH / 4);
+    const bool ok = e < 32 * FH / 4;
+    gh[j] = ok ? (r * FH + 4 * c4) * 4 : kOOB;
+    lh[j] = ok ? r * WS_ROWA + 2 * KX + 8 * c4 : -1;
+    rhr[j] = ok ? r : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < JD; ++j) {
+    const int e = tid + 512 * j, r = e / 52, c4 = e - r * 52;
+    const bool ok = e < 32 * 52 && c4 < nd4;
+    gd[j] = ok ? (r * FG + jbase + 4 * c4) * 4 : kOOB;
+    ld_[j] = ok ? WS_IMGD + r * WS_ROWD + 8 * c4 : -1;
+    rd_[j] = ok ? r : 0;
+  }
   const int step32 = 32 % Tn;
+
   f32x4 vx[JX], vh[JH], vd[JD];
   for (int seg = 0; seg < (Xd ? 2 : 1); ++seg) {
     const float* Xs = seg ? Xd : X;
@@ -1439,69 +1468,45 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
     // t = (row) mod Tn of this thread's H slots at the current chunk (h_{-1} = 0 rows)
     int tm[JH];
 #pragma unroll
-    for (int j = 0; j < JH; ++j) tm[j] = (mb + min((tid + 512 * j) / (FH / 4), 31)) % Tn;
-    auto opaque_tid = [&]() {
-      int t = tid;
-      asm volatile("" : "+v"(t));
-      return t;
-    };
+    for (int j = 0; j < JH; ++j) tm[j] = (mb + rhr[j]) % Tn;
     auto load = [&](int m0) {  // rows past me: voffset out of range, zeros
-      const int lim = me - m0, t0 = opaque_tid();
+      const int lim = me - m0;
 #pragma unroll
-      for (int j = 0; j < JX; ++j) {
-        const int e = t0 + 512 * j, r = e / (KX / 4), c4 = e - r * (KX / 4);
-        const bool ok = e < 32 * KX / 4 && r < lim;
-        vx[j] = ld4s(rx, ok ? (r * KX + 4 * c4) * 4 : kOOB, (m0 - mb) * KX * 4);
-      }
+      for (int j = 0; j < JX; ++j) vx[j] = ld4s(rx, (gx[j] >> 2) / KX < lim ? gx[j] : kOOB, (m0 - mb) * KX * 4);
 #pragma unroll
-      for (int j = 0; j < JH; ++j) {
-        const int e = t0 + 512 * j, r = e / (FH / 4), c4 = e - r * (FH / 4);
-        const bool ok = e < 32 * FH / 4 && r < lim && tm[j] != 0;
-        vh[j] = ld4s(rh, ok ? (r * FH + 4 * c4) * 4 : kOOB, (m0 - mb) * FH * 4);
-      }
+      for (int j = 0; j < JH; ++j) vh[j] = ld4s(rh, rhr[j] < lim && tm[j] != 0 ? gh[j] : kOOB, (m0 - mb) * FH * 4);
 #pragma unroll
-      for (int j = 0; j < JD; ++j) {
-        const int e = t0 + 512 * j, r = e / 52, c4 = e - r * 52;
-        const bool ok = e < 32 * 52 && c4 < nd4 && r < lim;
-        vd[j] = ld4s(rd, ok ? (r * FG + jbase + 4 * c4) * 4 : kOOB, (m0 - mb) * FG * 4);
-      }
+      for (int j = 0; j < JD; ++j) vd[j] = ld4s(rd, rd_[j] < lim ? gd[j] : kOOB, (m0 - mb) * FG * 4);
 #pragma unroll
       for (int j = 0; j < JH; ++j) {
         tm[j] += step32;
         if (tm[j] >= Tn) tm[j] -= Tn;
       }
     };
-    auto put = [&](char* dst, bool ok, const f32x4& v) {
-      if (ok) {
+    auto put = [&](lds_char* base, int lo, const f32x4& v) {
+      if (lo >= 0) {
         uint32_t p[3][2];
         split3(v, p);
+        const int pl = lo < WS_IMGD ? WS_PLA : WS_PLD;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(dst + q * WS_PLANE) = make_uint2(p[q][0], p[q][1]);
+        for (int q = 0; q < 3; ++q)
+          *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(base + lo + q * pl) = u32x2_t{p[q][0], p[q][1]};
       }
     };
     auto stage = [&](int buf) {
-      char* base = wsm + buf * WS_BUF;
-      const int t0 = opaque_tid();
+      lds_char* base = wsm + buf * WS_BUF;
 #pragma unroll
-      for (int j = 0; j < JX; ++j) {
-        const int e = t0 + 512 * j, r = e / (KX / 4), c4 = e - r * (KX / 4);
-        put(base + r * WS_ROWB + 8 * c4, e < 32 * KX / 4, vx[j]);
-      }
+      for (int j = 0; j < JX; ++j) put(base, lx[j], vx[j]);
 #pragma unroll
-      for (int j = 0; j < JH; ++j) {
-        const int e = t0 + 512 * j, r = e / (FH / 4), c4 = e - r * (FH / 4);
-        put(base + r * WS_ROWB + 2 * KX + 8 * c4, e < 32 * FH / 4, vh[j]);
-      }
+      for (int j = 0; j < JH; ++j) put(base, lh[j], vh[j]);
 #pragma unroll
-      for (int j = 0; j < JD; ++j) {
-        const int e = t0 + 512 * j, r = e / 52, c4 = e - r * 52;
-        put(base + WS_IMG + r * WS_ROWB + 8 * c4, e < 32 * 52 && c4 < nd4, vd[j]);
-      }
+      for (int j = 0; j < JD; ++j) put(base, ld_[j], vd[j]);
     };
     // bias column (column KR - 1 of A): 1 in plane h for the primal segment, 0 for the tangent one
     if (tid < 64) {
       const int buf = tid >> 5, r = tid & 31;
-      *reinterpret_cast<uint16_t*>(wsm + buf * WS_BUF + r * WS_ROWB + (G::KR - 1) * 2) = seg ? 0 : 0x3f80;
+      *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wsm + buf * WS_BUF + r * WS_ROWA + (G::KR - 1) * 2) =
+          seg ? 0 : 0x3f80;
     }
     const int nch = nr > 0 ? (nr + 31) / 32 : 0;
     if (nch > 0) {
@@ -1512,16 +1517,13 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
     for (int c = 0; c < nch; ++c) {
       const bool more = c + 1 < nch;
       if (more) load(mb + 32 * (c + 1));
-      const char* A_ = wsm + (c & 1) * WS_BUF;
-      const char* D_ = A_ + WS_IMG;
-      // straight-line MFMA code per (i-tiles, j-tiles) shape: with wave-uniform branches between an
-      // MFMA and the VALU read of its result the compiler did not count the wait states across the
-      // branch (2 instead of >= 7: stale sums)
+      const lds_char* A_ = wsm + (c & 1) * WS_BUF;
+      const lds_char* D_ = A_ + WS_IMGD;
       switch (ni * 8 + nj) {
-        case NI0 * 8 + 4: ws_chunk<NI0, 4>(acc, A_, D_, tr_off, i0, j0); break;
-        case NI0 * 8 + 3: ws_chunk<NI0, 3>(acc, A_, D_, tr_off, i0, j0); break;
-        case (NI - NI0) * 8 + 4: ws_chunk<NI - NI0, 4>(acc, A_, D_, tr_off, i0, j0); break;
-        default: ws_chunk<NI - NI0, 3>(acc, A_, D_, tr_off, i0, j0); break;
+        case NI0 * 8 + 4: ws_chunk<NI0, 4>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
+        case NI0 * 8 + 3: ws_chunk<NI0, 3>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
+        case (NI - NI0) * 8 + 4: ws_chunk<NI - NI0, 4>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
+        default: ws_chunk<NI - NI0, 3>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
       }
       if (more) stage((c + 1) & 1);
       __syncthreads();
@@ -1900,8 +1902,8 @@ static int wgradf_grid(int M) {
 bool lstmf_wgrad_supported(int K, int H, int N) { return H == FH && N == FG && (K == 32 || K == 36 || K == 100); }
 
 // HFREP_LSTMF_WGRAD=1 / 2: force the exact-fp32 MFMA kernel / the three-term bf16 split; default (0):
-// the split for K <= 36 (12.1 -> 10.8 ms at 12.6 M rows), the exact kernel for K = 100, where the split
-// kernel's 28-tile waves spill (36.5 vs 16.4 ms; profiles/r02_split/wgrad_split_vs_exact_v1.jsonl)
+// the split for K <= 36 (12.1 -> 9.8 ms at 12.6 M rows), the exact kernel for K = 100, where the split
+// kernel's 28-tile waves spill (52.8 vs 16.4 ms; profiles/r02_split)
 static int wgradf_version() {
   static const int v = [] {
     const char* e = getenv("HFREP_LSTMF_WGRAD");
