@@ -863,18 +863,19 @@ def _block_rel(model, a, b):
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
-@pytest.mark.parametrize("B", [16384, 262144])
-def test_bench_scale_gradients_are_slice_averages(cuda, dtype, B):
+@pytest.mark.parametrize("B,T,F,lrelu", [(16384, 24, 32, False), (262144, 24, 32, False), (32768, 168, 36, True)])
+def test_bench_scale_gradients_are_slice_averages(cuda, dtype, B, T, F, lrelu):
     """At the bench batch (B = 262,144: dZ of the critic's W terms is 20 GB) the critic GP and the
     generator gradients equal the average of the gradients of four row slices: every row's
     contribution is computed identically, only the reduction order differs.  Catches any kernel
-    whose addressing breaks past 2 / 4 GiB (the fp32 weight gradient did, before r02)."""
+    whose addressing breaks past 2 / 4 GiB (the fp32 weight gradient did, before r02).  Also at the
+    production generator shape (T = 168, F = 36, LeakyReLU after LSTM1: dZ 17.6 GB at 32k windows)."""
     from hfrep.train.gan_trainer import GANConfig, GANTrainer
 
-    T, F, S = 24, 32, 4
+    S = 4
     ds = np.random.RandomState(0).rand(64, T, F).astype(np.float32)
-    tr = GANTrainer(GANConfig(arch="lstm", loss="wgan_gp", window=T, features=F, batch_size=B, dtype=dtype), ds,
-                    device=cuda)
+    tr = GANTrainer(GANConfig(arch="lstm", loss="wgan_gp", window=T, features=F, batch_size=B, dtype=dtype,
+                              lrelu_after_first=lrelu), ds, device=cuda)
     dt = torch.float32 if dtype == "float32" else torch.bfloat16
     g = torch.Generator(device=cuda).manual_seed(41)
     real = torch.rand(B, T, F, device=cuda, generator=g).to(dt)
