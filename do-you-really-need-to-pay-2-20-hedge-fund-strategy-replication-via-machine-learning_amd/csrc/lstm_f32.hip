@@ -962,15 +962,43 @@ lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, 
         }
       }
     };
+    // the dz / dzdot stores ride on the MFMA role (they were 6 % of the cell role's time, which
+    // sets the half-phase length): threads 0..199 own chunk tid % 100 of rows 2 k + tid / 100; a
+    // half's rows are stable for exactly the half-phase after the one that completed them
+    const int srr = tid / 100, sch = tid - 100 * srr, sqq = sch / 25, sc = sch - 25 * sqq;
+    const int slo = (srr & 1) * BZ_LR + sqq * BZ_KQ + 4 * sc;
+    const int sgo = tid < 200 ? (srr * Tn * FG + sqq * FH + 4 * sc) * 4 : kOOB;
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
     for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+      const int row0 = rb * 32;
+      const rsrc_t rz = ftile_rsrc(dZ, row0, B, Tn, FG), rzd = ftile_rsrc(dZd, row0, B, Tn, FG);
+      const int nr = min(32, B - row0);
+      auto store_half = [&](auto M_, int ts) {
+        constexpr int M = decltype(M_)::value;
+#pragma unroll
+        for (int k = 8 * M; k < 8 * M + 8; ++k) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(zt + slo + 2 * k * BZ_LR);
+          const f32x4 vd = *reinterpret_cast<const f32x4*>(zdt + slo + 2 * k * BZ_LR);
+          const bool ok = 2 * k + srr < nr;
+          const int so = (2 * k * Tn + ts) * FG * 4;
+          st16(v, rz, ok, sgo, so);
+          st16(vd, rzd, ok, sgo, so);
+          if (k & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
       for (int i = tid; i < 2 * 32 * (BZ_LR + BH_LR); i += 512) zt[i] = 0.f;  // all four tiles
       __syncthreads();
       for (int t = Tn - 1; t >= 0; --t) {
-        half_a(std::integral_constant<int, 1>{});
+        if (t < Tn - 1) store_half(I1{}, t + 1);  // rows 16..31 of dz_{t+1}: stable during P1(t)
+        half_a(I1{});
         lds_barrier();
-        half_a(std::integral_constant<int, 0>{});
+        store_half(I0{}, t);                      // rows 0..15 of dz_t: stable during P2(t)
+        half_a(I0{});
         lds_barrier();
       }
+      store_half(I1{}, 0);
       __syncthreads();
     }
   } else {
@@ -1028,20 +1056,6 @@ lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, 
       load_half(std::integral_constant<int, 0>{}, Tn - 1, true);
       for (int i = tid; i < 2 * 32 * (BZ_LR + BH_LR); i += 512) zt[i] = 0.f;
       __syncthreads();
-      auto store_half = [&](auto M_, int ts) {
-        constexpr int M = decltype(M_)::value;
-#pragma unroll
-        for (int k = 8 * M; k < 8 * M + 8; ++k) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(zt + slo + 2 * k * BZ_LR);
-          const f32x4 vd = *reinterpret_cast<const f32x4*>(zdt + slo + 2 * k * BZ_LR);
-          const bool ok = 2 * k + srr < nr;
-          const int so = (2 * k * Tn + ts) * FG * 4;
-          st16(v, rz, ok, sgo, so);
-          st16(vd, rzd, ok, sgo, so);
-          if (k & 1) __builtin_amdgcn_sched_barrier(0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      };
       auto half_b = [&](auto M_) {
         constexpr int m = decltype(M_)::value;
 #pragma unroll
@@ -1089,18 +1103,15 @@ lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, 
       using I0 = std::integral_constant<int, 0>;
       using I1 = std::integral_constant<int, 1>;
       for (int t = Tn - 1; t >= 0; --t) {
-        if (t < Tn - 1) store_half(I1{}, t + 1);
         half_b(I0{});                             // P1(t): B(0, t)
         __builtin_amdgcn_sched_barrier(0);        //   (the load set is free only after the cells)
         load_half(I1{}, t, true);                 //   then half 1's loads for P2(t)
         lds_barrier();
-        store_half(I0{}, t);
         half_b(I1{});                             // P2(t): B(1, t)
         __builtin_amdgcn_sched_barrier(0);
         load_half(I0{}, t > 0 ? t - 1 : 0, t > 0);  //   then half 0's loads for P1(t - 1)
         lds_barrier();
       }
-      store_half(I1{}, 0);
       __syncthreads();
     }
   }
