@@ -27,7 +27,7 @@ from dataclasses import dataclass
 
 import torch
 
-from ..utils.checkpoint import load_training_state, save_training_state
+from ..utils.checkpoint import apply_training_state, load_training_state, read_training_state, save_training_state
 from ..utils.logger import AsyncScalars, JSONLLogger
 
 
@@ -93,11 +93,22 @@ class GraphedStep:
         self.graph = None
 
     def _capture(self):
+        """Capture one step.
+
+        The capture runs in THREAD-LOCAL mode: ProcessGroupNCCL's watchdog thread keeps polling
+        the events of the warmup steps' collectives (``WorkNCCL::isCompleted`` ->
+        ``hipEventQuery``), and in the default global mode any such query from another thread
+        while a stream captures is illegal -- the watchdog then takes the process down (the
+        round-2 driver run of tests/test_gpu_rccl.py).  Thread-local mode only forbids unsafe
+        calls on the capturing thread.  Every outstanding bucket is joined and the device drained
+        first, so no eager collective is still in flight when the capture starts."""
         t = self.t
+        if t.grad_sync is not None:
+            t.grad_sync.finish_()
         torch.cuda.synchronize()
         it = t.iteration
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             t.train_step()
         t.iteration = it  # capture recorded the step, it did not run it
 
@@ -127,9 +138,14 @@ def _log_tensors(trainer, nan_guard: bool) -> dict:
     import torch.distributed as dist
 
     ok = (torch.isfinite(d).all() & torch.isfinite(g).all()).to(d.dtype).reshape(1)
-    # a non-finite rank contributes zeros to the mean (its flag reports it)
-    pack = torch.cat([torch.nan_to_num(d, nan=0.0, posinf=0.0, neginf=0.0),
-                      torch.nan_to_num(g.to(d.dtype), nan=0.0, posinf=0.0, neginf=0.0), ok])
+    if nan_guard:
+        # the run stops at this record anyway: a non-finite rank contributes zeros to the logged
+        # mean and its flag (summed below) reports it
+        pack = torch.cat([torch.nan_to_num(d, nan=0.0, posinf=0.0, neginf=0.0),
+                          torch.nan_to_num(g.to(d.dtype), nan=0.0, posinf=0.0, neginf=0.0), ok])
+    else:
+        # unguarded runs log the raw mean, so a diverged rank shows up as NaN / Inf in the record
+        pack = torch.cat([d, g.to(d.dtype), ok])
     dist.all_reduce(pack, op=dist.ReduceOp.SUM, group=trainer.grad_sync.group)
     nd, ng, w = d.numel(), g.numel(), float(trainer.world)
     out = {"d": pack[:nd] / w, "g": pack[nd:nd + ng] / w}
@@ -139,9 +155,9 @@ def _log_tensors(trainer, nan_guard: bool) -> dict:
 
 
 def resolve_resume(opts: RunOptions, trainer) -> str | None:
-    """Checkpoint path to resume from.  Under data parallelism rank 0 resolves it and broadcasts
-    the path, so every rank loads the same iteration even when ``ckpt_dir`` is rank-local or
-    rank 0 is rotating files."""
+    """Checkpoint path to resume from.  Under data parallelism rank 0 resolves it (it is the rank
+    that writes checkpoints) and broadcasts the path, so every rank resumes the same iteration even
+    while rank 0 rotates files."""
     if not opts.resume:
         return None
     if opts.resume == "auto" and not opts.ckpt_dir:
@@ -156,6 +172,29 @@ def resolve_resume(opts: RunOptions, trainer) -> str | None:
         dist.broadcast_object_list(box, src=0, group=trainer.grad_sync.group)
         path = box[0]
     return path
+
+
+def resume_state(path: str, trainer) -> None:
+    """Load the training state at ``path`` on every rank.
+
+    With a shared checkpoint directory each rank reads the file itself.  When some rank cannot see
+    it (``ckpt_dir`` is local to rank 0's node or filesystem), rank 0 reads it and broadcasts the
+    state, so a rank-local ``ckpt_dir`` works too."""
+    if trainer.grad_sync is None or trainer.world <= 1:
+        load_training_state(path, trainer)
+        return
+    import torch.distributed as dist
+
+    seen = torch.tensor([1.0 if os.path.exists(path) else 0.0], dtype=torch.float64)
+    if trainer.grad_sync.backend == "nccl":
+        seen = seen.to(trainer.device)
+    dist.all_reduce(seen, op=dist.ReduceOp.MIN, group=trainer.grad_sync.group)
+    if float(seen.item()) > 0.5:
+        load_training_state(path, trainer)
+        return
+    box = [read_training_state(path) if trainer.rank == 0 else None]
+    dist.broadcast_object_list(box, src=0, group=trainer.grad_sync.group)
+    apply_training_state(box[0], trainer)
 
 
 def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[dict]:
@@ -182,7 +221,7 @@ def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[di
 
     path = resolve_resume(opts, trainer)
     if path:
-        load_training_state(path, trainer)
+        resume_state(path, trainer)
         logger.log({"event": "resumed", "path": path, "iteration": trainer.iteration})
     step = GraphedStep(trainer) if opts.graph else trainer.train_step
     snap = AsyncScalars()
@@ -201,8 +240,9 @@ def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[di
                 t_last, it_last = now, it
                 emit(snap.snapshot(meta, **_log_tensors(trainer, opts.nan_guard)))
             if opts.ckpt_dir and opts.ckpt_every and it % opts.ckpt_every == 0:
+                states = _gather_host_rng(trainer)
                 if trainer.rank == 0:
-                    _checkpoint(trainer, opts)
+                    _checkpoint(trainer, opts, states)
                 if trainer.grad_sync is not None and trainer.world > 1:
                     import torch.distributed as dist
 
@@ -214,10 +254,21 @@ def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[di
     return records
 
 
-def _checkpoint(trainer, opts: RunOptions) -> str:
+def _gather_host_rng(trainer):
+    """Every rank's host-RNG state (None with the device counter RNG or a single process)."""
+    if trainer.rng.native or trainer.grad_sync is None or trainer.world <= 1:
+        return None
+    import torch.distributed as dist
+
+    states = [None] * trainer.world
+    dist.all_gather_object(states, trainer.rng.gen.get_state(), group=trainer.grad_sync.group)
+    return states
+
+
+def _checkpoint(trainer, opts: RunOptions, rng_states=None) -> str:
     os.makedirs(opts.ckpt_dir, exist_ok=True)
     path = os.path.join(opts.ckpt_dir, f"state_{trainer.iteration:09d}.pt")
-    save_training_state(path, trainer)
+    save_training_state(path, trainer, rng_states)
     old = sorted(glob.glob(os.path.join(opts.ckpt_dir, "state_*.pt")))[:-opts.keep]
     for p in old:
         os.remove(p)

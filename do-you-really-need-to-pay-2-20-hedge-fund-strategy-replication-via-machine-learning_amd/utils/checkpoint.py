@@ -101,7 +101,10 @@ def load_windows(path: str) -> np.ndarray:
 # ---------------------------------------------------------------------------------------------
 # full training state (resume)
 # ---------------------------------------------------------------------------------------------
-def save_training_state(path: str, trainer) -> str:
+def save_training_state(path: str, trainer, rng_states_by_rank=None) -> str:
+    """``rng_states_by_rank``: under data parallelism with the host (torch.Generator) RNG, every
+    rank's generator state (gathered by the caller), so each rank resumes its OWN stream; the
+    device Philox counter is identical on all ranks and needs no such list."""
     opt = trainer.opt
     st = {
         "format": "hfrep-train-state-v1",
@@ -114,6 +117,7 @@ def save_training_state(path: str, trainer) -> str:
         "opt_slots_critic": list(opt._slots(trainer.critic.flat)),
         "rng_ctr": trainer.rng.ctr.detach().cpu() if trainer.rng.native else torch.zeros(1, dtype=torch.int64),
         "rng_gen_state": (trainer.rng.gen.get_state() if not trainer.rng.native else torch.zeros(0, dtype=torch.uint8)),
+        "rng_gen_states_by_rank": list(rng_states_by_rank or []),
         "config_json": torch.tensor(list(json.dumps(trainer.cfg.__dict__, default=str).encode()), dtype=torch.uint8),
     }
     st["opt_slots_generator"] = [s.detach().cpu() for s in st["opt_slots_generator"]]
@@ -124,9 +128,17 @@ def save_training_state(path: str, trainer) -> str:
     return path
 
 
-def load_training_state(path: str, trainer) -> None:
+def read_training_state(path: str) -> dict:
     st = torch.load(path, weights_only=True, map_location="cpu")
     assert st["format"] == "hfrep-train-state-v1"
+    return st
+
+
+def load_training_state(path: str, trainer) -> None:
+    apply_training_state(read_training_state(path), trainer)
+
+
+def apply_training_state(st: dict, trainer) -> None:
     with torch.no_grad():
         trainer.generator.flat.copy_(st["generator"].to(trainer.generator.flat))
         trainer.critic.flat.copy_(st["critic"].to(trainer.critic.flat))
@@ -137,6 +149,9 @@ def load_training_state(path: str, trainer) -> None:
         opt.load_slots(trainer.critic.flat, st["opt_slots_critic"])
         if trainer.rng.native:
             trainer.rng.ctr.copy_(st["rng_ctr"].to(trainer.rng.ctr))
-        elif st["rng_gen_state"].numel():
-            trainer.rng.gen.set_state(st["rng_gen_state"])
+        else:
+            by_rank = st.get("rng_gen_states_by_rank") or []
+            gs = by_rank[trainer.rank] if trainer.rank < len(by_rank) else st["rng_gen_state"]
+            if gs.numel():
+                trainer.rng.gen.set_state(gs)
     trainer.iteration = int(st["iteration"])

@@ -14,6 +14,7 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from _spawn import gather
 
 
 def _free_port():
@@ -71,12 +72,9 @@ def test_dp_gloo_matches_single_process(world):
     for p in procs:
         p.start()
     res = {}
-    for _ in range(world):
-        r, v = q.get(timeout=300)
+    for r, v in gather(procs, q, world, timeout=300):
         assert not isinstance(v, str), v
         res[r] = v
-    for p in procs:
-        p.join(timeout=60)
 
     # single-process reference on the full global batch
     import hfrep  # noqa: F401
@@ -147,12 +145,9 @@ def test_dp_runner_averages_logged_losses_and_resumes_consistently(tmp_path):
     for p in procs:
         p.start()
     res = {}
-    for _ in range(world):
-        r, v = q.get(timeout=300)
+    for r, v in gather(procs, q, world, timeout=300):
         assert not isinstance(v, str), v
         res[r] = v
-    for p in procs:
-        p.join(timeout=60)
     assert res[0]["losses"] == res[1]["losses"]
     last = res[0]["losses"][-1][0]
     mean_local = 0.5 * (res[0]["local_last"][0] + res[1]["local_last"][0])
@@ -160,3 +155,57 @@ def test_dp_runner_averages_logged_losses_and_resumes_consistently(tmp_path):
     assert res[0]["local_last"][0] != res[1]["local_last"][0]
     assert res[0]["resumed_at"] == res[1]["resumed_at"] == 5
     np.testing.assert_array_equal(res[0]["params"], res[1]["params"])
+
+
+def _local_ckpt_worker(rank, world, port, base, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        import hfrep  # noqa: F401
+        from hfrep.parallel.dp import init_distributed
+        from hfrep.train.gan_trainer import GANConfig, GANTrainer
+        from hfrep.train.runner import RunOptions, run
+
+        r, _, w, pg = init_distributed(backend="gloo")
+        ds = np.random.RandomState(0).rand(30, 6, 4)
+        ckdir = os.path.join(base, f"rank{r}")  # rank-LOCAL: only rank 0's directory gets files
+
+        def trainer():
+            cfg = GANConfig(arch="lstm", loss="wgan_gp", window=6, features=4, batch_size=4, hidden=8, dtype="float64")
+            return GANTrainer(cfg, ds, process_group=pg, rank=r, world=w, param_dtype=torch.float64)
+
+        full = trainer()
+        run(full, RunOptions(epochs=6, log_every=1, echo=False))
+        a = trainer()
+        run(a, RunOptions(epochs=4, log_every=1, echo=False, ckpt_dir=ckdir, ckpt_every=4))
+        b = trainer()
+        recs = run(b, RunOptions(epochs=6, log_every=1, echo=False, ckpt_dir=ckdir, resume="auto"))
+        q.put((r, {"resumed_at": recs[0]["iteration"], "files": sorted(os.listdir(ckdir)) if os.path.isdir(ckdir) else [],
+                   "params": torch.cat([b.generator.flat.detach(), b.critic.flat.detach()]).numpy(),
+                   "full": torch.cat([full.generator.flat.detach(), full.critic.flat.detach()]).numpy()}))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+
+
+def test_dp_resume_from_rank_local_checkpoint_dir(tmp_path):
+    """ckpt_dir visible to rank 0 only: rank 0 reads the state and broadcasts it; the resumed run
+    continues bitwise like an uninterrupted one on every rank."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_local_ckpt_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for r, v in gather(procs, q, world, timeout=300):
+        assert not isinstance(v, str), v
+        res[r] = v
+    assert res[1]["files"] == [] and res[0]["files"]
+    assert res[0]["resumed_at"] == res[1]["resumed_at"] == 5
+    for r in range(world):
+        np.testing.assert_array_equal(res[r]["params"], res[r]["full"])

@@ -17,7 +17,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _worker(port, graph, q):
+def _worker(port, graph, key, q):
     try:
         import os
 
@@ -35,7 +35,7 @@ def _worker(port, graph, q):
         torch.cuda.set_device(dev)
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
         ds = np.random.RandomState(0).rand(256, 24, 32).astype(np.float32)
-        cfg = dict(arch="lstm", loss="wgan_gp", window=24, features=32, batch_size=64, dtype="float32")
+        cfg = dict(arch=key[0], loss=key[1], window=24, features=32, batch_size=64, dtype="float32")
         ref = GANTrainer(GANConfig(**cfg), ds, device=dev)
         syn = GANTrainer(GANConfig(**cfg), ds, device=dev)
         syn.grad_sync = GradSync(dist.group.WORLD, 2, buckets=2)
@@ -55,8 +55,10 @@ def _worker(port, graph, q):
         q.put(traceback.format_exc())
 
 
-def _run(graph):
+def _run(graph, key=("lstm", "wgan_gp")):
     import torch.multiprocessing as mp
+
+    from _spawn import gather
 
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -64,14 +66,9 @@ def _run(graph):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_worker, args=(port, graph, q))
+    p = ctx.Process(target=_worker, args=(port, graph, key, q))
     p.start()
-    try:
-        res = q.get(timeout=240)
-    finally:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
+    (res,) = gather([p], q, 1, timeout=240)  # a dead child fails within seconds, with its exit code
     assert not isinstance(res, str), res
     return res
 
@@ -81,6 +78,8 @@ def test_rccl_bucketed_grad_sync(cuda):
     assert res["g"] and res["c"] and res["finite"], res
 
 
-def test_rccl_grad_sync_in_graph(cuda):
-    res = _run(graph=True)
+# BASELINE configs 3-5: the vanilla MLP GAN, the MLP WGAN-GP and the LSTM WGAN-GP
+@pytest.mark.parametrize("key", [("lstm", "wgan_gp"), ("mlp", "wgan_gp"), ("mlp", "gan")])
+def test_rccl_grad_sync_in_graph(cuda, key):
+    res = _run(graph=True, key=key)
     assert res["captured"] and res["g"] and res["c"] and res["finite"], res

@@ -101,13 +101,12 @@ def test_dp_two_ranks_on_gpu_tensors(cuda):
     procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
+    from _spawn import gather
+
     res = {}
-    for _ in range(2):
-        r, v = q.get(timeout=600)
+    for r, v in gather(procs, q, 2, timeout=600):
         assert not isinstance(v, str), v
         res[r] = v
-    for p in procs:
-        p.join(timeout=60)
     assert np.isfinite(res[0]).all()
     assert np.array_equal(res[0], res[1])
 
