@@ -50,8 +50,19 @@ MODELS = {
 }
 
 
+def _sync(dev):
+    import torch
+
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def _measure(args, dtype, rank, world, pg, dev):
-    """Warm up, then time exactly args.steps training iterations at one compute dtype."""
+    """Warm up, then time exactly args.steps training iterations at one compute dtype.
+
+    The timed window is bracketed by a barrier and a device synchronisation on both sides; the
+    job's elapsed time is the MAX over ranks, and ``value`` = windows per step on all ranks x steps
+    / that elapsed time.  (``dev`` may be a CPU device: the gloo multi-rank test drives this path.)"""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -64,9 +75,12 @@ def _measure(args, dtype, rank, world, pg, dev):
     T, F, B = args.window, args.features, args.batch_per_gpu
     arch, loss = zoo.resolve(args.model)
     ds = synthetic_windows(args.dataset_windows, T, F, seed=1234)
-    cfg = GANConfig(arch=arch, loss=loss, window=T, features=F, batch_size=B, dtype=dtype, seed=123)
+    cfg = GANConfig(arch=arch, loss=loss, window=T, features=F, batch_size=B, dtype=dtype, seed=123,
+                    hidden=getattr(args, "hidden", 100))
     tr = GANTrainer(cfg, ds, device=dev, process_group=pg, rank=rank, world=world)
-    torch.cuda.reset_peak_memory_stats(dev)
+    cuda = dev.type == "cuda"
+    if cuda:
+        torch.cuda.reset_peak_memory_stats(dev)
 
     def barrier():
         if world > 1:
@@ -74,16 +88,17 @@ def _measure(args, dtype, rank, world, pg, dev):
 
     for _ in range(args.warmup):
         tr.train_step()
-    torch.cuda.synchronize()
+    _sync(dev)
     barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.train_step()
-    torch.cuda.synchronize()
+    _sync(dev)
     barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    _sync(dev)
+    local = time.perf_counter() - t0
+    elapsed = local
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -95,7 +110,7 @@ def _measure(args, dtype, rank, world, pg, dev):
     else:
         for _ in range(args.profile_steps):
             tr.train_step()
-    torch.cuda.synchronize()
+    _sync(dev)
     losses = tr.losses()
     per_rank = tr.windows_per_iteration()
     out = {
@@ -103,10 +118,13 @@ def _measure(args, dtype, rank, world, pg, dev):
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "windows_per_step": per_rank * world,
         "losses_finite": bool(all(np.isfinite(v) for k, v in losses.items() if k != "iteration")),
-        "peak_mem_gb_rank0": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
+        "peak_mem_gb_rank0": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2) if cuda else 0.0,
+        "elapsed_s": elapsed,
+        "elapsed_local_s": local,
     }
     del tr, ds
-    torch.cuda.empty_cache()
+    if cuda:
+        torch.cuda.empty_cache()
     return out
 
 
@@ -136,11 +154,15 @@ def main():
     import torch.distributed as dist
 
     import hfrep  # noqa: F401
-    from hfrep.parallel.dp import init_distributed
+    from hfrep.parallel.dp import env_rank, init_distributed
 
+    _, _, env_world = env_rank()
+    if env_world != args.gpus:
+        # the record's n_gpus / aggregate must describe the job that actually ran
+        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE {env_world} (launch N > 1 with "
+              f"torch.distributed.run --nproc-per-node N)", file=sys.stderr)
+        sys.exit(2)
     rank, local_rank, world, pg = init_distributed()
-    if world != args.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 

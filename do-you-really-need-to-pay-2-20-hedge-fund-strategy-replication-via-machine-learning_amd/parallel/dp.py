@@ -37,8 +37,12 @@ def init_distributed(backend: str | None = None, timeout_s: float = 600.0):
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    # torchrun always sets MASTER_PORT; a hand-launched job may choose it with HFREP_MASTER_PORT
-    os.environ.setdefault("MASTER_PORT", os.environ.get("HFREP_MASTER_PORT", "29511"))
+    # torchrun always sets MASTER_PORT; a hand-launched job names it with HFREP_MASTER_PORT (no
+    # fixed default: two jobs on one node would silently rendezvous with each other)
+    if "MASTER_PORT" not in os.environ:
+        if "HFREP_MASTER_PORT" not in os.environ:
+            raise RuntimeError("WORLD_SIZE > 1 needs MASTER_PORT (torchrun sets it) or HFREP_MASTER_PORT")
+        os.environ["MASTER_PORT"] = os.environ["HFREP_MASTER_PORT"]
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
         # surface RCCL errors as Python exceptions instead of hanging a collective forever

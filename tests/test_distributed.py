@@ -209,3 +209,73 @@ def test_dp_resume_from_rank_local_checkpoint_dir(tmp_path):
     assert res[0]["resumed_at"] == res[1]["resumed_at"] == 5
     for r in range(world):
         np.testing.assert_array_equal(res[r]["params"], res[r]["full"])
+
+
+def _bench_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        import argparse
+        import sys
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        import hfrep  # noqa: F401
+        from hfrep.parallel.dp import init_distributed
+
+        r, _, w, pg = init_distributed(backend="gloo")
+        args = argparse.Namespace(window=6, features=4, batch_per_gpu=4, hidden=8, model="mtss_wgan_gp",
+                                  dataset_windows=32, warmup=1, steps=2, trace_out="", profile_steps=0)
+        if r == world - 1:  # the slowest rank sets the job's elapsed time
+            import time
+
+            orig = bench.time.perf_counter
+            calls = {"n": 0}
+
+            def slow():
+                calls["n"] += 1
+                return orig() + (0.5 if calls["n"] == 2 else 0.0)  # +0.5 s on the timed window's end
+
+            bench.time = type("T", (), {"perf_counter": staticmethod(slow)})
+        out = bench._measure(args, "float32", r, w, pg, torch.device("cpu"))
+        q.put((r, out))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+
+
+def test_bench_aggregate_uses_max_elapsed_over_ranks():
+    """bench.py at world 8 (gloo, CPU, tiny shape): every rank reports the same elapsed time, the
+    MAX of the per-rank timed windows, and value = all ranks' windows x steps / that time."""
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for r, v in gather(procs, q, world, timeout=300):
+        assert not isinstance(v, str), v
+        res[r] = v
+    local = [res[r]["elapsed_local_s"] for r in range(world)]
+    assert local[world - 1] >= 0.5 and local[world - 1] == max(local)
+    for r in range(world):
+        assert res[r]["elapsed_s"] == max(local)
+        per_rank_windows = 5 * 4 + 4  # n_critic * B + B
+        assert res[r]["windows_per_step"] == per_rank_windows * world
+        assert res[r]["value"] == round(per_rank_windows * world * 2 / max(local), 2)
+
+
+def test_bench_refuses_gpus_world_mismatch():
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert p.returncode == 2 and "WORLD_SIZE" in p.stderr
