@@ -71,6 +71,9 @@ Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act) {
   if (hfrep::skinny_supported(K, N))
     hfrep::launch_skinny_fwd(dt_of(x), x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
                              y.data_ptr(), M, K, N, (int)act, cur_stream(x));
+  else if (dt_of(x) == hfrep::DT_F32 && hfrep::narrowf_supported(K, N))
+    hfrep::launch_narrowf(x.data_ptr<float>(), W.data_ptr<float>(), N, 1, b.has_value() ? b->data_ptr<float>() : nullptr,
+                          y.data_ptr<float>(), M, K, N, (int)act, cur_stream(x));
   else if (dt_of(x) == hfrep::DT_BF16 && hfrep::narrow_supported(K, N))
     hfrep::launch_narrow_fwd(x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
                              y.data_ptr(), M, K, N, (int)act, cur_stream(x));
@@ -92,6 +95,9 @@ Tensor linear_dgrad(Tensor dz, Tensor W) {
   // dx = dz . W^T : W stored (N, K) row-major -> w_trans
   if (hfrep::skinny_supported(N, K))
     hfrep::launch_skinny_dgrad(dt_of(dz), dz.data_ptr(), W.data_ptr<float>(), dx.data_ptr(), M, N, K, cur_stream(dz));
+  else if (dt_of(dz) == hfrep::DT_F32 && hfrep::narrowf_supported(K, N))  // B[k][n] = W[n][k]
+    hfrep::launch_narrowf(dz.data_ptr<float>(), W.data_ptr<float>(), 1, K, nullptr, dx.data_ptr<float>(), M, K, N, 0,
+                          cur_stream(dz));
   else if (dt_of(dz) == hfrep::DT_BF16 && N > 64)
     hfrep::launch_linear2(dz.data_ptr(), W.data_ptr<float>(), nullptr, dx.data_ptr(), M, N, K, 1, 0, cur_stream(dz));
   else
@@ -263,6 +269,7 @@ std::tuple<Tensor, Tensor> lstm_tbwd(optional<Tensor> dH, Tensor dHd, Tensor gat
 
 // ------------------------------------------------------------------------------------ LSTM fp32 fused
 bool lstmf_supported(int64_t H, int64_t K, int64_t act) { return hfrep::lstmf_supported((int)H, (int)K, (int)act); }
+bool narrowf_supported(int64_t K, int64_t N) { return hfrep::narrowf_supported((int)K, (int)N); }
 
 std::tuple<Tensor, Tensor> lstmf_fwd(Tensor x, Tensor W, optional<Tensor> b, Tensor U, int64_t act, bool save) {
   CHECK_F32(x); CHECK_F32(W);
@@ -706,6 +713,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstm_tfwd(Tensor dzx, Tensor gates, Tensor cs, Tensor U, int act) -> (Tensor, Tensor, Tensor)");
   m.def("lstm_tbwd(Tensor? dH, Tensor dHd, Tensor gates, Tensor cs, Tensor zds, Tensor cds, Tensor U, int act) -> (Tensor, Tensor)");
   m.def("lstmf_supported(int H, int K, int act) -> bool", &lstmf_supported);  // no tensor inputs: catch-all kernel
+  m.def("narrowf_supported(int K, int N) -> bool", &narrowf_supported);
   m.def("lstmf_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
   m.def("lstmf_bwd(Tensor? dH, Tensor tape, Tensor U, int act, int B, int T) -> Tensor");
   m.def("lstmf_tbwd(Tensor? dH, Tensor? dHd, Tensor tape, Tensor ttape, Tensor U, int act, int B, int T) -> (Tensor, Tensor)");

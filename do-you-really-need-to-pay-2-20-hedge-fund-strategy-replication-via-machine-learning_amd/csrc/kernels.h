@@ -101,6 +101,10 @@ bool skinny_supported(int K, int N);
 bool narrow_supported(int K, int N);  // 4 < N <= 64, K <= 128 (bf16 forward only)
 void launch_narrow_fwd(const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
                        hipStream_t s);
+// exact-fp32 narrow GEMM y = act(x B + b), B[k][n] = Bp[k sk + n sn]; K in {32, 36, 64, 100, 128}, 4 < N <= 112
+bool narrowf_supported(int K, int N);
+void launch_narrowf(const float* x, const float* B, int sk, int sn, const float* b, float* y, int M, int K, int N,
+                    int act, hipStream_t s);
 void launch_skinny_fwd(int dt, const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
                        hipStream_t s);
 size_t skinny_wgrad_workspace_floats(int M, int K, int N);

@@ -306,6 +306,115 @@ void launch_narrow_fwd(const void* x, const float* W, const float* b, void* y, i
   }
 }
 
+// ------------------------------------------------------------------------------------ narrow fp32
+// y = act(x B + b) in exact fp32 for K <= 128 (K % 4 == 0) and 4 < N <= 112, B given by strides
+// (B[k][n] = Bp[k sk + n sn]): the generator's output Dense(F) forward (K = 100, N = F) and its input
+// gradient dz W^T (K = F, N = 100), the MLP models' 100-wide Dense layers.  hipBLASLt ran the
+// forward at ~1.1 ms per 6.3 M-row call on the B = 262k step (Cijk_..._MT32x256x16,
+// profiles/r02_end); its tile shape wastes most of a 256-wide N tile on N = 32.
+//
+// One wave owns a 16-row chunk and ALL NT 16-column output tiles; B^T fragments of the whole
+// reduction live in registers (NT x KS), the A operand comes straight from HBM into registers (k is
+// permuted inside each 16-wide k group: k-step 4 q + j of lane group g reads k = 16 q + 4 g + j, so
+// a lane's four k-steps are one contiguous dwordx4; the remainder k-steps read k = 16 NQ + 4 r + g;
+// the sum over k is order-free and A / B use the same map).  The next chunk's A is loaded before
+// the current chunk's MFMAs (grid-stride over chunks, 4 waves per block, several blocks per CU).
+template <int NT, int NQ, int RS>
+__global__ void __launch_bounds__(256) narrowf_kernel(const float* __restrict__ x, const float* __restrict__ Bp, int sk,
+                                                      int sn, const float* __restrict__ bias, float* __restrict__ y,
+                                                      int M, int N, int act) {
+  constexpr int K = 16 * NQ + 4 * RS, KS = 4 * NQ + RS;
+  const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  float bw[NT][KS], bv[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int col = 16 * n + c16;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = s < 4 * NQ ? 16 * (s >> 2) + 4 * g + (s & 3) : 16 * NQ + 4 * (s - 4 * NQ) + g;
+      bw[n][s] = col < N ? Bp[(size_t)k * sk + (size_t)col * sn] : 0.f;
+    }
+    bv[n] = (bias && col < N) ? bias[col] : 0.f;
+  }
+  const int nch = (M + 15) / 16;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  typedef __amdgpu_buffer_rsrc_t rsrc_t;
+  auto rsrc_of = [&](int c) -> rsrc_t {  // rows of chunk c (past M: zero-size descriptor, loads read 0)
+    const int r0 = c * 16, nr = c < nch ? min(16, M - r0) : 0;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x) + (nr ? (size_t)r0 * K : 0), 0, nr * K * 4, 0x00020000);
+  };
+  f32x4 a4[2][NQ > 0 ? NQ : 1];
+  float ar[2][RS > 0 ? RS : 1];
+  const int vo = (c16 * K + 4 * g) * 4;
+  auto load = [&](int set, int c) {
+    const rsrc_t r = rsrc_of(c);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      a4[set][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo + 64 * q, 0, 0));
+#pragma unroll
+    for (int rr = 0; rr < RS; ++rr)
+      ar[set][rr] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (c16 * K + 16 * NQ + 4 * rr + g) * 4, 0, 0));
+  };
+  auto body = [&](int set, int c) {
+    f32x4 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const float av = s < 4 * NQ ? a4[set][s < 4 * NQ ? s >> 2 : 0][s & 3] : ar[set][s < 4 * NQ ? 0 : s - 4 * NQ];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bw[n][s], acc[n], 0, 0, 0);
+    }
+    const int r0 = c * 16 + 4 * g;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int col = 16 * n + c16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (col < N && r0 + i < M) y[(size_t)(r0 + i) * N + col] = act_f(act, acc[n][i] + bv[n]);
+    }
+  };
+  int c = wid;
+  if (c < nch) load(0, c);
+  for (; c < nch; c += 2 * nw) {
+    load(1, c + nw);  // (past the end: zero-size descriptor)
+    body(0, c);
+    if (c + nw >= nch) break;
+    load(0, c + 2 * nw);
+    body(1, c + nw);
+  }
+}
+
+bool narrowf_supported(int K, int N) {
+  return N > 4 && N <= 112 && (K == 32 || K == 36 || K == 64 || K == 100 || K == 128);
+}
+
+void launch_narrowf(const float* x, const float* B, int sk, int sn, const float* b, float* y, int M, int K, int N,
+                    int act, hipStream_t s) {
+  if (M <= 0) return;
+  const int nch = (M + 15) / 16;
+  const int grid = std::max(1, std::min((nch + 3) / 4, device_cu_count() * 4));
+  const int nt = (N + 15) / 16;
+#define HFREP_NARROWF(NQ, RS)                                                                                        \
+  switch (nt) {                                                                                                      \
+    case 1: hipLaunchKernelGGL((narrowf_kernel<1, NQ, RS>), dim3(grid), dim3(256), 0, s, x, B, sk, sn, b, y, M, N, act); break; \
+    case 2: hipLaunchKernelGGL((narrowf_kernel<2, NQ, RS>), dim3(grid), dim3(256), 0, s, x, B, sk, sn, b, y, M, N, act); break; \
+    case 3: hipLaunchKernelGGL((narrowf_kernel<3, NQ, RS>), dim3(grid), dim3(256), 0, s, x, B, sk, sn, b, y, M, N, act); break; \
+    case 4: hipLaunchKernelGGL((narrowf_kernel<4, NQ, RS>), dim3(grid), dim3(256), 0, s, x, B, sk, sn, b, y, M, N, act); break; \
+    case 5: hipLaunchKernelGGL((narrowf_kernel<5, NQ, RS>), dim3(grid), dim3(256), 0, s, x, B, sk, sn, b, y, M, N, act); break; \
+    case 6: hipLaunchKernelGGL((narrowf_kernel<6, NQ, RS>), dim3(grid), dim3(256), 0, s, x, B, sk, sn, b, y, M, N, act); break; \
+    default: hipLaunchKernelGGL((narrowf_kernel<7, NQ, RS>), dim3(grid), dim3(256), 0, s, x, B, sk, sn, b, y, M, N, act); break; \
+  }
+  switch (K) {
+    case 32: HFREP_NARROWF(2, 0) break;
+    case 36: HFREP_NARROWF(2, 1) break;
+    case 64: HFREP_NARROWF(4, 0) break;
+    case 100: HFREP_NARROWF(6, 1) break;
+    default: HFREP_NARROWF(8, 0) break;
+  }
+#undef HFREP_NARROWF
+}
+
 // ------------------------------------------------------------------------------------ host
 bool skinny_supported(int K, int N) {
   return N >= 1 && N <= 4 && K % 8 == 0 && K >= 8 && K / 8 <= 1024 && K * N <= 16384;  // W in <= 64 KB LDS

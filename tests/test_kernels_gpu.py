@@ -905,3 +905,38 @@ def test_bench_scale_gradients_are_slice_averages(cuda, dtype, B, T, F, lrelu):
         rel = ((full - avg).norm() / avg.norm()).item()
         assert torch.isfinite(full).all() and rel < tol, (f"generator: full-batch vs slice-average rel {rel:.2e}",
                                                           _block_rel(tr.generator, full, avg))
+
+
+@pytest.mark.parametrize("M,K,N,act", [(6291456 + 5, 100, 32, 0), (1000, 36, 36, 1), (333, 64, 112, 2),
+                                       (77, 128, 5, 3), (4099, 32, 100, 0)])
+def test_narrowf_linear(cuda, M, K, N, act):
+    """Exact-fp32 narrow GEMM (csrc/skinny.hip narrowf_kernel) on the Dense forward: the generator's
+    Dense(32) at the bench's 6.3 M rows (B = 262144 x T = 24) and every K / partial-tile case; fp64
+    reference computed on the device; bitwise run-to-run."""
+    assert _ops().narrowf_supported(K, N)
+    g = torch.Generator(device=cuda).manual_seed(41)
+    x = torch.randn(M, K, generator=g, device=cuda)
+    W = torch.randn(K, N, generator=g, device=cuda) * (1.0 / K ** 0.5)
+    b = torch.randn(N, generator=g, device=cuda) * 0.1
+    y = _ops().linear(x, W, b, act)
+    ref = R.apply_act(x.double() @ W.double() + b.double(), act)
+    err = (y.double() - ref).abs().max().item()
+    scale = max(ref.abs().max().item(), 1e-3)
+    assert err <= TOL[torch.float32]["atol"] * max(1.0, scale) + TOL[torch.float32]["rtol"] * scale, (err, scale)
+    assert torch.equal(y, _ops().linear(x, W, b, act))
+    del x, y, ref
+
+
+@pytest.mark.parametrize("M,K,N", [(6291456 + 3, 32, 100), (513, 36, 100), (70, 100, 32)])
+def test_narrowf_dgrad(cuda, M, K, N):
+    """dz W^T on the narrow fp32 kernel (the generator's Dense(32) input gradient at 6.3 M rows)."""
+    assert _ops().narrowf_supported(K, N)
+    g = torch.Generator(device=cuda).manual_seed(43)
+    dz = torch.randn(M, K, generator=g, device=cuda)
+    W = torch.randn(N, K, generator=g, device=cuda) * 0.1
+    dx = _ops().linear_dgrad(dz, W)
+    ref = dz.double() @ W.double().t()
+    err = (dx.double() - ref).abs().max().item()
+    scale = max(ref.abs().max().item(), 1e-3)
+    assert err <= TOL[torch.float32]["atol"] * max(1.0, scale) + TOL[torch.float32]["rtol"] * scale, (err, scale)
+    assert torch.equal(dx, _ops().linear_dgrad(dz, W))
