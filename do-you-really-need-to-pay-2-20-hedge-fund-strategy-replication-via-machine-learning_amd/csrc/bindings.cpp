@@ -61,13 +61,18 @@ inline Tensor out_empty_like(const Tensor& t) {
 bool set_debug_poison(bool on) { return poison_flag().exchange(on); }
 
 // ------------------------------------------------------------------------------------ GEMM
-Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act) {
+// out (optional): a contiguous (M, N) destination of x's dtype, e.g. a row slice of a larger buffer
+// (the generator writes its fake batch straight into the critic's [real; fake] input)
+Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act, optional<Tensor> out) {
   CHECK_GPU(x); CHECK_F32(W);
   TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && x.size(1) == W.size(0), "linear: shape mismatch");
   if (b.has_value()) { CHECK_F32(*b); TORCH_CHECK(b->numel() == W.size(1), "linear: bias size"); }
   GUARD(x);
   const int M = x.size(0), K = x.size(1), N = W.size(1);
-  Tensor y = out_empty({M, N}, x.options());
+  if (out.has_value())
+    TORCH_CHECK(out->is_cuda() && out->is_contiguous() && out->scalar_type() == x.scalar_type() && out->numel() == (int64_t)M * N,
+                "linear: out must be a contiguous (M, N) tensor of x's dtype");
+  Tensor y = out.has_value() ? out->view({M, N}) : out_empty({M, N}, x.options());
   if (hfrep::skinny_supported(K, N))
     hfrep::launch_skinny_fwd(dt_of(x), x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
                              y.data_ptr(), M, K, N, (int)act, cur_stream(x));
@@ -643,13 +648,17 @@ void philox_fill_(Tensor out, int64_t seed, Tensor ctr, int64_t dist) {
                             cur_stream(out));
 }
 
-Tensor sample_windows(Tensor data, int64_t batch, int64_t seed, Tensor ctr, at::ScalarType out_dtype) {
+Tensor sample_windows(Tensor data, int64_t batch, int64_t seed, Tensor ctr, at::ScalarType out_dtype,
+                      optional<Tensor> dst) {
   CHECK_F32(data);
   TORCH_CHECK(ctr.is_cuda() && ctr.scalar_type() == at::kLong && ctr.numel() == 1, "ctr must be a 1-element int64 GPU tensor");
   GUARD(data);
   std::vector<int64_t> shape(data.sizes().begin(), data.sizes().end());
   shape[0] = batch;
-  Tensor out = out_empty(shape, data.options().dtype(out_dtype));
+  if (dst.has_value())
+    TORCH_CHECK(dst->is_cuda() && dst->is_contiguous() && dst->scalar_type() == out_dtype && dst->sizes() == at::IntArrayRef(shape),
+                "sample_windows: dst must be a contiguous (batch, ...) tensor of out_dtype");
+  Tensor out = dst.has_value() ? *dst : out_empty(shape, data.options().dtype(out_dtype));
   const int64_t N = data.size(0), D = data.numel() / N;
   hfrep::launch_sample_windows(dt_of(out), data.data_ptr<float>(), N, D, out.data_ptr(), (int)batch, (uint64_t)seed,
                                ctr.data_ptr<int64_t>(), cur_stream(data));
@@ -701,7 +710,7 @@ void clip_(Tensor p, double c) {
 }  // namespace
 
 TORCH_LIBRARY(hfrep, m) {
-  m.def("linear(Tensor x, Tensor W, Tensor? b, int act) -> Tensor");
+  m.def("linear(Tensor x, Tensor W, Tensor? b, int act, Tensor? out=None) -> Tensor");
   m.def("linear_dgrad(Tensor dz, Tensor W) -> Tensor");
   m.def("linear_wgrad_(Tensor x, Tensor dz, Tensor(a!) gW, Tensor(b!)? gb, int shiftT=0) -> ()");
   m.def("lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor(a!) gW, Tensor(b!) gU, Tensor(c!)? gb, Tensor? xd=None, Tensor? hds=None, Tensor? dZd=None, int impl=0) -> ()");
@@ -739,7 +748,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("col2im_causal(Tensor dcols, int k, int dil, int C) -> Tensor");
   m.def("interpolate(Tensor real, Tensor fake, Tensor alpha) -> Tensor");
   m.def("philox_fill_(Tensor(a!) out, int seed, Tensor(b!) ctr, int dist) -> ()");
-  m.def("sample_windows(Tensor data, int batch, int seed, Tensor(a!) ctr, ScalarType out_dtype) -> Tensor");
+  m.def("sample_windows(Tensor data, int batch, int seed, Tensor(a!) ctr, ScalarType out_dtype, Tensor? dst=None) -> Tensor");
   m.def("rmsprop_(Tensor(a!) p, Tensor g, Tensor(b!) ms, float lr, float rho, float eps, float clip, float gscale) -> ()");
   m.def("adam_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, float lr, float b1, float b2, float eps, float clip, float gscale) -> ()");
   m.def("nadam_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor m_cache, float lr, float b1, float b2, float eps, float gscale) -> ()");

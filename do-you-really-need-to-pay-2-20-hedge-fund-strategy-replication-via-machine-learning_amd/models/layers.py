@@ -154,8 +154,8 @@ class Dense(Layer):
     def forward(self, x):
         return R.dense(x, self.w("kernel"), self.w("bias") if self.use_bias else None, self.act)
 
-    def efwd(self, x, save):
-        y = Fn.linear(x, self.p("kernel"), self.p("bias") if self.use_bias else None, self.act_code)
+    def efwd(self, x, save, out=None):
+        y = Fn.linear(x, self.p("kernel"), self.p("bias") if self.use_bias else None, self.act_code, out=out)
         return y, ({"x": x, "y": y} if save else None)
 
     def _dgrad(self, dz):
@@ -513,7 +513,9 @@ class Sequential(torch.nn.Module):
         return x
 
     # ---- explicit engine -----------------------------------------------------------------
-    def efwd(self, x, save: bool = True):
+    def efwd(self, x, save: bool = True, out=None):
+        """``out``: destination of the model output, used when the last layer can write into it
+        (Dense); otherwise the output is copied there."""
         tape = []
         i, n = 0, len(self.layers)
         while i < n:
@@ -529,14 +531,19 @@ class Sequential(torch.nn.Module):
                 x = y
                 i += 2
                 continue
-            x, ctx = l.efwd(x, save)
+            if out is not None and i == n - 1 and isinstance(l, Dense):
+                x, ctx = l.efwd(x, save, out=out)
+            else:
+                x, ctx = l.efwd(x, save)
             tape.append(ctx)
             i += 1
+        if out is not None and x.data_ptr() != out.data_ptr():
+            x = out.copy_(x)
         return x, tape
 
     @torch.no_grad()
-    def predict(self, x):
-        return self.efwd(x, save=False)[0]
+    def predict(self, x, out=None):
+        return self.efwd(x, save=False, out=out)[0]
 
     @staticmethod
     def _adj(layer, dy):

@@ -47,19 +47,23 @@ def _blas_fp32(a: torch.Tensor, rows: int, K: int, N: int) -> bool:
             and not _ops().narrowf_supported(int(K), int(N)))
 
 
-def linear(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: int) -> torch.Tensor:
-    """act(x @ W + b) on the last axis. Output dtype = x dtype."""
+def linear(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: int,
+           out: torch.Tensor | None = None) -> torch.Tensor:
+    """act(x @ W + b) on the last axis. Output dtype = x dtype.  ``out``: a contiguous destination
+    of the output's shape (e.g. a row slice of a larger buffer); the result is written there."""
     if _nat(x) and act == 0 and W.shape[1] > 4 and _blas_fp32(x, x.numel() // x.shape[-1], W.shape[0], W.shape[1]):
         x2 = _2d(x.contiguous())
         y = torch.addmm(b, x2, W) if b is not None else torch.mm(x2, W)
-        return y.reshape(*x.shape[:-1], W.shape[1])
+        y = y.reshape(*x.shape[:-1], W.shape[1])
+        return y if out is None else out.copy_(y)
     if _nat(x):
-        y = _ops().linear(_2d(x.contiguous()), W, b, int(act))
+        y = _ops().linear(_2d(x.contiguous()), W, b, int(act), out)
         return y.reshape(*x.shape[:-1], W.shape[1])
     y = torch.matmul(x, W.to(x.dtype))
     if b is not None:
         y = y + b.to(x.dtype)
-    return R.apply_act(y, act)
+    y = R.apply_act(y, act)
+    return y if out is None else out.copy_(y)
 
 
 # fp32 dZ (.., 400) @ W^T with W (K <= 112, 400): the LSTM layers' input gradient, on the
@@ -381,8 +385,19 @@ def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None, impl: int = 
     split exactly into three bf16 terms, six products on the bf16 matrix pipe; default for K <= 36,
     ``impl=2``) or the exact-fp32 MFMA kernel lstmf_wgrad_kernel (default for K = 100, ``impl=1``);
     otherwise per-product calls."""
-    f32 = (dZ.dtype == torch.float32 and _LSTMF and x.shape[-1] in (32, 36, 100) and hs.shape[-1] == 100
+    f32 = (dZ.dtype == torch.float32 and _LSTMF and x.shape[-1] in (32, 35, 36, 100) and hs.shape[-1] == 100
            and dZ.shape[-1] == 400)
+    if f32 and x.shape[-1] == 35 and _nat(dZ):
+        # the reference's 35-feature windows (GAN/MTSS_WGAN_GP.py:101): one zero column makes the rows
+        # 16-byte aligned for the fused kernel (instead of four per-product launches that each re-read dZ)
+        pad = torch.nn.functional.pad
+        gW36 = torch.zeros(36, gW.shape[-1], dtype=gW.dtype, device=gW.device)
+        _ops().lstm_wgrad_(pad(x, (0, 1)).contiguous(), hs.contiguous(), dZ.contiguous(), gW36, gU, gb,
+                           None if xd is None else pad(xd, (0, 1)).contiguous(),
+                           None if hds is None else hds.contiguous(), None if dZd is None else dZd.contiguous(),
+                           int(impl))
+        gW.add_(gW36[:35].reshape(gW.shape))
+        return
     if (dZ.dtype == torch.bfloat16 or f32) and _nat(dZ):
         _ops().lstm_wgrad_(x.contiguous(), hs.contiguous(), dZ.contiguous(), gW, gU, gb,
                            None if xd is None else xd.contiguous(), None if hds is None else hds.contiguous(),

@@ -105,8 +105,8 @@ class GANTrainer:
             self.grad_sync.broadcast_params([self.generator, self.critic])
 
     # ------------------------------------------------------------------------------------
-    def _batch(self, B):
-        real = self.rng.sample_windows(self.dataset, B, out_dtype=self.dtype)
+    def _batch(self, B, out=None):
+        real = self.rng.sample_windows(self.dataset, B, out_dtype=self.dtype, out=out)
         noise = self.rng.normal((B, self.cfg.window, self.cfg.features), dtype=self.dtype)
         return real, noise
 
@@ -154,21 +154,25 @@ class GANTrainer:
         self._apply(C, clip=clip)
         return out[0].to(self._acc)
 
-    def _gp_step(self, real, noise):
+    def _gp_step(self, real, noise, xrf=None):
         with trange("critic/generate"):
-            fake = self.generator.predict(noise)
+            fake = self.generator.predict(noise, out=None if xrf is None else xrf[real.shape[0]:])
             alpha = self.rng.uniform((real.shape[0],))
-        out = self.critic_gp_grads(real, fake, alpha)
+        out = self.critic_gp_grads(real, fake, alpha, xrf=xrf)
         self._apply(self.critic)
         return out
 
-    def critic_gp_grads(self, real, fake, alpha):
-        """Accumulate d/dtheta_C of W(real,-1) + W(fake,+1) + lambda*GP(x_hat) into C.flat.grad."""
+    def critic_gp_grads(self, real, fake, alpha, xrf=None):
+        """Accumulate d/dtheta_C of W(real,-1) + W(fake,+1) + lambda*GP(x_hat) into C.flat.grad.
+
+        ``xrf``: the [real; fake] critic input when ``real`` / ``fake`` already are its two row
+        halves (the sampler and the generator write straight into it: no concatenation copy)."""
         C = self.critic
         xh = Fn.interpolate(real, fake, alpha)
         # W terms on [real; fake]
         with trange("critic/w_terms"):
-            xrf = torch.cat([real, fake], 0)
+            if xrf is None:
+                xrf = torch.cat([real, fake], 0)
             s, tape = C.efwd(xrf, save=True)
             # W(real, -1) and W(fake, +1): both segment means and the score gradient in one launch
             w, ds = Fn.gan_loss(s, s.numel() // 2, -1.0, 1.0, 0)
@@ -232,8 +236,9 @@ class GANTrainer:
         else:
             for _ in range(self.n_critic):
                 with trange("critic/sample"):
-                    real, noise = self._batch(B)
-                self._d_acc = self._gp_step(real, noise)
+                    xrf = torch.empty((2 * B, cfg.window, cfg.features), dtype=self.dtype, device=self.device)
+                    real, noise = self._batch(B, out=xrf[:B])
+                self._d_acc = self._gp_step(real, noise, xrf)
             self._g_acc = self._generator_step(noise).reshape(1)
         self.iteration += 1
 

@@ -47,13 +47,15 @@ class DeviceRNG:
             return out
         return torch.rand(shape, generator=self.gen, dtype=torch.float32).to(self.device, dtype)
 
-    def sample_windows(self, dataset: torch.Tensor, batch: int, out_dtype=None) -> torch.Tensor:
-        """``dataset[randint(0, N, batch)]`` (with replacement, GAN/GAN.py:178)."""
+    def sample_windows(self, dataset: torch.Tensor, batch: int, out_dtype=None, out=None) -> torch.Tensor:
+        """``dataset[randint(0, N, batch)]`` (with replacement, GAN/GAN.py:178); ``out``: a contiguous
+        destination (e.g. the first rows of the critic's [real; fake] input buffer)."""
         out_dtype = out_dtype or dataset.dtype
         if self.native:
-            return _native.native().sample_windows(dataset, int(batch), self.seed, self.ctr, out_dtype)
+            return _native.native().sample_windows(dataset, int(batch), self.seed, self.ctr, out_dtype, out)
         idx = torch.randint(0, dataset.shape[0], (batch,), generator=self.gen)
-        return dataset.index_select(0, idx.to(dataset.device)).to(out_dtype)
+        y = dataset.index_select(0, idx.to(dataset.device)).to(out_dtype)
+        return y if out is None else out.copy_(y)
 
     def state(self):
         return {"seed": self.seed, "ctr": (self.ctr.item() if self.native else None),

@@ -726,7 +726,7 @@ def test_lstmf_persistent_multi_pass(cuda):
 
 
 @pytest.mark.parametrize("B,T,K,tangent", [(70, 24, 32, False), (33, 12, 100, True), (1000, 24, 100, False),
-                                           (41, 5, 36, True)])
+                                           (41, 5, 36, True), (32, 48, 35, True), (65, 48, 35, False)])
 def test_lstmf_wgrad_fused(cuda, B, T, K, tangent):
     """fp32 fused LSTM weight gradient (one launch for every product) vs fp64."""
     from hfrep.ops import functional as Fn
