@@ -63,6 +63,10 @@ _DT = {"float32": torch.float32, "fp32": torch.float32, "bfloat16": torch.bfloat
 
 
 class GANTrainer:
+    # the generator step reuses the last critic step's generator forward (bitwise the same result as
+    # recomputing it: tests/test_engine.py::test_generator_forward_reuse_is_exact)
+    reuse_gen_forward = True
+
     def __init__(self, cfg: GANConfig, dataset, device="cpu", process_group=None, rank: int = 0, world: int = 1,
                  param_dtype=torch.float32):
         self.cfg = cfg
@@ -154,13 +158,19 @@ class GANTrainer:
         self._apply(C, clip=clip)
         return out[0].to(self._acc)
 
-    def _gp_step(self, real, noise, xrf=None):
+    def _gp_step(self, real, noise, xrf=None, keep_gen_tape=False):
+        """One GP critic update.  ``keep_gen_tape``: run the generator forward with its tape and
+        return (fake, tape) for the generator step that follows (see train_step)."""
+        dst = None if xrf is None else xrf[real.shape[0]:]
         with trange("critic/generate"):
-            fake = self.generator.predict(noise, out=None if xrf is None else xrf[real.shape[0]:])
+            if keep_gen_tape:
+                fake, gtape = self.generator.efwd(noise, save=True, out=dst)
+            else:
+                fake, gtape = self.generator.predict(noise, out=dst), None
             alpha = self.rng.uniform((real.shape[0],))
         out = self.critic_gp_grads(real, fake, alpha, xrf=xrf)
         self._apply(self.critic)
-        return out
+        return out, ((fake, gtape) if keep_gen_tape else None)
 
     def critic_gp_grads(self, real, fake, alpha, xrf=None):
         """Accumulate d/dtheta_C of W(real,-1) + W(fake,+1) + lambda*GP(x_hat) into C.flat.grad.
@@ -192,16 +202,20 @@ class GANTrainer:
         return torch.stack([w_real + w_fake + self.gp_weight * pen, w_real, w_fake, pen])
 
     # ---- generator ------------------------------------------------------------------------
-    def _generator_step(self, noise):
+    def _generator_step(self, noise, gen=None):
         with trange("generator"):
-            loss = self.generator_grads(noise)
+            loss = self.generator_grads(noise, gen=gen)
         self._apply(self.generator)
         return loss
 
-    def generator_grads(self, noise):
-        """Accumulate d/dtheta_G of the generator loss through the frozen critic."""
+    def generator_grads(self, noise, gen=None):
+        """Accumulate d/dtheta_G of the generator loss through the frozen critic.
+
+        ``gen``: (fake, tape) of G(noise) already computed with the CURRENT generator weights (the
+        last critic step's forward of the same noise: the critic updates do not touch G), reused
+        instead of a second identical forward."""
         G, C = self.generator, self.critic
-        fake, tg = G.efwd(noise, save=True)
+        fake, tg = gen if gen is not None else G.efwd(noise, save=True)
         s, tc = C.efwd(fake, save=True)
         if self.cfg.loss == "gan":
             out, ds = Fn.gan_loss(s, s.numel(), 1.0, 1.0, 1)
@@ -226,20 +240,28 @@ class GANTrainer:
             noise2 = self.rng.normal((B, cfg.window, cfg.features), dtype=self.dtype)
             self._g_acc = self._generator_step(noise2).reshape(1)
         elif cfg.loss == "wgan":
-            for _ in range(self.n_critic):
+            gen = None
+            for k in range(self.n_critic):
                 real, noise = self._batch(B)
-                fake = self.generator.predict(noise)
+                if self.reuse_gen_forward and k == self.n_critic - 1:  # reused by the G step (same noise, same G)
+                    gen = self.generator.efwd(noise, save=True)
+                    fake = gen[0]
+                else:
+                    fake = self.generator.predict(noise)
                 lr_ = self._wgan_step(real, -1.0, 0.0)
                 lf_ = self._wgan_step(fake, 1.0, self.clip)
                 self._d_acc = torch.stack([0.5 * (lr_ + lf_), lr_, lf_, torch.zeros_like(lr_)])
-            self._g_acc = self._generator_step(noise).reshape(1)
+            self._g_acc = self._generator_step(noise, gen=gen).reshape(1)
         else:
-            for _ in range(self.n_critic):
+            gen = None
+            for k in range(self.n_critic):
                 with trange("critic/sample"):
                     xrf = torch.empty((2 * B, cfg.window, cfg.features), dtype=self.dtype, device=self.device)
                     real, noise = self._batch(B, out=xrf[:B])
-                self._d_acc = self._gp_step(real, noise, xrf)
-            self._g_acc = self._generator_step(noise).reshape(1)
+                # the generator step trains on the LAST critic step's noise (GAN/MTSS_WGAN_GP.py:281)
+                # with the same generator weights: that step keeps its generator tape for it
+                self._d_acc, gen = self._gp_step(real, noise, xrf, keep_gen_tape=self.reuse_gen_forward and k == self.n_critic - 1)
+            self._g_acc = self._generator_step(noise, gen=gen).reshape(1)
         self.iteration += 1
 
     def losses(self) -> dict:

@@ -150,3 +150,23 @@ def test_gan_loss_contract_matches_keras_losses(kind):
     (la_ + lb_).backward()
     assert torch.allclose(out, torch.stack([la_, lb_]).detach(), rtol=1e-12, atol=1e-12)
     assert torch.allclose(grad, q.grad, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("loss", ["wgan_gp", "wgan"])
+def test_generator_forward_reuse_is_exact(loss):
+    """The generator step reuses the last critic step's G(noise) forward and tape (same noise, and the
+    critic updates leave G untouched): bitwise the same training as recomputing it."""
+    import numpy as np
+
+    from hfrep.train.gan_trainer import GANConfig, GANTrainer
+
+    ds = np.random.RandomState(0).rand(40, 6, 4)
+    runs = []
+    for reuse in (True, False):
+        cfg = GANConfig(arch="lstm", loss=loss, window=6, features=4, batch_size=5, hidden=8, dtype="float64")
+        tr = GANTrainer(cfg, ds, param_dtype=torch.float64)
+        tr.reuse_gen_forward = reuse
+        for _ in range(3):
+            tr.train_step()
+        runs.append(torch.cat([tr.generator.flat.detach(), tr.critic.flat.detach(), tr._g_acc.reshape(-1)]))
+    assert torch.equal(runs[0], runs[1])
