@@ -61,6 +61,18 @@ def _flags():
     return kern, bind, link
 
 
+# per-translation-unit extra flags.  lstm_f32.hip: its split weight-gradient kernel runs one
+# straight-line body per wave kind behind a switch on the wave index; SimplifyCFG's common-code
+# sinking merged those bodies into one block with a run-time accumulator index, which moved the
+# accumulators to scratch memory (80 B per lane at K = 32)
+EXTRA_FLAGS = {"lstm_f32.hip": ["-mllvm", "-simplifycfg-sink-common=false"]}
+
+
+def kernel_flags(src: str) -> list[str]:
+    """The full hipcc flag list the library build uses for the kernel source ``src``."""
+    return _flags()[0] + EXTRA_FLAGS.get(os.path.basename(src), [])
+
+
 def _sources():
     hips = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
     cpps = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".cpp"))
@@ -98,7 +110,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
         for f in os.listdir(BUILD_DIR):
             os.remove(os.path.join(BUILD_DIR, f))
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
-    tasks = [(s, os.path.join(BUILD_DIR, os.path.basename(s) + ".o"), kern) for s in hips]
+    tasks = [(s, os.path.join(BUILD_DIR, os.path.basename(s) + ".o"), kern + EXTRA_FLAGS.get(os.path.basename(s), []))
+             for s in hips]
     tasks += [(s, os.path.join(BUILD_DIR, os.path.basename(s) + ".o"), bind) for s in cpps]
     changed = False
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:

@@ -1559,6 +1559,253 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------------------
+// split weight gradient, column QUAD: lstmf_wgrad_q4_kernel
+// ------------------------------------------------------------------------------------------
+// lstmf_wgrad_split_kernel (a workgroup PAIR per row range, 208 columns each) runs its 8 waves in one
+// phase at a time -- load -> MFMAs -> split + LDS store -> barrier -- so the matrix pipe idles through
+// the split (39.5 % MFMA busy at K = 32), and at K = 100 its 28-tile waves spill (53 ms vs 16 ms
+// exact).  Here FOUR workgroups share a row range and split the 400 gate columns in quarters of 100
+// (7 j-tiles, the last one 4 / 16 real); the quad sits on one XCD (blocks b, b + 8, b + 16, b + 24),
+// so the A rows [x | h_{t-1} | 1] that all four stage come from the same L2.  8 waves (2 per SIMD):
+// the NI x 7 output tiles are dealt out in j-major order (11-12 per wave at K = 100), so a wave keeps
+// its accumulators and <= 2 j-tiles' D fragments in registers and streams the A fragments.
+// Prefetch distance two chunks: chunk c + 2's fp32 rows are loaded at the top of chunk c (two
+// register sets alternate), and chunk c + 1's rows are split and stored into the other LDS buffer in
+// slices between chunk c's i-tiles, so the HBM latency hides under 1.5 chunks of MFMAs and the
+// split's VALU issue interleaves with the MFMAs of the same and the partner wave.  Same products and
+// accumulation as lstmf_wgrad_split_kernel: six bf16 products per tile into a fresh accumulator,
+// added to the running sum in VALU fp32.
+constexpr int WQ_CD = 100, WQ_NJ = 7, WQ_W = 8;  // D columns per part, j-tiles per part, waves
+template <int KX>
+struct WQGeo {
+  static constexpr int KR = KX + FH + 1;
+  static constexpr int NI = (KR + 15) / 16;
+  static constexpr int NIG = (NI + 3) / 4;                  // i-tiles of the first i-group (the rest NI / 4)
+  static constexpr int MAXT = NIG * 4;                      // tiles per wave (max): <= 4 i x 4 j
+  static constexpr int JX = (32 * KX / 4 + 511) / 512, JH = (32 * FH / 4 + 511) / 512;
+  static constexpr int JD = (32 * WQ_CD / 4 + 511) / 512;
+  static constexpr int NS = JX + JH + JD;                   // float4 staging slots per thread
+  static_assert(KX % 4 == 0 && 16 * NI <= WS_CA && NI <= 16, "wgrad q4: K");
+  // wave w: i-group ig, j-group jg (j-tiles 0-3 / 4-6); the two waves of a SIMD (w, w + 4) take
+  // mirrored i-groups so the SIMDs carry 25 / 21 / 21 / 24 tiles at K = 100
+  static constexpr int ig(int w) { return w < 4 ? w : 3 - (w & 3); }
+  static constexpr int i0(int g) { return g == 0 ? 0 : NIG + (g - 1) * ((NI - NIG) / 3) + ((g - 1) < (NI - NIG) % 3 ? g - 1 : (NI - NIG) % 3); }
+  static constexpr int ni(int g) { return i0(g + 1 > 3 ? 3 : g + 1) - i0(g) + (g == 3 ? NI - i0(3) : 0); }
+  static constexpr int j0(int w) { return w < 4 ? 0 : 4; }
+  static constexpr int nj(int w) { return w < 4 ? 4 : 3; }
+};
+
+template <int KX>
+__global__ void __launch_bounds__(512, 1)
+lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs, const float* __restrict__ D,
+                      const float* __restrict__ Xd, const float* __restrict__ Hds, const float* __restrict__ Dd,
+                      float* __restrict__ slab, int M, int Tn, int rows_per_z, int Z) {
+  using G = WQGeo<KX>;
+  constexpr int JX = G::JX, JH = G::JH, NS = G::NS, MAXT = G::MAXT;
+  extern __shared__ __attribute__((aligned(16))) char wsm_[];
+  lds_char* wsm = (lds_char*)wsm_;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // block -> (row range z, column part jq); with Z % 8 == 0 the quad shares an XCD (b, b+8, b+16, b+24)
+  int z, jq;
+  if (Z % 8 == 0) {
+    const int slot = blockIdx.x >> 3;
+    jq = slot & 3;
+    z = (slot >> 2) * 8 + (blockIdx.x & 7);
+  } else {
+    jq = blockIdx.x & 3;
+    z = blockIdx.x >> 2;
+  }
+  const int mb = z * rows_per_z, me = min(M, mb + rows_per_z);
+  const int jbase = WQ_CD * jq;
+
+  for (int i = tid; i < 2 * WS_BUF / 16; i += 512) reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(wsm)[i] = u32x4_t{0, 0, 0, 0};
+  __syncthreads();
+
+  f32x4 acc[MAXT];
+#pragma unroll
+  for (int a = 0; a < MAXT; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int trr = 8 * (lane >> 4) + ((lane & 15) >> 2);
+  const int tro_a = trr * WS_ROWA + 8 * (lane & 3), tro_d = trr * WS_ROWD + 8 * (lane & 3);
+  const int step32 = 32 % Tn;
+
+  // staging slot s of this thread: kind (x / h / d) is compile-time in s
+  auto slot_rc = [&](int s, int& r, int& c4, bool& ok) {
+    if (s < JX) {
+      const int e = tid + 512 * s;
+      r = e / (KX / 4); c4 = e - r * (KX / 4); ok = e < 32 * KX / 4;
+    } else if (s < JX + JH) {
+      const int e = tid + 512 * (s - JX);
+      r = e / (FH / 4); c4 = e - r * (FH / 4); ok = e < 32 * FH / 4;
+    } else {
+      const int e = tid + 512 * (s - JX - JH);
+      r = e / (WQ_CD / 4); c4 = e - r * (WQ_CD / 4); ok = e < 32 * WQ_CD / 4;
+    }
+    if (!ok) r = c4 = 0;
+  };
+
+  f32x4 v[2][NS];
+  for (int seg = 0; seg < (Xd ? 2 : 1); ++seg) {
+    const float* Xs = seg ? Xd : X;
+    const float* Hq = seg ? Hds : Hs;
+    const float* Dq = seg ? Dd : D;
+    const int nr = me > mb ? me - mb : 0;
+    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * KX, nr * KX * 4);
+    // (row mb - 1 based: every voffset >= 0; h_{-1} rows are masked by t)
+    const rsrc_t rh = make_rsrc(Hq + ((ptrdiff_t)mb - 1) * FH, (nr ? nr + 1 : 0) * FH * 4);
+    const rsrc_t rd = make_rsrc(Dq + (size_t)mb * FG + jbase, nr ? ((nr - 1) * FG + WQ_CD) * 4 : 0);
+    int tm[JH];  // (row mod Tn) of this thread's H slots at the next chunk to load
+#pragma unroll
+    for (int j = 0; j < JH; ++j) {
+      int r, c4;
+      bool ok;
+      slot_rc(JX + j, r, c4, ok);
+      tm[j] = (mb + r) % Tn;
+    }
+    // chunk loads into register set S (rows past me -- or past the range -- read zeros)
+    auto load = [&](auto S_, int m0) {
+      constexpr int S = decltype(S_)::value;
+      const int lim = me - m0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        int r, c4;
+        bool ok;
+        slot_rc(s, r, c4, ok);
+        ok = ok && r < lim;
+        if (s < JX) {
+          v[S][s] = ld4s(rx, ok ? (r * KX + 4 * c4) * 4 : kOOB, (m0 - mb) * KX * 4);
+        } else if (s < JX + JH) {
+          v[S][s] = ld4s(rh, ok && tm[s - JX] != 0 ? (r * FH + 4 * c4) * 4 : kOOB, (m0 - mb) * FH * 4);
+        } else {
+          v[S][s] = ld4s(rd, ok ? (r * FG + 4 * c4) * 4 : kOOB, (m0 - mb) * FG * 4);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < JH; ++j) {
+        tm[j] += step32;
+        if (tm[j] >= Tn) tm[j] -= Tn;
+      }
+    };
+    auto stage = [&](auto S_, lds_char* base, int s) {
+      constexpr int S = decltype(S_)::value;
+      int r, c4;
+      bool ok;
+      slot_rc(s, r, c4, ok);
+      if (!ok) return;
+      uint32_t p[3][2];
+      split3(v[S][s], p);
+      int lo, pl;
+      if (s < JX) { lo = r * WS_ROWA + 8 * c4; pl = WS_PLA; }
+      else if (s < JX + JH) { lo = r * WS_ROWA + 2 * KX + 8 * c4; pl = WS_PLA; }
+      else { lo = WS_IMGD + r * WS_ROWD + 8 * c4; pl = WS_PLD; }
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(base + lo + q * pl) = u32x2_t{p[q][0], p[q][1]};
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    if (tid < 64) {  // bias column KR - 1: 1 in plane h for the primal segment, 0 for the tangent one
+      const int buf = tid >> 5, r = tid & 31;
+      *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wsm + buf * WS_BUF + r * WS_ROWA + (G::KR - 1) * 2) =
+          seg ? 0 : 0x3f80;
+    }
+    const int nch = nr > 0 ? (nr + 31) / 32 : 0;
+    // prologue: chunk 0 staged into buffer 0, chunk 1 in flight in set 1
+    load(I0{}, mb);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) stage(I0{}, wsm, s);
+    load(I1{}, mb + 32);
+    __syncthreads();
+    // chunk c (S = c & 1): loads of chunk c + 2 into set S, MFMAs on buffer S, chunk c + 1 (set S ^ 1)
+    // split into buffer S ^ 1 in slices between the i-tiles
+    auto chunk = [&](auto S_, int c) {
+      constexpr int S = decltype(S_)::value;
+      load(S_, mb + 32 * (c + 2));
+      const lds_char* A_ = wsm + S * WS_BUF;
+      const lds_char* D_ = A_ + WS_IMGD;
+      lds_char* nxt = wsm + (S ^ 1) * WS_BUF;
+      // one straight-line body per wave (no branch between an MFMA and the VALU read of its
+      // result); wave W owns tiles [TS, TE) of the j-major list (tile L = j NI + i).  The staging
+      // slices are unconditional: after the last chunk they store the (zero) rows past the range
+      // into the idle buffer
+      auto body = [&](auto WK) {
+        constexpr int W = decltype(WK)::value;
+        constexpr int IG = G::ig(W), I0 = G::i0(IG), NIW = G::ni(IG), J0 = G::j0(W), NJW = G::nj(W);
+        constexpr int NJH = (NJW + 1) / 2;                  // j-tiles in pairs: 2 x 3 D fragments held
+        constexpr int SPI = (NS + NJH * NIW - 1) / (NJH * NIW);  // staging slots per (pair, i-tile)
+        auto jpair = [&](auto JH_) {  // (a lambda per pair: the slot indices below stay compile-time)
+          constexpr int jh = decltype(JH_)::value;
+          bf16x8 bfr[2][3];
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            if (2 * jh + jj < NJW) {
+#pragma unroll
+              for (int q = 0; q < 3; ++q) bfr[jj][q] = tr_frag<WS_ROWD>(D_ + q * WS_PLD, tro_d, 16 * (J0 + 2 * jh + jj));
+            }
+#pragma unroll
+          for (int ii = 0; ii < NIW; ++ii) {
+            __builtin_amdgcn_sched_barrier(0);
+            bf16x8 a3[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) a3[q] = tr_frag<WS_ROWA>(A_ + q * WS_PLA, tro_a, 16 * (I0 + ii));
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+              if (2 * jh + jj >= NJW) continue;  // (compile-time)
+              f32x4 t = mma32(a3[2], bfr[jj][0], f32x4{0.f, 0.f, 0.f, 0.f});  // lh
+              t = mma32(a3[0], bfr[jj][2], t);                                 // hl
+              t = mma32(a3[1], bfr[jj][1], t);                                 // mm
+              t = mma32(a3[1], bfr[jj][0], t);                                 // mh
+              t = mma32(a3[0], bfr[jj][1], t);                                 // hm
+              t = mma32(a3[0], bfr[jj][0], t);                                 // hh
+              acc[ii * 4 + 2 * jh + jj] += t;
+            }
+            const int it = jh * NIW + ii;
+#pragma unroll
+            for (int s = it * SPI; s < (it + 1) * SPI && s < NS; ++s) stage(std::integral_constant<int, S ^ 1>{}, nxt, s);
+          }
+        };
+        jpair(std::integral_constant<int, 0>{});
+        if constexpr (NJH > 1) jpair(std::integral_constant<int, 1>{});
+      };
+      switch (w) {
+        case 0: body(std::integral_constant<int, 0>{}); break;
+        case 1: body(std::integral_constant<int, 1>{}); break;
+        case 2: body(std::integral_constant<int, 2>{}); break;
+        case 3: body(std::integral_constant<int, 3>{}); break;
+        case 4: body(std::integral_constant<int, 4>{}); break;
+        case 5: body(std::integral_constant<int, 5>{}); break;
+        case 6: body(std::integral_constant<int, 6>{}); break;
+        default: body(std::integral_constant<int, 7>{}); break;
+      }
+      __syncthreads();
+    };
+    int c = 0;
+    for (; c + 1 < nch; c += 2) {
+      chunk(I0{}, c);
+      chunk(I1{}, c + 1);
+    }
+    if (c < nch) chunk(I0{}, c);
+    __syncthreads();  // (the bias column of both buffers is rewritten for the next segment)
+  }
+  // slab store: acc[4 ii + jj] -> C[16 (i0 + ii) + 4 g + r][jbase + 16 (j0 + jj) + c16]
+  float* out = slab + (size_t)z * G::KR * FG;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int igw = G::ig(w), i0w = G::i0(igw), niw = G::ni(igw), j0w = G::j0(w), njw = G::nj(w);
+#pragma unroll
+  for (int ii = 0; ii < G::NIG; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int col = 16 * (j0w + jj) + c16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * (i0w + ii) + 4 * g + r;
+        if (ii < niw && jj < njw && i < G::KR && col < WQ_CD) out[(size_t)i * FG + jbase + col] = acc[ii * 4 + jj][r];
+      }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // fp32 input gradient on the bf16 matrix pipe: dX = dZ W^T with the exact three-term split
 // ------------------------------------------------------------------------------------------
 // Same split as lstmf_wgrad_split_kernel (a = h + m + l by truncation, six products
@@ -1668,6 +1915,139 @@ lstmf_dgrad_split_kernel(const float* __restrict__ D, const float* __restrict__ 
       for (int i = 0; i < 4; ++i) st1(v[i], rx, col < KO && row + i < nrows ? ((row + i) * KO + col) * 4 : kOOB, 0);
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// fp32 input gradient on the bf16 matrix pipe, LDS-staged: lstmf_dgrad_s4_kernel
+// ------------------------------------------------------------------------------------------
+// dX = dZ W^T with the exact three-term split (six products, dropped terms <= 2^-24 of each product).
+// lstmf_dgrad_split_kernel splits the 400-long reduction across its 8 waves and reduces their partial
+// tiles in LDS per 16-row tile (barrier + 8-way sum per tile: slower than the exact kernel).  Here the
+// reduction stays inside one wave: 4 waves (one per SIMD, 512-register budget), wave w owns output
+// columns 32 w .. 32 w + 31 (two 16-column tiles) and holds the three W^T planes of BOTH tiles and ALL 13
+// k-steps (k = 400..415 zero) in registers (312 VGPRs).  The 16-row dZ chunks are fp32-loaded two chunks
+// ahead (two register sets), split into the three bf16 planes and stored to a double-buffered LDS image
+// (row stride 408 elements: conflict-free ds_read_b128 A fragments) in slices between the second half
+// of the k-steps, so the split's VALU issue interleaves with the wave's MFMAs.  One barrier per chunk;
+// each chunk's output tiles are final (no partial tiles, no cross-wave reduction).
+constexpr int DS4_RS = 408;                   // LDS image row stride (bf16 elements)
+constexpr int DS4_PL = 16 * DS4_RS * 2;       // bytes per plane image (16 rows)
+constexpr int DS4_BUF = 3 * DS4_PL;           // one buffer: three planes
+constexpr int DS4_SLOTS = (16 * 100 + 255) / 256;  // float4 staging slots per thread per chunk (7)
+constexpr int DS4_K0 = DS_KS - DS4_SLOTS;     // first k-step followed by a staging slot
+
+template <int NT2>
+__global__ void __launch_bounds__(256, 1)
+lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, float* __restrict__ X, int M, int KO) {
+  extern __shared__ __attribute__((aligned(16))) char dsm_[];
+  lds_char* dsm = (lds_char*)dsm_;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int nch = (M + 15) / 16;
+  // W^T planes of output tiles 2 w + e: B[k = 32 ks + 8 g + j][col 16 (2 w + e) + c16] = W[col][k]
+  bf16x8 bw[2][DS_KS][3];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int col = 16 * (2 * w + e) + c16;
+#pragma unroll
+    for (int ks = 0; ks < DS_KS; ++ks) {
+      const int k0 = 32 * ks + 8 * g;
+      f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
+      if (w < NT2 && col < KO && k0 < FG) {
+        v0 = *reinterpret_cast<const f32x4*>(W + (size_t)col * FG + k0);
+        v1 = *reinterpret_cast<const f32x4*>(W + (size_t)col * FG + k0 + 4);
+      }
+      uint32_t p0[3][2], p1[3][2];
+      split3(v0, p0);
+      split3(v1, p1);
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        bw[e][ks][q] = __builtin_bit_cast(bf16x8, make_uint4(p0[q][0], p0[q][1], p1[q][0], p1[q][1]));
+    }
+  }
+  f32x4 v[2][DS4_SLOTS];
+  auto load = [&](auto S_, int c) {  // chunk c's rows (past M: zero-size descriptor, zeros)
+    constexpr int S = decltype(S_)::value;
+    const int r0 = c * 16, nr = c < nch ? min(16, M - r0) : 0;
+    const rsrc_t rd = make_rsrc(D + (nr ? (size_t)r0 * FG : 0), nr * FG * 4);
+#pragma unroll
+    for (int j = 0; j < DS4_SLOTS; ++j) {
+      const int e = tid + 256 * j, r = e / 100, c4 = e - 100 * r;
+      v[S][j] = ld4(rd, e < 1600 ? (r * FG + 4 * c4) * 4 : kOOB);
+    }
+  };
+  auto stage = [&](auto S_, lds_char* buf, int j) {
+    constexpr int S = decltype(S_)::value;
+    const int e = tid + 256 * j, r = e / 100, c4 = e - 100 * r;
+    if (e >= 1600) return;
+    uint32_t p[3][2];
+    split3(v[S][j], p);
+    const int lo = (r * DS4_RS + 4 * c4) * 2;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(buf + q * DS4_PL + lo) = u32x2_t{p[q][0], p[q][1]};
+  };
+  // zero the k = 400..407 pad columns of both buffers (never staged; the k-step 12 fragments read them)
+  for (int i = tid; i < 2 * 3 * 16; i += 256) {
+    const int b = i / 48, q = (i / 16) % 3, r = i % 16;
+    *reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(dsm + b * DS4_BUF + q * DS4_PL + (r * DS4_RS + FG) * 2) =
+        u32x4_t{0, 0, 0, 0};
+  }
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  const int cs = gridDim.x;
+  // prologue: the first chunk staged into buffer 0, the second in flight in set 1
+  load(I0{}, blockIdx.x);
+#pragma unroll
+  for (int j = 0; j < DS4_SLOTS; ++j) stage(I0{}, dsm, j);
+  load(I1{}, blockIdx.x + cs);
+  __syncthreads();
+  const int ao = (c16 * DS4_RS + 8 * g) * 2;  // this lane's A fragment: row c16, k = 8 g .. + 7 of a k-step
+  // chunk cc (buffer S): chunk cc + 2 cs loaded into set S, the MFMAs on buffer S, chunk cc + cs (set
+  // S ^ 1) split into buffer S ^ 1 in slices after the last DS4_SLOTS k-steps (unconditional: past
+  // the end it stages zeros)
+  auto chunk = [&](auto S_, int cc) {
+    constexpr int S = decltype(S_)::value;
+    load(S_, cc + 2 * cs);
+    const lds_char* A_ = dsm + S * DS4_BUF;
+    lds_char* nxt = dsm + (S ^ 1) * DS4_BUF;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < DS_KS; ++ks) {
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 a[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(A_ + q * DS4_PL + ao + 64 * ks);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        acc[e] = mma32(a[2], bw[e][ks][0], acc[e]);  // lh
+        acc[e] = mma32(a[0], bw[e][ks][2], acc[e]);  // hl
+        acc[e] = mma32(a[1], bw[e][ks][1], acc[e]);  // mm
+        acc[e] = mma32(a[1], bw[e][ks][0], acc[e]);  // mh
+        acc[e] = mma32(a[0], bw[e][ks][1], acc[e]);  // hm
+        acc[e] = mma32(a[0], bw[e][ks][0], acc[e]);  // hh
+      }
+      if (ks >= DS4_K0) stage(std::integral_constant<int, S ^ 1>{}, nxt, ks - DS4_K0);  // (compile-time)
+    }
+    // output rows 16 cc + 4 g + i, columns 16 (2 w + e) + c16
+    const int nr = min(16, M - 16 * cc);
+    const rsrc_t rx = make_rsrc(X + (size_t)16 * cc * KO, nr * KO * 4);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int col = 16 * (2 * w + e) + c16;
+      const bool ok = w < NT2 && col < KO;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st1(acc[e][i], rx, ok ? ((4 * g + i) * KO + col) * 4 : kOOB, 0);
+    }
+    __syncthreads();
+  };
+  int c = blockIdx.x;
+  for (; c + cs < nch; c += 2 * cs) {
+    chunk(I0{}, c);
+    chunk(I1{}, c + cs);
+  }
+  if (c < nch) chunk(I0{}, c);
 }
 
 // ==========================================================================================
@@ -1927,18 +2307,41 @@ static int wgrads_z(int M) {
   const int chunks = (M + 31) / 32, half = device_cu_count() / 2;
   return chunks < half ? chunks : half;
 }
+// quad kernel: Z row ranges x 4 column quarters, one workgroup per CU
+static int wgradq_z(int M) {
+  const int chunks = (M + 31) / 32, q = device_cu_count() / 4;
+  return chunks < q ? chunks : q;
+}
 static int wgradf_pick(int impl, int K) {
-  const int v = impl == 1 || impl == 2 ? impl : wgradf_version();
+  const int v = impl >= 1 && impl <= 3 ? impl : wgradf_version();
   return v ? v : (K <= 36 ? 2 : 1);
 }
 size_t lstmf_wgrad_workspace_floats(int M, int K, int impl) {
-  const int z = wgradf_pick(impl, K) == 1 ? wgradf_grid(M) : wgrads_z(M);
+  const int v = wgradf_pick(impl, K);
+  const int z = v == 1 ? wgradf_grid(M) : v == 3 ? wgradq_z(M) : wgrads_z(M);
   return (size_t)z * (K + FH + 1) * FG;
 }
 
 bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
                         float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl) {
   if (!lstmf_wgrad_supported(K, FH, FG) || M <= 0) return false;
+  if (wgradf_pick(impl, K) == 3) {
+    const int z0 = wgradq_z(M);
+    const int rpz = ((M + z0 - 1) / z0 + 31) / 32 * 32;
+    const int z = (M + rpz - 1) / rpz;
+    const size_t sm = 2 * WS_BUF;
+    auto go = [&](auto k) {
+      allow_lds(reinterpret_cast<const void*>(k));
+      hipLaunchKernelGGL(k, dim3(4 * z), dim3(512), sm, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpz, z);
+    };
+    switch (K) {
+      case 32: go(lstmf_wgrad_q4_kernel<32>); break;
+      case 36: go(lstmf_wgrad_q4_kernel<36>); break;
+      default: go(lstmf_wgrad_q4_kernel<100>); break;
+    }
+    launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s);
+    return true;
+  }
   if (wgradf_pick(impl, K) != 1) {
     const int z0 = wgrads_z(M);
     const int rpz = ((M + z0 - 1) / z0 + 31) / 32 * 32;
@@ -1984,7 +2387,22 @@ static int dgradf_version() {
 
 bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl) {
   if (!lstmf_dgrad_supported(N, KO) || M <= 0) return false;
-  if ((impl == 1 || impl == 2 ? impl : dgradf_version()) == 2) {
+  if ((impl >= 1 && impl <= 3 ? impl : dgradf_version()) == 3) {
+    const int chunks = (M + 15) / 16, cus = device_cu_count();
+    const int grid = chunks < cus ? chunks : cus;
+    auto go = [&](auto k) {
+      allow_lds(reinterpret_cast<const void*>(k));
+      hipLaunchKernelGGL(k, dim3(grid), dim3(256), (size_t)2 * DS4_BUF, s, D, W, X, M, KO);
+    };
+    switch ((KO + 31) / 32) {
+      case 1: go(lstmf_dgrad_s4_kernel<1>); break;
+      case 2: go(lstmf_dgrad_s4_kernel<2>); break;
+      case 3: go(lstmf_dgrad_s4_kernel<3>); break;
+      default: go(lstmf_dgrad_s4_kernel<4>); break;
+    }
+    return true;
+  }
+  if ((impl >= 1 && impl <= 3 ? impl : dgradf_version()) == 2) {
     const int chunks = (M + 15) / 16, cus = device_cu_count();
     int grid = chunks < cus ? chunks : cus;
     const int min_grid = (int)(((long long)M * FG * 4 + (1ll << 31) - 1) / (1ll << 31));

@@ -24,7 +24,8 @@ def main():
     a = ap.parse_args()
     dt = getattr(torch, a.dtype)
     # bf16: impl 2 = tile kernel (gemm2), 0 = LDS-DMA streaming (wgrad3); fp32: 1 = exact MFMA, 2 = bf16 split
-    impls, names = ((2, 0), {2: "wgrad2", 0: "wgrad3"}) if dt == torch.bfloat16 else ((1, 2), {1: "f32_exact", 2: "f32_split"})
+    impls, names = (((2, 0), {2: "wgrad2", 0: "wgrad3"}) if dt == torch.bfloat16 else
+                    ((1, 2, 3), {1: "f32_exact", 2: "f32_split", 3: "f32_split_quad"}))
     dev = torch.device("cuda:0")
     H, N = 100, 400
     for K, rows_mult, tangent in [(32, 2, False), (100, 2, False), (32, 1, True), (100, 1, True)]:
@@ -57,9 +58,10 @@ def main():
             gW.zero_(); gU.zero_(); gb.zero_()
             Fn.lstm_wgrad_(x, hs, dZ, gW, gU, gb, *seg, impl=impl)
             outs.append(torch.cat([gW.flatten(), gU.flatten(), gb]).clone())
-        rel = ((outs[0] - outs[1]).abs().max() / outs[0].abs().max()).item()
-        print(json.dumps({"K": K, "tangent": tangent, "maxrel": rel, "speedup": round(res[impls[0]] / res[impls[1]], 2)}),
-              flush=True)
+        for o, impl in zip(outs[1:], impls[1:]):
+            rel = ((outs[0] - o).abs().max() / outs[0].abs().max()).item()
+            print(json.dumps({"K": K, "tangent": tangent, "impl": names[impl], "maxrel_vs_first": rel,
+                              "speedup": round(res[impls[0]] / res[impl], 2)}), flush=True)
 
 
 if __name__ == "__main__":

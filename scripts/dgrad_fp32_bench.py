@@ -37,14 +37,17 @@ def main():
             fl = 2.0 * M * 400 * KO
             t_n = timeit(lambda: ops.lstmf_dgrad(dz, W, 1))
             t_s = timeit(lambda: ops.lstmf_dgrad(dz, W, 2))
+            t_4 = timeit(lambda: ops.lstmf_dgrad(dz, W, 3))
             t_t = timeit(lambda: torch.mm(dz, W.t()))
             diff = (ops.lstmf_dgrad(dz, W, 1) - torch.mm(dz, W.t())).abs().max().item()
             diff_s = (ops.lstmf_dgrad(dz, W, 2) - ops.lstmf_dgrad(dz, W, 1)).abs().max().item()
+            diff_4 = (ops.lstmf_dgrad(dz, W, 3) - ops.lstmf_dgrad(dz, W, 1)).abs().max().item()
             print(json.dumps({"op": "lstmf_dgrad", "M": M, "KO": KO, "native_ms": round(t_n, 3),
-                              "split_ms": round(t_s, 3), "hipblaslt_ms": round(t_t, 3),
+                              "split_ms": round(t_s, 3), "split_lds_ms": round(t_4, 3), "hipblaslt_ms": round(t_t, 3),
                               "native_tf": round(fl / t_n / 1e9, 1), "split_tf": round(fl / t_s / 1e9, 1),
                               "hipblaslt_tf": round(fl / t_t / 1e9, 1), "split_GBs": round(M * 400 * 4 / t_s / 1e6, 0),
-                              "maxdiff": diff, "split_vs_exact_maxdiff": diff_s}), flush=True)
+                              "maxdiff": diff, "split_vs_exact_maxdiff": diff_s, "split_lds_vs_exact_maxdiff": diff_4}),
+                  flush=True)
         del dz
         torch.cuda.empty_cache()
 

@@ -27,12 +27,10 @@ def test_no_buffer_store_data_hazard(tmp_path):
     # on register allocation, so the scanned assembly must come from the same compile as the library
     from hfrep import build_native
 
-    kern_flags = build_native._flags()[0]
-
     def asm(src):
         out = str(tmp_path / (os.path.basename(src) + ".s"))
-        subprocess.run([HIPCC] + kern_flags + ["--cuda-device-only", "-S", src, "-o", out], check=True,
-                       capture_output=True)
+        subprocess.run([HIPCC] + build_native.kernel_flags(src) + ["--cuda-device-only", "-S", src, "-o", out],
+                       check=True, capture_output=True)
         return out
 
     with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:

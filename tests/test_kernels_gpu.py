@@ -772,7 +772,7 @@ def test_lstmf_wgrad_split_vs_exact(cuda, B, T, K, tangent):
         rW = rW + xd.double().reshape(-1, K).t() @ dzd.double().reshape(-1, N)
         rU = rU + R.shift_prev(hds.double()).reshape(-1, H).t() @ dzd.double().reshape(-1, N)
     errs = {}
-    for impl in (1, 2, 2):
+    for impl in (1, 2, 2, 3, 3):
         gW, gU, gb = torch.zeros(K, N, device=cuda), torch.zeros(H, N, device=cuda), torch.zeros(N, device=cuda)
         Fn.lstm_wgrad_(x, hs, dz, gW, gU, gb, xd, hds, dzd, impl=impl)
         out = torch.cat([gW.reshape(-1), gU.reshape(-1), gb])
@@ -782,9 +782,10 @@ def test_lstmf_wgrad_split_vs_exact(cuda, B, T, K, tangent):
         ref = torch.cat([rW.reshape(-1), rU.reshape(-1), rb])
         errs[impl] = ((out.double() - ref).abs().max().item(), out)
     refmax = max(rW.abs().max().item(), rU.abs().max().item(), rb.abs().max().item())
-    e1, e2 = errs[1][0], errs[2][0]
-    print(f"max abs err exact {e1:.3e} split {e2:.3e} (max |ref| {refmax:.3e})")
+    e1, e2, e3 = errs[1][0], errs[2][0], errs[3][0]
+    print(f"max abs err exact {e1:.3e} split {e2:.3e} quad split {e3:.3e} (max |ref| {refmax:.3e})")
     assert e1 <= 1e-5 * refmax + 1e-5 and e2 <= 2 * e1 + 1e-6 * refmax, (e1, e2, refmax)
+    assert e3 <= 2 * e1 + 1e-6 * refmax, (e1, e3, refmax)
 
 
 @pytest.mark.parametrize("K,tangent", [(100, False), (32, True)])
@@ -807,7 +808,7 @@ def test_lstmf_wgrad_large_m(cuda, K, tangent):
     rb = dz.double().reshape(-1, N).sum(0)
     # random-sign sums of 3 M products: scale by the root-sum-square, not the absolute sum
     tol = 2e-5 * (B * T) ** 0.5 * (2 if tangent else 1)
-    for impl in (1, 2):
+    for impl in (1, 2, 3):
         gW, gU, gb = (torch.zeros(K, N, device=cuda), torch.zeros(H, N, device=cuda), torch.zeros(N, device=cuda))
         Fn.lstm_wgrad_(x, hs, dz, gW, gU, gb, xd, hds, dzd, impl=impl)
         for got, ref in ((gW, rW), (gU, rU), (gb, rb)):
@@ -827,7 +828,7 @@ def test_lstmf_dgrad(cuda, M, KO):
     ref = dz.double() @ W.double().t()
     scale = (dz.abs().double() @ W.abs().double().t()).max().item()
     errs = {}
-    for impl in (1, 2):  # exact-fp32 MFMA kernel, three-term bf16 split kernel (the default)
+    for impl in (1, 2, 3):  # exact-fp32 MFMA kernel, three-term bf16 split kernels (partial-sum / LDS-staged)
         out = _native.native().lstmf_dgrad(dz.to(cuda), W.to(cuda), impl)
         _close(out, ref, torch.float32, scale=scale)
         again = _native.native().lstmf_dgrad(dz.to(cuda), W.to(cuda), impl)
@@ -835,6 +836,7 @@ def test_lstmf_dgrad(cuda, M, KO):
         errs[impl] = (out.double().cpu() - ref).abs().max().item()
     # the split's dropped terms are <= 2^-24 of each product: within 2x the exact kernel's error
     assert errs[2] <= 2 * errs[1] + 1e-6 * scale, errs
+    assert errs[3] <= 2 * errs[1] + 1e-6 * scale, errs
 
 
 def test_gan_eval_device_path(cuda):
