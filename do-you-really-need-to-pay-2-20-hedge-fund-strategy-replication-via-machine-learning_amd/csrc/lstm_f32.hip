@@ -1743,12 +1743,23 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
 #pragma unroll
               for (int q = 0; q < 3; ++q) bfr[jj][q] = tr_frag<WS_ROWD>(D_ + q * WS_PLD, tro_d, 16 * (J0 + 2 * jh + jj));
             }
+          // A fragments one i-tile ahead (two sets) where the registers allow (K <= 36): the LDS
+          // latency hides under the MFMAs
+          constexpr bool PF = KX <= 36;
+          bf16x8 af[2][3];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) af[0][q] = tr_frag<WS_ROWA>(A_ + q * WS_PLA, tro_a, 16 * I0);
 #pragma unroll
           for (int ii = 0; ii < NIW; ++ii) {
             __builtin_amdgcn_sched_barrier(0);
-            bf16x8 a3[3];
+            if (PF && ii + 1 < NIW) {
 #pragma unroll
-            for (int q = 0; q < 3; ++q) a3[q] = tr_frag<WS_ROWA>(A_ + q * WS_PLA, tro_a, 16 * (I0 + ii));
+              for (int q = 0; q < 3; ++q) af[(ii + 1) & 1][q] = tr_frag<WS_ROWA>(A_ + q * WS_PLA, tro_a, 16 * (I0 + ii + 1));
+            } else if (!PF && ii > 0) {
+#pragma unroll
+              for (int q = 0; q < 3; ++q) af[ii & 1][q] = tr_frag<WS_ROWA>(A_ + q * WS_PLA, tro_a, 16 * (I0 + ii));
+            }
+            const bf16x8(&a3)[3] = af[ii & 1];
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj) {
               if (2 * jh + jj >= NJW) continue;  // (compile-time)
@@ -1927,10 +1938,10 @@ lstmf_dgrad_split_kernel(const float* __restrict__ D, const float* __restrict__ 
 // columns 32 w .. 32 w + 31 (two 16-column tiles) and holds the three W^T planes of BOTH tiles and ALL 13
 // k-steps (k = 400..415 zero) in registers (312 VGPRs).  The 16-row dZ chunks are fp32-loaded two chunks
 // ahead (two register sets), split into the three bf16 planes and stored to a double-buffered LDS image
-// (row stride 408 elements: conflict-free ds_read_b128 A fragments) in slices between the second half
+// (row stride 424 elements: conflict-free ds_read_b128 A fragments) in slices between the second half
 // of the k-steps, so the split's VALU issue interleaves with the wave's MFMAs.  One barrier per chunk;
 // each chunk's output tiles are final (no partial tiles, no cross-wave reduction).
-constexpr int DS4_RS = 408;                   // LDS image row stride (bf16 elements)
+constexpr int DS4_RS = 424;                   // LDS image row stride (bf16 elements): >= 416, conflict-free b128
 constexpr int DS4_PL = 16 * DS4_RS * 2;       // bytes per plane image (16 rows)
 constexpr int DS4_BUF = 3 * DS4_PL;           // one buffer: three planes
 constexpr int DS4_SLOTS = (16 * 100 + 255) / 256;  // float4 staging slots per thread per chunk (7)
@@ -1962,8 +1973,13 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
       split3(v0, p0);
       split3(v1, p1);
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < 3; ++q) {
         bw[e][ks][q] = __builtin_bit_cast(bf16x8, make_uint4(p0[q][0], p0[q][1], p1[q][0], p1[q][1]));
+        // tile 1's planes live in the accumulator half of the register file (MFMA B operands may be
+        // AGPRs): without the pin the compiler parks them there anyway and copies each one back to
+        // VGPRs before its MFMA (4 v_accvgpr_read per MFMA)
+        if (e == 1) asm volatile("" : "+a"(bw[e][ks][q]));
+      }
     }
   }
   f32x4 v[2][DS4_SLOTS];
@@ -1988,11 +2004,11 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
     for (int q = 0; q < 3; ++q)
       *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(buf + q * DS4_PL + lo) = u32x2_t{p[q][0], p[q][1]};
   };
-  // zero the k = 400..407 pad columns of both buffers (never staged; the k-step 12 fragments read them)
-  for (int i = tid; i < 2 * 3 * 16; i += 256) {
-    const int b = i / 48, q = (i / 16) % 3, r = i % 16;
-    *reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(dsm + b * DS4_BUF + q * DS4_PL + (r * DS4_RS + FG) * 2) =
-        u32x4_t{0, 0, 0, 0};
+  // zero the k = 400..415 pad columns of both buffers (never staged; the k-step 12 fragments read them)
+  for (int i = tid; i < 2 * 3 * 16 * 2; i += 256) {
+    const int h = i & 1, b = i / 96, q = (i / 32) % 3, r = (i / 2) % 16;
+    *reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(dsm + b * DS4_BUF + q * DS4_PL +
+                                                                  (r * DS4_RS + FG + 8 * h) * 2) = u32x4_t{0, 0, 0, 0};
   }
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -2013,12 +2029,19 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
     const lds_char* A_ = dsm + S * DS4_BUF;
     lds_char* nxt = dsm + (S ^ 1) * DS4_BUF;
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    // A fragments one k-step ahead (two sets): the LDS latency hides under the previous k-step's MFMAs
+    bf16x8 af[2][3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) af[0][q] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(A_ + q * DS4_PL + ao);
 #pragma unroll
     for (int ks = 0; ks < DS_KS; ++ks) {
       __builtin_amdgcn_sched_barrier(0);
-      bf16x8 a[3];
+      if (ks + 1 < DS_KS) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(A_ + q * DS4_PL + ao + 64 * ks);
+        for (int q = 0; q < 3; ++q)
+          af[(ks + 1) & 1][q] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(A_ + q * DS4_PL + ao + 64 * (ks + 1));
+      }
+      const bf16x8(&a)[3] = af[ks & 1];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         acc[e] = mma32(a[2], bw[e][ks][0], acc[e]);  // lh
@@ -2292,9 +2315,9 @@ static int wgradf_grid(int M) {
 }
 bool lstmf_wgrad_supported(int K, int H, int N) { return H == FH && N == FG && (K == 32 || K == 36 || K == 100); }
 
-// HFREP_LSTMF_WGRAD=1 / 2: force the exact-fp32 MFMA kernel / the three-term bf16 split; default (0):
-// the split for K <= 36 (12.1 -> 9.8 ms at 12.6 M rows), the exact kernel for K = 100, where the split
-// kernel's 28-tile waves spill (52.8 vs 16.4 ms; profiles/r02_split)
+// HFREP_LSTMF_WGRAD=1 / 2 / 3: force the exact-fp32 MFMA kernel / the three-term bf16 split (pair) /
+// the split quad; default (0): the pair split for K <= 36 (12.1 -> 9.8 ms at 12.6 M rows), the quad
+// for K = 100 (16.4 -> 15.3 ms; the pair kernel's 28-tile waves spill there: 52.8 ms; profiles/r03_split)
 static int wgradf_version() {
   static const int v = [] {
     const char* e = getenv("HFREP_LSTMF_WGRAD");
@@ -2314,7 +2337,7 @@ static int wgradq_z(int M) {
 }
 static int wgradf_pick(int impl, int K) {
   const int v = impl >= 1 && impl <= 3 ? impl : wgradf_version();
-  return v ? v : (K <= 36 ? 2 : 1);
+  return v ? v : (K <= 36 ? 2 : 3);
 }
 size_t lstmf_wgrad_workspace_floats(int M, int K, int impl) {
   const int v = wgradf_pick(impl, K);
@@ -2373,21 +2396,23 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
 
 bool lstmf_dgrad_supported(int N, int KO) { return N == FG && KO >= 1 && KO <= 16 * FNT; }
 
-// HFREP_LSTMF_DGRAD_IMPL=2: the three-term bf16 split kernel; default 1: the exact-fp32 MFMA kernel
-// (the split one measured slower: 5.76 vs 4.69 ms at 6.3 M rows, KO = 100; 3.56 vs 2.28 at KO = 32 --
-// 16-row tiles with a barrier and an 8-wave reduction each do not hide the dZ stream;
-// profiles/r02_split/dgrad_split_vs_exact.jsonl)
+// HFREP_LSTMF_DGRAD_IMPL=1 / 2 / 3: the exact-fp32 MFMA kernel / the partial-sum split kernel (slower
+// than exact: 5.76 vs 4.69 ms at 6.3 M rows, KO = 100 -- 16-row tiles with a barrier and an 8-wave
+// reduction each do not hide the dZ stream; profiles/r02_split) / the LDS-staged split kernel
+// lstmf_dgrad_s4_kernel; default (0): s4 for KO > 64, exact otherwise (s4 keeps one wave busy per
+// 32 output columns, so KO = 32 leaves three SIMDs idle; profiles/r03_split)
 static int dgradf_version() {
   static const int v = [] {
     const char* e = getenv("HFREP_LSTMF_DGRAD_IMPL");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   return v;
 }
 
 bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl) {
   if (!lstmf_dgrad_supported(N, KO) || M <= 0) return false;
-  if ((impl >= 1 && impl <= 3 ? impl : dgradf_version()) == 3) {
+  const int dv = impl >= 1 && impl <= 3 ? impl : dgradf_version();
+  if (dv == 3 || (dv == 0 && KO > 64)) {
     const int chunks = (M + 15) / 16, cus = device_cu_count();
     const int grid = chunks < cus ? chunks : cus;
     auto go = [&](auto k) {
@@ -2402,7 +2427,7 @@ bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, 
     }
     return true;
   }
-  if ((impl >= 1 && impl <= 3 ? impl : dgradf_version()) == 2) {
+  if (dv == 2) {
     const int chunks = (M + 15) / 16, cus = device_cu_count();
     int grid = chunks < cus ? chunks : cus;
     const int min_grid = (int)(((long long)M * FG * 4 + (1ll << 31) - 1) / (1ll << 31));
