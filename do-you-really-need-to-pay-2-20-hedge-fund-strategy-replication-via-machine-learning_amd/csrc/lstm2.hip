@@ -1503,8 +1503,8 @@ __device__ __forceinline__ void tape_image_store(const bf16_t* img, rsrc_t rt, i
       // non-temporal (aux 2 = nt): the tape is read back only by the reverse kernels, long after;
       // under the nt policy the concurrent x reads of the recurrence wait less behind it (tape
       // forward 2.72 -> 2.55 ms, tangent 3.33 -> 3.03 ms at B = 262144; sc1 / sc0 sc1: no gain;
-      // nt on the reverse kernels' dZ stores: BPTT +8 %; nt tape loads: tangent reverse +3-4 %.  scripts/gpu_store_policy.sh,
-      // scripts/gpu_ab_lstm.sh, profiles/r01_fwd5/store_policy.jsonl)
+      // nt on the reverse kernels' dZ stores: BPTT +8 %; nt tape loads: tangent reverse +3-4 %.  profiles/archive_scripts/gpu_store_policy.sh,
+      // profiles/archive_scripts/gpu_ab_lstm.sh, profiles/r01_fwd5/store_policy.jsonl)
       __builtin_amdgcn_raw_buffer_store_b128(d[j], rt, ok ? base + ch * 1024 : kOOB, 0, 2);
     }
   }

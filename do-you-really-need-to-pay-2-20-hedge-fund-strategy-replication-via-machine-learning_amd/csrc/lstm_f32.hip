@@ -180,7 +180,7 @@ __device__ __forceinline__ void st4(f32x4 v, rsrc_t r, int voff) {
 // than 8 bytes whose data VGPRs the next VALU instruction overwrites needs one wait state, and the
 // compiler only inserts it when soffset is NOT a register: with the uniform step offset in soffset
 // the BPTT's dZ stores wrote the next value for a few 16-byte chunks per 10^5 rows (rows 14 / 15
-// of a 32-row block, r02: scripts/dbg_large_bwd.py, scripts/isa_store_hazard.py)
+// of a 32-row block, r02: profiles/archive_scripts/dbg_large_bwd.py, scripts/isa_store_hazard.py)
 __device__ __forceinline__ void st16(f32x4 v, rsrc_t r, bool ok, int voff, int uoff) {
   // (unsigned: voff may already be kOOB; the sum stays past every descriptor's size)
   const int off = (int)((unsigned)voff + (unsigned)uoff);
