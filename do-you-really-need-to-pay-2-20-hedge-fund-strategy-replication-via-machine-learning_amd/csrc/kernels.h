@@ -65,6 +65,9 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
                         float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl = 0);
 // fp32 input gradient X (M, KO) = D (M, N) W^T, W (KO, N) row-major; N = 400, KO <= 112
 bool lstmf_dgrad_supported(int N, int KO);
+// forward kernel selection: 1 = exact-fp32 everywhere, 2 = split recurrent product for K <= 36 (default);
+// returns the previous setting
+int set_lstmf_fwd_impl(int v);
 // impl: 0 = default (HFREP_LSTMF_DGRAD_IMPL, else the exact-fp32 MFMA kernel), 1 = exact, 2 = three-term bf16 split
 bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl = 0);
 

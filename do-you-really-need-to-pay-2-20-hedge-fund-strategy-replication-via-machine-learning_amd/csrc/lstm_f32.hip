@@ -31,6 +31,7 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <type_traits>
@@ -1928,6 +1929,258 @@ lstmf_dgrad_split_kernel(const float* __restrict__ D, const float* __restrict__ 
   }
 }
 
+// ==========================================================================================
+// forward / tangent forward with the recurrent product on the bf16 pipe (K <= 36 layers)
+// ==========================================================================================
+// lstmf_fwd_kernel spends 25 of its 33 k-steps per tile on h_{t-1} U (K = 32: 800 of 1056 MFMA cycles
+// per tile and row half on v_mfma_f32_16x16x4_f32).  Here h_{t-1} U runs as the exact three-term split
+// (h = h_h + h_m + h_l, U = U_h + U_m + U_l by truncation, six products lh + hl + mm + mh + hm + hh on
+// v_mfma_f32_16x16x32_bf16, dropped terms <= 2^-24 of each product) over k = 0..95 and exactly in fp32
+// for k = 96..99 (one 16x16x4 k-step): 3 x 6 x 16 + 32 = 320 instead of 800 cycles per tile and row
+// half.  The split products chain into the exact-fp32 x W accumulator.  U's planes (3 k-steps x 7 tiles x 3 planes, 252 registers) are pinned in AGPRs; h_{t-1} lives
+// in LDS as three bf16 planes [32 rows][104] (row stride: conflict-free ds_read_b128) plus an fp32
+// tail [32][4]; the cell update writes its h (or hdot) straight into them.  Everything else -- the
+// gate-interleaved tiles, the quad transpose, the tapes, x W on the exact fp32 MFMA -- is
+// lstmf_fwd_kernel's.
+constexpr int FS_HR = 104;                                // h plane row stride (bf16 elements)
+constexpr int FS_HPL = 32 * FS_HR * 2;                    // bytes per h plane (32 rows)
+constexpr int FS_HB = 3 * FS_HPL + 32 * 4 * 4;            // one h buffer: 3 planes + fp32 tail [32][4]
+
+__device__ __forceinline__ uint32_t trunc_hi(float a) { return __builtin_bit_cast(uint32_t, a) & 0xffff0000u; }
+
+template <int ACT, int KX, bool TAPE, bool TAN>
+__global__ void __launch_bounds__(256, 1)
+lstmf_fwds_kernel(const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
+                  const float* __restrict__ U, const float* __restrict__ ptape, float* __restrict__ hs,
+                  float* __restrict__ tape, int B, int Tn) {
+  using GX = FGeo<KX>;
+  static_assert(GX::KS <= 12, "split forward: K <= 48 (W^T in registers)");
+  constexpr int NW = GX::KS;
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  float* xb = fsm;                                                  // [2][32 * LRX] fp32, K-permuted
+  lds_char* hb = (lds_char*)(xb + 2 * 32 * GX::LR);                 // [2][FS_HB] h planes + tail
+  float* trash = reinterpret_cast<float*>(hb + 2 * FS_HB);          // [4] (x-tile loader padding)
+  lds_char* trashc = hb + 2 * FS_HB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane & 3, g = lane >> 4, j4 = (lane & 15) >> 2;
+  const int ub = FUW * w + j4;
+  const int nrb = (B + 31) / 32;
+
+  for (int i = tid; i < 2 * 32 * GX::LR; i += 256) xb[i] = 0.f;
+
+  constexpr float GSC = ACT == ACT_TANH ? -2.f * kLog2e : ACT == ACT_SIGMOID ? -kLog2e : 1.f;
+  const float sc = TAN ? 1.f : (q == 2 ? GSC : -kLog2e);
+  // B operands.  16x16x32: lane l holds B[k = 32 ks + 8 (l >> 4) + j][col l & 15] (j < 8); the fp32
+  // tail 16x16x4: B[k = 96 + (l >> 4)][col]; x W (16x16x4): B[k = 4 ks + (l >> 4)][col]
+  bf16x8 up[3][FNT][3];
+  float ut[FNT], wf[NW][FNT], bq[FNT];
+#pragma unroll
+  for (int n = 0; n < FNT; ++n) {
+    const int u = ub + 4 * n;
+    const bool ok = u < FH;
+    const int cl = q * FH + (ok ? u : FH - 1);
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      uint32_t hh[8], mm[8], ll[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * ks + 8 * g + j;  // < 96
+        const float v = ok ? U[k * FG + cl] * sc : 0.f;
+        const uint32_t h = trunc_hi(v);
+        const float r1 = v - __builtin_bit_cast(float, h);
+        const uint32_t m = trunc_hi(r1);
+        const float r2 = r1 - __builtin_bit_cast(float, m);
+        hh[j] = h; mm[j] = m; ll[j] = __builtin_bit_cast(uint32_t, r2);
+      }
+      uint4 ph, pm, pl;
+      ph.x = __builtin_amdgcn_perm(hh[1], hh[0], 0x07060302u); ph.y = __builtin_amdgcn_perm(hh[3], hh[2], 0x07060302u);
+      ph.z = __builtin_amdgcn_perm(hh[5], hh[4], 0x07060302u); ph.w = __builtin_amdgcn_perm(hh[7], hh[6], 0x07060302u);
+      pm.x = __builtin_amdgcn_perm(mm[1], mm[0], 0x07060302u); pm.y = __builtin_amdgcn_perm(mm[3], mm[2], 0x07060302u);
+      pm.z = __builtin_amdgcn_perm(mm[5], mm[4], 0x07060302u); pm.w = __builtin_amdgcn_perm(mm[7], mm[6], 0x07060302u);
+      pl.x = __builtin_amdgcn_perm(ll[1], ll[0], 0x07060302u); pl.y = __builtin_amdgcn_perm(ll[3], ll[2], 0x07060302u);
+      pl.z = __builtin_amdgcn_perm(ll[5], ll[4], 0x07060302u); pl.w = __builtin_amdgcn_perm(ll[7], ll[6], 0x07060302u);
+      up[ks][n][0] = __builtin_bit_cast(bf16x8, ph);
+      up[ks][n][1] = __builtin_bit_cast(bf16x8, pm);
+      up[ks][n][2] = __builtin_bit_cast(bf16x8, pl);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) asm volatile("" : "+a"(up[ks][n][p]));
+    }
+    ut[n] = ok ? U[(96 + g) * FG + cl] * sc : 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NW; ++ks) {
+      const int k = 4 * ks + g;
+      const float v = W[min(k, KX - 1) * FG + cl];
+      wf[ks][n] = (ok && k < KX) ? v * sc : 0.f;
+    }
+    const float bv = bias ? bias[cl] : 0.f;
+    bq[n] = (!TAN && ok) ? bv * sc : 0.f;
+  }
+  const bool glin = !TAN && ACT == ACT_LINEAR && q == 2;
+  const float am = (ACT == ACT_TANH && q == 2) ? 2.f : 1.f, bm = (ACT == ACT_TANH && q == 2) ? -1.f : 0.f;
+  const int ax = (lane & 15) * GX::LR + g * GX::KQ;
+  // this lane's h fragments: plane row (lane & 15) (+ 16 m), k = 32 ks + 8 g; tail row, k = 96 + g
+  const int ahp = ((lane & 15) * FS_HR + 8 * g) * 2, aht = 3 * FS_HPL + ((lane & 15) * 4 + g) * 4;
+
+  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+    const int row0 = rb * 32;
+    const rsrc_t rx = ftile_rsrc(x, row0, B, Tn, KX);
+    const rsrc_t rh = ftile_rsrc(hs, row0, B, Tn, FH);
+    const rsrc_t rt = ftape_rsrc(TAPE ? tape : nullptr, rb, nrb, Tn);
+    const rsrc_t rp = ftape_rsrc(TAN ? ptape : nullptr, rb, nrb, Tn);
+    int vp1[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) vp1[m] = ((16 * m + 4 * g + q) * Tn * FH + ub) * 4;
+    const int tl = ftape_lane(w, lane), tcl = ftape_cell(w, lane);
+    float cprev[TAN ? 2 : 1][FNT];
+    if constexpr (TAN) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < FNT; ++n) cprev[m][n] = 0.f;
+    }
+    float cst[2][FNT];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < FNT; ++n) cst[m][n] = 0.f;
+    FXPart<KX> xp;
+    xp.set(Tn, tid);
+    xp.load(rx, Tn, 0, true);
+    // h_{-1} = 0: buffer 0 planes + tail
+    for (int i = tid; i < FS_HB / 16; i += 256)
+      reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(hb)[i] = u32x4_t{0, 0, 0, 0};
+    xp.to_lds(xb, trash);
+    __syncthreads();
+    for (int t = 0; t < Tn; ++t) {
+      const float* xcur = xb + (t & 1) * 32 * GX::LR;
+      const lds_char* hcur = hb + (t & 1) * FS_HB;
+      lds_char* hnext = hb + ((t + 1) & 1) * FS_HB;
+      xp.load(rx, Tn, t + 1, t + 1 < Tn);
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        f32x4 pg[TAN ? FNT : 1];
+        float pc[TAN ? FNT : 1];
+        const int p1 = vp1[m] + t * FH * 4, tb = t * FT_STEP * 4;
+        if constexpr (TAN) {
+#pragma unroll
+          for (int n = 0; n < FNT; ++n) {
+            const bool tok = !(w == 3 && n >= 4);
+            pg[n] = ld4(rp, tok ? tl + tb + ftape_slot(m, n) : kOOB);
+            pc[n] = ld1(rp, tok ? tcl + tb + ftape_slot(m, n) : kOOB, 0);
+          }
+        }
+        f32x4 acc[FNT];
+#pragma unroll
+        for (int n = 0; n < FNT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // ---- z = x_t W (exact fp32) ----
+#pragma unroll
+        for (int j = 0; j < GX::NJ; ++j) {
+          const f32x4 a4 = *reinterpret_cast<const f32x4*>(xcur + ax + 16 * m * GX::LR + 4 * j);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int ks = 4 * j + s4;
+            if (ks >= GX::KS) break;
+#pragma unroll
+            for (int n = 0; n < FNT; ++n) acc[n] = mma4(a4[s4], wf[ks][n], acc[n]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // ---- + h_{t-1} U: the split k < 96 and the exact fp32 tail, chained into acc (20 accumulation
+        // steps per element: the MFMA C-addition rounding stays at the fp32 noise level here) ----
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+          const lds_char* ar = hcur + ahp + 16 * m * FS_HR * 2 + 64 * ks;
+          const bf16x8 a0 = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(ar);
+          const bf16x8 a1 = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(ar + FS_HPL);
+          const bf16x8 a2 = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(ar + 2 * FS_HPL);
+#pragma unroll
+          for (int n = 0; n < FNT; ++n) {
+            f32x4 t6 = acc[n];
+            t6 = mma32(a2, up[ks][n][0], t6);  // lh
+            t6 = mma32(a0, up[ks][n][2], t6);  // hl
+            t6 = mma32(a1, up[ks][n][1], t6);  // mm
+            t6 = mma32(a1, up[ks][n][0], t6);  // mh
+            t6 = mma32(a0, up[ks][n][1], t6);  // hm
+            acc[n] = mma32(a0, up[ks][n][0], t6);  // hh
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        {
+          const float at = *reinterpret_cast<const __attribute__((address_space(3))) float*>(hcur + aht + 16 * m * 16);
+#pragma unroll
+          for (int n = 0; n < FNT; ++n) acc[n] = mma4(at, ut[n], acc[n]);
+        }
+        // ---- gate math, cell update, stores (row 16 m + 4 g + q, unit ub + 4 n after the transpose) ----
+#pragma unroll
+        for (int n = 0; n < FNT; ++n) {
+          const bool tok = !(w == 3 && n >= 4);  // wave 3's tiles 4..6 are padding units 100..111
+          const int v1 = tok ? p1 + 16 * n : kOOB;
+          const f32x4 zs = acc[n];
+          float hv;
+          if constexpr (!TAN) {
+            float y[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float s_ = zs[i] + bq[n];
+              const float e = am * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(s_)) + bm;
+              y[i] = glin ? s_ : e;
+            }
+            quad_transpose(y, q);
+            const float cn = y[1] * cst[m][n] + y[0] * y[2];
+            float ca;
+            if constexpr (ACT == ACT_TANH) ca = 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(GSC * cn)) - 1.f;
+            else if constexpr (ACT == ACT_SIGMOID) ca = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(GSC * cn));
+            else ca = cn;
+            hv = tok ? y[3] * ca : 0.f;
+            cst[m][n] = cn;
+            if constexpr (TAPE) {
+              st4(f32x4{y[0], y[1], y[2], y[3]}, rt, tok ? tl + tb + ftape_slot(m, n) : kOOB);
+              st1(cn, rt, tok ? tcl + tb + ftape_slot(m, n) : kOOB, 0);
+            }
+          } else {
+            float zd[4] = {zs[0], zs[1], zs[2], zs[3]};
+            quad_transpose(zd, q);
+            const f32x4 y = pg[n];
+            const float idot = y[0] * (1.f - y[0]) * zd[0], fdot = y[1] * (1.f - y[1]) * zd[1];
+            const float gdot = act_dy(ACT, y[2]) * zd[2], odot = y[3] * (1.f - y[3]) * zd[3];
+            const float c = pc[n];
+            float cdn = fdot * cprev[m][n] + y[1] * cst[m][n] + idot * y[2] + y[0] * gdot;
+            const float ca = act_f(ACT, c);
+            float hd = odot * ca + y[3] * act_dy(ACT, ca) * cdn;
+            if (!tok) { cdn = 0.f; hd = 0.f; }
+            cst[m][n] = cdn;
+            cprev[m][n] = c;
+            hv = hd;
+            st4(f32x4{zd[0], zd[1], zd[2], zd[3]}, rt, tok ? tl + tb + ftape_slot(m, n) : kOOB);
+            st1(cdn, rt, tok ? tcl + tb + ftape_slot(m, n) : kOOB, 0);
+          }
+          // h (or hdot) of (row 16 m + 4 g + q, unit u) into the next step's planes / tail; units
+          // >= 100 (wave 3's padding tiles) go to the trash word
+          {
+            const int u = ub + 4 * n, row = 16 * m + 4 * g + q;
+            const uint32_t h1 = trunc_hi(hv);
+            const float r1 = hv - __builtin_bit_cast(float, h1);
+            const uint32_t m1 = trunc_hi(r1);
+            const uint32_t l1 = __builtin_bit_cast(uint32_t, r1 - __builtin_bit_cast(float, m1));
+            const bool pl = u < 96;
+            lds_char* dp = pl ? hnext + (row * FS_HR + u) * 2 : trashc;
+            *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(dp) = (uint16_t)(h1 >> 16);
+            *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(dp + (pl ? FS_HPL : 0)) = (uint16_t)(m1 >> 16);
+            *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(dp + (pl ? 2 * FS_HPL : 0)) = (uint16_t)(l1 >> 16);
+            const bool tl4 = u >= 96 && u < FH;
+            lds_char* tp = tl4 ? hnext + 3 * FS_HPL + (row * 4 + (u - 96)) * 4 : trashc;
+            *reinterpret_cast<__attribute__((address_space(3))) float*>(tp) = hv;
+          }
+          st1(hv, rh, v1, 0);
+        }
+      }
+      xp.to_lds(xb + ((t + 1) & 1) * 32 * GX::LR, trash);
+      lds_barrier();
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // fp32 input gradient on the bf16 matrix pipe, LDS-staged: lstmf_dgrad_s4_kernel
 // ------------------------------------------------------------------------------------------
@@ -2203,12 +2456,35 @@ void allow_lds(const void* k) {
   if (done.insert(k).second)
     HFREP_CHECK_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)F_LDS_MAX));
 }
+template <int KX>
+constexpr size_t fwds_smem() {
+  return (size_t)(2 * 32 * FGeo<KX>::LR) * 4 + 2 * FS_HB + 16;
+}
+// HFREP_LSTMF_FWD=1: the exact-fp32 forward everywhere (A / B); default: the split-recurrent forward
+// for the K <= 36 layers (lstmf_fwds_kernel)
+static std::atomic<int>& fwdf_impl() {
+  static std::atomic<int> v{[] {
+    const char* e = getenv("HFREP_LSTMF_FWD");
+    return e ? atoi(e) : 2;
+  }()};
+  return v;
+}
+static int fwdf_version() { return fwdf_impl().load(std::memory_order_relaxed); }
 template <int ACT, int KX, bool TAPE, bool TAN>
 void fwdf_launch(const float* x, const float* W, const float* b, const float* U, const float* pt, float* hs, float* tp,
                  int B, int Tn, hipStream_t s) {
+  const int nrb = (B + 31) / 32, cus = device_cu_count();
+  // (K = 35 / 36 tangent forwards: the split kernel spills there -- registers; they stay exact)
+  if constexpr (FGeo<KX>::KS <= 8 || (FGeo<KX>::KS <= 12 && !TAN)) {
+    if (fwdf_version() == 2) {
+      auto k = lstmf_fwds_kernel<ACT, KX, TAPE, TAN>;
+      allow_lds(reinterpret_cast<const void*>(k));
+      hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(256), fwds_smem<KX>(), s, x, W, b, U, pt, hs, tp, B, Tn);
+      return;
+    }
+  }
   auto k = lstmf_fwd_kernel<ACT, KX, TAPE, TAN>;
   allow_lds(reinterpret_cast<const void*>(k));
-  const int nrb = (B + 31) / 32, cus = device_cu_count();
   hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(256), fwdf_smem<KX>(), s, x, W, b, U, pt, hs, tp, B, Tn);
 }
 template <int KX, bool TAPE, bool TAN>
@@ -2232,6 +2508,8 @@ bool fwdf_k(int K, int act, const float* x, const float* W, const float* b, cons
   }
 }
 }  // namespace
+
+int set_lstmf_fwd_impl(int v) { return fwdf_impl().exchange(v); }
 
 bool lstmf_supported(int H, int K, int act) {
   return H == FH && (K == 32 || K == 35 || K == 36 || K == 100) && (act == ACT_LINEAR || act == ACT_SIGMOID || act == ACT_TANH);

@@ -942,3 +942,44 @@ def test_narrowf_dgrad(cuda, M, K, N):
     scale = max(ref.abs().max().item(), 1e-3)
     assert err <= TOL[torch.float32]["atol"] * max(1.0, scale) + TOL[torch.float32]["rtol"] * scale, (err, scale)
     assert torch.equal(dx, _ops().linear_dgrad(dz, W))
+
+
+@pytest.mark.parametrize("act", [2, 1, 0])
+@pytest.mark.parametrize("B,T,K", [(70, 24, 32), (8192 + 45, 6, 32), (64, 7, 35), (40, 5, 36)])
+def test_lstmf_split_forward_vs_exact(cuda, act, B, T, K):
+    """The split-recurrent forward (lstmf_fwds_kernel: h_{t-1} U as the exact three-term bf16 split on
+    v_mfma_f32_16x16x32_bf16 for k < 96, fp32 for the tail) vs the exact-fp32 forward and fp64: primal and
+    tangent forward within 2x the exact kernel's error (+ fp32 noise), bitwise run to run."""
+    from hfrep.ops import functional as Fn
+
+    H = 100
+    g = torch.Generator().manual_seed(57)
+    x = torch.randn(B, T, K, generator=g) * 0.5
+    W = torch.randn(K, 4 * H, generator=g) * (1.0 / K ** 0.5)
+    b = torch.randn(4 * H, generator=g) * 0.1
+    U = torch.randn(H, 4 * H, generator=g) * (1.0 / H ** 0.5)
+    xd = torch.randn(B, T, K, generator=g) * 0.3
+    xg, Wg, bg, Ug, xdg = (t_.to(cuda) for t_ in (x, W, b, U, xd))
+    zx = x.double() @ W.double() + b.double()
+    rh, rg, rc = R.lstm_seq_fwd(zx, U.double(), act)
+    th, _, _ = R.lstm_seq_tfwd(xd.double() @ W.double(), rg, rc, U.double(), act)
+    ops = _ops()
+    out, errs = {}, {}
+    prev = ops.set_lstmf_fwd_impl(1)
+    try:
+        for impl in (1, 2, 2):
+            ops.set_lstmf_fwd_impl(impl)
+            hs, tape = Fn.lstm_layer_fwd(xg, Wg, bg, Ug, act, True)
+            hs0, _ = Fn.lstm_layer_fwd(xg, Wg, bg, Ug, act, False)
+            hds, _ = Fn.lstm_layer_tfwd(xdg, Wg, tape, Ug, act)
+            if impl in out:
+                assert all(torch.equal(a_, b_) for a_, b_ in zip(out[impl], (hs, hs0, hds))), "not bitwise"
+                continue
+            out[impl] = (hs, hs0, hds)
+            errs[impl] = ((hs.double().cpu() - rh).abs().max().item(), (hs0.double().cpu() - rh).abs().max().item(),
+                          (hds.double().cpu() - th).abs().max().item())
+    finally:
+        ops.set_lstmf_fwd_impl(prev)
+    print(f"max abs err exact {errs[1]} split {errs[2]}")
+    for e1, e2 in zip(errs[1], errs[2]):
+        assert e2 <= 2 * e1 + 2e-6, (errs[1], errs[2])
