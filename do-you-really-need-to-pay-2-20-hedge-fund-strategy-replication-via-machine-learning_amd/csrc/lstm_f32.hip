@@ -1958,9 +1958,9 @@ lstmf_fwds_kernel(const float* __restrict__ x, const float* __restrict__ W, cons
   constexpr int NW = GX::KS;
   extern __shared__ __attribute__((aligned(16))) float fsm[];
   float* xb = fsm;                                                  // [2][32 * LRX] fp32, K-permuted
-  lds_char* hb = (lds_char*)(xb + 2 * 32 * GX::LR);                 // [2][FS_HB] h planes + tail
-  float* trash = reinterpret_cast<float*>(hb + 2 * FS_HB);          // [4] (x-tile loader padding)
-  lds_char* trashc = hb + 2 * FS_HB;
+  float* trash = xb + 2 * 32 * GX::LR;                              // [4] padding / out-of-range writes
+  lds_char* trashc = (lds_char*)trash;
+  lds_char* hb = (lds_char*)(trash + 4);                            // [2][FS_HB] h planes + tail
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane & 3, g = lane >> 4, j4 = (lane & 15) >> 2;

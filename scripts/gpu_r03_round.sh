@@ -15,5 +15,5 @@ if [ "$2" != "--no-suite" ]; then
 fi
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/$OUT/prof" -o run -- python "$R/bench.py" --steps 3 --warmup 1 --dtype float32 > "$R/$OUT/prof.log" 2>&1 || { tail "$R/$OUT/prof.log"; exit 1; }
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/prof" -o run -- python "$R/bench.py" --steps 3 --warmup 1 --dtype float32 > "$R/$OUT/prof.log" 2>&1 || { tail "$R/$OUT/prof.log"; exit 1; }
 cd "$R" && python scripts/prof_summary.py $(find $OUT/prof -name "*kernel_stats.csv" | head -1) 40 > $OUT/kernel_summary.txt 2>&1; head -30 $OUT/kernel_summary.txt
