@@ -276,6 +276,7 @@ std::tuple<Tensor, Tensor> lstm_tbwd(optional<Tensor> dH, Tensor dHd, Tensor gat
 bool lstmf_supported(int64_t H, int64_t K, int64_t act) { return hfrep::lstmf_supported((int)H, (int)K, (int)act); }
 bool narrowf_supported(int64_t K, int64_t N) { return hfrep::narrowf_supported((int)K, (int)N); }
 int64_t set_lstmf_fwd_impl(int64_t v) { return hfrep::set_lstmf_fwd_impl((int)v); }
+int64_t set_lstmf_bwd_impl(int64_t v) { return hfrep::set_lstmf_bwd_impl((int)v); }
 
 std::tuple<Tensor, Tensor> lstmf_fwd(Tensor x, Tensor W, optional<Tensor> b, Tensor U, int64_t act, bool save) {
   CHECK_F32(x); CHECK_F32(W);
@@ -725,6 +726,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstmf_supported(int H, int K, int act) -> bool", &lstmf_supported);  // no tensor inputs: catch-all kernel
   m.def("narrowf_supported(int K, int N) -> bool", &narrowf_supported);
   m.def("set_lstmf_fwd_impl(int v) -> int", &set_lstmf_fwd_impl);
+  m.def("set_lstmf_bwd_impl(int v) -> int", &set_lstmf_bwd_impl);
   m.def("lstmf_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
   m.def("lstmf_bwd(Tensor? dH, Tensor tape, Tensor U, int act, int B, int T) -> Tensor");
   m.def("lstmf_tbwd(Tensor? dH, Tensor? dHd, Tensor tape, Tensor ttape, Tensor U, int act, int B, int T) -> (Tensor, Tensor)");

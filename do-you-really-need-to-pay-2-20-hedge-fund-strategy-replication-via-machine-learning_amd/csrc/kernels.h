@@ -68,6 +68,7 @@ bool lstmf_dgrad_supported(int N, int KO);
 // forward kernel selection: 1 = exact-fp32 everywhere, 2 = split recurrent product for K <= 36 (default);
 // returns the previous setting
 int set_lstmf_fwd_impl(int v);
+int set_lstmf_bwd_impl(int v);  // 1 / 2: exact-fp32 BPTT kernels, else the split-recurrent one
 // impl: 0 = default (HFREP_LSTMF_DGRAD_IMPL, else the exact-fp32 MFMA kernel), 1 = exact, 2 = three-term bf16 split
 bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl = 0);
 

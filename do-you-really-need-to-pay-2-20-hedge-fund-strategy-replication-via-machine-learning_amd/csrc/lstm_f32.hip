@@ -2182,6 +2182,219 @@ lstmf_fwds_kernel(const float* __restrict__ x, const float* __restrict__ W, cons
 }
 
 // ------------------------------------------------------------------------------------------
+// BPTT with the recurrent product on the bf16 matrix pipe: lstmf_bwds_kernel
+// ------------------------------------------------------------------------------------------
+// lstmf_bwdp_kernel's step is bound by dh_rec = dz_{t+1} U^T on the exact fp32 MFMA (400 16x16x4
+// MFMAs per MFMA-role wave and step).  Here the product is the exact three-term bf16 split (dz and U^T
+// each h + m + l; six products lh hl mm mh hm hh, the dropped terms <= 2^-24 of each product) on
+// v_mfma_f32_16x16x32_bf16: 13 k-steps x 2 tiles x 6 = 156 MFMAs per half tile and wave, ~1/2.5 of the
+// fp32 pipe time.  The matrix work and the cell math are then of the same size, so the roles merge:
+// 4 waves (one per SIMD, 512 registers), wave w does the MFMAs of output tiles 2 w, 2 w + 1 AND the
+// cells of units 28 w .. 28 w + 27, one cell after each of the first 7 k-steps, so the VALU issues the
+// cell math of one row half while the matrix pipe runs the other half's product.  The row-half pipeline
+// is lstmf_bwdp_kernel's:
+//   P1(t): B(0, t) + A(1, t)      P2(t): B(1, t) + A(0, t - 1)
+// The dz tile has two images: the fp32 rows (dZ's coalesced HBM stores, as before) and three bf16
+// planes in the gate-interleaved column order k = 4 u + q (a cell writes its four gates as one 8-byte
+// word per plane), row stride 424 (conflict-free ds_read_b128).  B[k][j] = U[j][(k & 3) H + (k >> 2)],
+// k >= 400 zero: 312 registers per wave, 252 of them pinned in AGPRs.  One tape register set: a cell's
+// loads for the other half's next use are issued as soon as it has consumed the set.
+constexpr int BS_LZ = 424;             // dz plane row stride (bf16 elements)
+constexpr int BS_PL = 32 * BS_LZ * 2;  // bytes per dz plane (32 rows)
+
+template <int ACT>
+__global__ void __launch_bounds__(256, 1)
+lstmf_bwds_kernel(const float* __restrict__ dH, const float* __restrict__ tape, const float* __restrict__ U,
+                  float* __restrict__ dZ, int B, int Tn) {
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  float* zt = fsm;                                     // fp32 dz tile [32][BZ_LR]: [q][u'] per row
+  float* ht = zt + 32 * BZ_LR;                         // dh_rec tile [32][BH_LR]
+  float* trash = ht + 32 * BH_LR;                      // [4 * BZ_KQ + 4] padding words, never read
+  lds_char* trashp = (lds_char*)(trash + 4 * BZ_KQ);
+  lds_char* zp = (lds_char*)(trash + 4 * BZ_KQ + 4);   // dz planes [3][32][BS_LZ] bf16
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane & 3, g = lane >> 4, j4 = (lane & 15) >> 2, c16 = lane & 15;
+  const int nrb = (B + 31) / 32;
+  // U^T planes: B[k = 32 ks + 8 g + j][col 16 (2 w + e) + c16] = U[col][(k & 3) H + (k >> 2)]
+  bf16x8 up[2][DS_KS][3];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int col = 16 * (2 * w + e) + c16;
+    const bool ok = col < FH;
+#pragma unroll
+    for (int ks = 0; ks < DS_KS; ++ks) {
+      f32x4 v[2];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = min(32 * ks + 8 * g + j, FG - 1);
+        const float x = U[(ok ? col : 0) * FG + (k & 3) * FH + (k >> 2)];
+        v[j >> 2][j & 3] = (ok && 32 * ks + 8 * g + j < FG) ? x : 0.f;
+      }
+      uint32_t p0[3][2], p1[3][2];
+      split3(v[0], p0);
+      split3(v[1], p1);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        up[e][ks][p] = __builtin_bit_cast(bf16x8, make_uint4(p0[p][0], p0[p][1], p1[p][0], p1[p][1]));
+        if (e == 1 || ks < 8) asm volatile("" : "+a"(up[e][ks][p]));
+      }
+    }
+  }
+  const int ub = FUW * w + j4;
+  const int hr = (4 * g + q) * BH_LR + ub, zw = (4 * g + q) * BZ_LR + ub;  // (+16 m rows, + 4 n units)
+  const int zpw = ((4 * g + q) * BS_LZ + 4 * ub) * 2;                    // plane word (+ 32 n bytes)
+  const int ao = (c16 * BS_LZ + 8 * g) * 2;  // A fragment: row c16 (+ 16 M), k = 32 ks + 8 g .. + 7
+  // dZ store share: threads 0..199 own chunk tid % 100 of rows 2 k + tid / 100 (k < 16)
+  const int srr = tid / 100, sch = tid - 100 * srr, sqq = sch / 25, sc = sch - 25 * sqq;
+  const int slo = (srr & 1) * BZ_LR + sqq * BZ_KQ + 4 * sc;
+  const int sgo = tid < 200 ? (srr * Tn * FG + sqq * FH + 4 * sc) * 4 : kOOB;
+  const int tl = ftape_lane(w, lane), tcl = ftape_cell(w, lane);
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+    const int row0 = rb * 32;
+    const rsrc_t rdh = ftile_rsrc(dH, row0, B, Tn, FH), rt = ftape_rsrc(tape, rb, nrb, Tn);
+    const rsrc_t rz = ftile_rsrc(dZ, row0, B, Tn, FG);
+    const int nr = min(32, B - row0);
+    int vp1[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) vp1[m] = ((16 * m + 4 * g + q) * Tn * FH + ub) * 4;
+    float dc[2][FNT], tc[2][FNT];
+    f32x4 tg[FNT];
+    float tcp[FNT], tdh[FNT];
+    const int T1 = Tn - 1;
+#pragma unroll
+    for (int n = 0; n < FNT; ++n) {
+      const bool tok = !(w == 3 && n >= 4);
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        dc[m][n] = 0.f;
+        tc[m][n] = ld1(rt, tok ? tcl + T1 * FT_STEP * 4 + ftape_slot(m, n) : kOOB, 0);  // c_{T-1}
+      }
+      bwdf_tape_load(tg[n], tcp[n], tdh[n], rt, rdh, tl + T1 * FT_STEP * 4 + ftape_slot(0, n),
+                     tcl + (T1 - 1) * FT_STEP * 4 + ftape_slot(0, n), vp1[0] + T1 * FH * 4 + 16 * n, tok, T1 > 0);
+    }
+    // dz_T = 0 (planes, pad columns k >= 400 included), dh_rec(T - 1) = 0
+    for (int i = tid; i < 3 * BS_PL / 16; i += 256)
+      reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(zp)[i] = u32x4_t{0, 0, 0, 0};
+    for (int i = tid; i < 32 * BH_LR; i += 256) ht[i] = 0.f;
+    __syncthreads();
+    // rows of half M of the fp32 dz tile (dz at step ts) -> dZ[:, ts, :]
+    auto store_half = [&](auto M_, int ts) {
+      constexpr int M = decltype(M_)::value;
+#pragma unroll
+      for (int k = 8 * M; k < 8 * M + 8; ++k) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(zt + slo + 2 * k * BZ_LR);
+        st16(v, rz, 2 * k + srr < nr, sgo, (2 * k * Tn + ts) * FG * 4);
+      }
+    };
+    // cell adjoint of (row half M, unit tile n) at step t, then the loads for the set's next use
+    auto cell = [&](auto M_, int n, float hrec, int t) {
+      constexpr int m = decltype(M_)::value;
+      const bool tok = !(w == 3 && n >= 4);
+      const float ig = tg[n][0], fg = tg[n][1], gg = tg[n][2], og = tg[n][3];
+      const float dht = tdh[n] + hrec;
+      const float ca = act_f(ACT, tc[m][n]);
+      const float dov = dht * ca;
+      const float dct = dc[m][n] + dht * og * act_dy(ACT, ca);
+      dc[m][n] = tok ? dct * fg : 0.f;
+      f32x4 z4;
+      z4[0] = dct * gg * ig * (1.f - ig);
+      z4[1] = dct * tcp[n] * fg * (1.f - fg);
+      z4[2] = dct * ig * act_dy(ACT, gg);
+      z4[3] = dov * og * (1.f - og);
+      float* zd = tok ? zt + zw + 16 * m * BZ_LR + 4 * n : trash;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) zd[k * BZ_KQ] = z4[k];
+      uint32_t p[3][2];
+      split3(z4, p);
+      lds_char* pd = tok ? zp + zpw + 16 * m * BS_LZ * 2 + 32 * n : trashp;
+      const int ps = tok ? BS_PL : 0;
+#pragma unroll
+      for (int pp = 0; pp < 3; ++pp)
+        *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(pd + pp * ps) = u32x2_t{p[pp][0], p[pp][1]};
+      tc[m][n] = tcp[n];  // c_{t-1} is the next step's c
+      if constexpr (m == 0) {  // next use: B(1, t)
+        bwdf_tape_load(tg[n], tcp[n], tdh[n], rt, rdh, tl + t * FT_STEP * 4 + ftape_slot(1, n),
+                       tcl + (t - 1) * FT_STEP * 4 + ftape_slot(1, n), vp1[1] + t * FH * 4 + 16 * n, tok, t > 0);
+      } else {  // next use: B(0, t - 1)
+        const int tp = t > 0 ? t - 1 : 0;
+        bwdf_tape_load(tg[n], tcp[n], tdh[n], rt, rdh, tl + tp * FT_STEP * 4 + ftape_slot(0, n),
+                       tcl + (tp - 1) * FT_STEP * 4 + ftape_slot(0, n), vp1[0] + tp * FH * 4 + 16 * n, tok && t > 0,
+                       tp > 0);
+      }
+    };
+    // one half-phase: dz rows of half MA out to HBM, the cells of half 1 - MA at step t, and rows MA of
+    // dh_rec = dz[rows MA] U^T (the planes hold dz_{t + 1} there for MA = 1, dz_t for MA = 0)
+    auto phase = [&](auto MA_, int t) {
+      constexpr int MA = decltype(MA_)::value;
+      if constexpr (MA == 1) {
+        if (t < T1) store_half(I1{}, t + 1);
+      } else {
+        store_half(I0{}, t);
+      }
+      float hv[FNT];  // the cells' dh_rec words (rows of half 1 - MA, completed in the previous phase)
+#pragma unroll
+      for (int n = 0; n < FNT; ++n) hv[n] = ht[hr + 16 * (1 - MA) * BH_LR + 4 * n];
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      const lds_char* ar = zp + ao + 16 * MA * BS_LZ * 2;
+      bf16x8 af[2][3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) af[0][p] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(ar + p * BS_PL);
+#pragma unroll
+      for (int ks = 0; ks < DS_KS; ++ks) {
+        if (ks + 1 < DS_KS) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            af[(ks + 1) & 1][p] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(ar + p * BS_PL + 64 * (ks + 1));
+        }
+        const bf16x8(&a)[3] = af[ks & 1];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          acc[e] = mma32(a[2], up[e][ks][0], acc[e]);  // lh
+          acc[e] = mma32(a[0], up[e][ks][2], acc[e]);  // hl
+          acc[e] = mma32(a[1], up[e][ks][1], acc[e]);  // mm
+          acc[e] = mma32(a[1], up[e][ks][0], acc[e]);  // mh
+          acc[e] = mma32(a[0], up[e][ks][1], acc[e]);  // hm
+          acc[e] = mma32(a[0], up[e][ks][0], acc[e]);  // hh
+        }
+        if (ks < FNT) cell(std::integral_constant<int, 1 - MA>{}, ks, hv[ks], t);  // (compile-time)
+      }
+      // one schedule for the whole phase: per k-step its A fragments, then its 12 MFMAs with 3 VALU
+      // slots (the cells' math) after each one; loads and LDS stores of the cells go where they fit
+#pragma unroll
+      for (int ks = 0; ks < DS_KS; ++ks) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // rows 16 MA + 4 g + i, column 16 (2 w + e) + c16 (wave 3's second tile is past the 112 units: trash)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const bool ok = 2 * w + e < 7;
+        float* hd = ok ? ht + (16 * MA + 4 * g) * BH_LR + 16 * (2 * w + e) + c16 : trash;
+        const int hs = ok ? BH_LR : 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hd[i * hs] = acc[e][i];
+      }
+      lds_barrier();
+    };
+    for (int t = T1; t >= 0; --t) {
+      phase(I1{}, t);  // P1(t): B(0, t) + A(1, t)
+      phase(I0{}, t);  // P2(t): B(1, t) + A(0, t - 1)
+    }
+    store_half(I1{}, 0);
+    __syncthreads();  // (the tiles are re-zeroed for the next row block)
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // fp32 input gradient on the bf16 matrix pipe, LDS-staged: lstmf_dgrad_s4_kernel
 // ------------------------------------------------------------------------------------------
 // dX = dZ W^T with the exact three-term split (six products, dropped terms <= 2^-24 of each product).
@@ -2528,19 +2741,32 @@ bool launch_lstmf_tfwd(const float* xd, const float* W, const float* U, const fl
   return fwdf_k<true, true>(K, act, xd, W, nullptr, U, tape, hds, ttape, B, Tn, s);
 }
 
+// HFREP_LSTMF_BWD=1: the unpipelined two-phase kernel; 2: the exact-fp32 role split (A / B
+// comparisons); default 3: the split-recurrent BPTT (lstmf_bwds_kernel)
+static std::atomic<int>& bwdf_impl() {
+  static std::atomic<int> v{[] {
+    const char* e = getenv("HFREP_LSTMF_BWD");
+    return e ? atoi(e) : 3;
+  }()};
+  return v;
+}
 template <int ACT>
 void bwdf_launch(const float* dH, const float* tape, const float* U, float* dZ, int B, int Tn, hipStream_t s) {
-  // HFREP_LSTMF_BWD=1: the unpipelined two-phase kernel (A / B comparison); default: row-half pipelined
-  static const int ver = [] {
-    const char* e = getenv("HFREP_LSTMF_BWD");
-    return e ? atoi(e) : 2;
-  }();
-  auto k = ver == 1 ? lstmf_bwd_kernel<ACT> : lstmf_bwdp_kernel<ACT>;
-  allow_lds(reinterpret_cast<const void*>(k));
+  const int ver = bwdf_impl().load(std::memory_order_relaxed);
   const int nrb = (B + 31) / 32, cus = device_cu_count();
   const size_t sm = (size_t)(32 * BZ_LR + 32 * BH_LR + 4 * BZ_KQ) * 4;
+  if (ver != 1 && ver != 2) {
+    auto k = lstmf_bwds_kernel<ACT>;
+    allow_lds(reinterpret_cast<const void*>(k));
+    hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(256), sm + 16 + 3 * BS_PL, s, dH, tape, U, dZ, B, Tn);
+    return;
+  }
+  auto k = ver == 1 ? lstmf_bwd_kernel<ACT> : lstmf_bwdp_kernel<ACT>;
+  allow_lds(reinterpret_cast<const void*>(k));
   hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(ver == 1 ? 256 : 512), sm, s, dH, tape, U, dZ, B, Tn);
 }
+static_assert((32 * BZ_LR + 32 * BH_LR + 4 * BZ_KQ) * 4 + 16 + 3 * BS_PL <= F_LDS_MAX, "split BPTT LDS");
+int set_lstmf_bwd_impl(int v) { return bwdf_impl().exchange(v); }
 bool launch_lstmf_bwd(const float* dH, const float* tape, const float* U, float* dZ, int B, int Tn, int H, int act,
                       hipStream_t s) {
   if (H != FH || B <= 0 || Tn <= 0) return false;

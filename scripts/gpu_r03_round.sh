@@ -5,7 +5,7 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"
 OUT=gpurun_out/${1:-r03_round}; mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "lstmf_wgrad or lstmf_dgrad or narrowf" -q --timeout 200 \
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "lstmf_wgrad or lstmf_dgrad or narrowf or split_bptt or split_forward" -q --timeout 200 \
   --timeout-method thread > $OUT/tests_split.txt 2>&1 || { tail -n 30 $OUT/tests_split.txt; exit 1; }
 tail -n 2 $OUT/tests_split.txt
 if [ "$2" != "--no-suite" ]; then

@@ -983,3 +983,45 @@ def test_lstmf_split_forward_vs_exact(cuda, act, B, T, K):
     print(f"max abs err exact {errs[1]} split {errs[2]}")
     for e1, e2 in zip(errs[1], errs[2]):
         assert e2 <= 2 * e1 + 2e-6, (errs[1], errs[2])
+
+
+@pytest.mark.parametrize("act", [2, 1, 0])
+@pytest.mark.parametrize("B,T", [(70, 24), (8192 + 45, 6), (33, 1), (40, 5)])
+def test_lstmf_split_bptt_vs_exact(cuda, act, B, T):
+    """The split-recurrent BPTT (lstmf_bwds_kernel: dz_{t+1} U^T as the exact three-term bf16 split on
+    v_mfma_f32_16x16x32_bf16) vs the exact-fp32 role-split BPTT (lstmf_bwdp_kernel) and fp64: dZ (and the
+    fused dX) within 2x the exact kernel's error (+ fp32 noise), bitwise run to run; the tape comes from
+    the exact forward so both kernels see the same input."""
+    from hfrep.ops import functional as Fn
+
+    H, K = 100, 32
+    g = torch.Generator().manual_seed(61)
+    x = torch.randn(B, T, K, generator=g) * 0.5
+    W = torch.randn(K, 4 * H, generator=g) * (1.0 / K ** 0.5)
+    b = torch.randn(4 * H, generator=g) * 0.1
+    U = torch.randn(H, 4 * H, generator=g) * (1.0 / H ** 0.5)
+    dH = torch.randn(B, T, H, generator=g)
+    xg, Wg, bg, Ug, dHg = (t_.to(cuda) for t_ in (x, W, b, U, dH))
+    zx = x.double() @ W.double() + b.double()
+    _, rg, rc = R.lstm_seq_fwd(zx, U.double(), act)
+    rdz = R.lstm_seq_bwd(dH.double(), rg, rc, U.double(), act)
+    ops = _ops()
+    pf = ops.set_lstmf_fwd_impl(1)
+    pb = ops.set_lstmf_bwd_impl(2)
+    out, errs = {}, {}
+    try:
+        _, tape = Fn.lstm_layer_fwd(xg, Wg, bg, Ug, act, True)
+        for impl in (2, 3, 3):
+            ops.set_lstmf_bwd_impl(impl)
+            dZ = Fn.lstm_layer_bwd(dHg, tape, Ug, act)
+            if impl in out:
+                assert torch.equal(out[impl], dZ), "not bitwise"
+                continue
+            out[impl] = dZ
+            errs[impl] = (dZ.double().cpu() - rdz).abs().max().item()
+    finally:
+        ops.set_lstmf_fwd_impl(pf)
+        ops.set_lstmf_bwd_impl(pb)
+    print(f"max abs err exact {errs[2]:.3e} split {errs[3]:.3e}")
+    assert torch.isfinite(out[3]).all()
+    assert errs[3] <= 2 * errs[2] + 2e-6, errs
