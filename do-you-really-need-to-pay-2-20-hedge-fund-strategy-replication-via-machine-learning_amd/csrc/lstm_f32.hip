@@ -1296,11 +1296,27 @@ lstmf_wgrad_kernel(const float* __restrict__ X, const float* __restrict__ Hs, co
 // MFMA counts); its B fragments (all three planes of its <= 3 j-tiles) stay in registers for the
 // chunk, the A fragments stream: every operand is read from LDS once per wave.  (A three-part
 // column split was measured slower: profiles/r02_split.)
-constexpr int WS_CA = 208, WS_CD = 208;                   // image columns (A, D part)
-constexpr int WS_ROWA = WS_CA * 2, WS_ROWD = WS_CD * 2;   // bytes per image row
-constexpr int WS_PLA = 32 * WS_ROWA, WS_PLD = 32 * WS_ROWD;  // bytes per plane
-constexpr int WS_IMGD = 3 * WS_PLA;                       // D image offset in a buffer
-constexpr int WS_BUF = 3 * WS_PLA + 3 * WS_PLD;           // one buffer: A + D images (79,872 B)
+constexpr int WS_CA = 208, WS_CD = 208;                   // max image columns (A, D part)
+// Row stride of a plane image with `cols` bf16 columns: S dwords with S % 64 == 8 (cf), else packed.
+// One ds_read_b64_tr_b16 lane group (32 lanes) reads 8 consecutive chunk rows (tr_frag's row order) x 8
+// dwords; at S % 64 == 8 those are the 64 banks once each.  The r02 stride (416 B = 104 dwords) put
+// rows r and r + 8 of the old row order on the same banks: 2-way on every operand read
+// (SQ_LDS_BANK_CONFLICT ~ 24 % of the q4 kernel's cycles, profiles/r03_split/pmc_summary_v1.txt).
+constexpr int ws_row_bytes(int cols, bool cf) {
+  const int dw = (cols + 1) / 2;
+  return 4 * (cf ? dw + ((8 - dw % 64) + 64) % 64 : (dw + 3) / 4 * 4);
+}
+// one double-buffered LDS stage: A image (CA columns) + D image (CD columns), three planes each; the
+// conflict-free strides where both buffers fit the 160 KiB
+template <int CA, int CD>
+struct WImg {
+  static constexpr bool CF = 2 * 3 * 32 * (ws_row_bytes(CA, true) + ws_row_bytes(CD, true)) <= 160 * 1024;
+  static constexpr int ROWA = ws_row_bytes(CA, CF), ROWD = ws_row_bytes(CD, CF);  // bytes per image row
+  static constexpr int PLA = 32 * ROWA, PLD = 32 * ROWD;                           // bytes per plane
+  static constexpr int IMGD = 3 * PLA;                                             // D image offset
+  static constexpr int BUF = 3 * PLA + 3 * PLD;                                    // one buffer
+  static_assert(2 * BUF <= 160 * 1024, "wgrad split LDS");
+};
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((address_space(3))) char lds_char;
@@ -1315,6 +1331,7 @@ struct WSGeo {
   static constexpr int JX = (32 * KX / 4 + 511) / 512, JH = (32 * FH / 4 + 511) / 512;  // float4 slots per thread
   static constexpr int JD = (32 * 52 + 511) / 512;  // D slots: 52 float4 per row (the second part uses 48)
   static_assert(KX % 4 == 0 && 16 * NI <= WS_CA, "wgrad split: K");
+  using Img = WImg<16 * NI, WS_CD>;
 };
 
 // three bf16 planes of four fp32 values, packed two per dword
@@ -1341,12 +1358,17 @@ __device__ __forceinline__ void split3(const f32x4 v, uint32_t (&p)[3][2]) {
 }
 
 // one 16x16x32 operand (8 bf16) of a plane image (row stride ROWB) at column block c0: two
-// transposed reads (rows 8 G + q and 8 G + 4 + q of this lane's group G); lane_off = the lane's
-// (8 G + q) ROWB + 8 p
+// transposed reads, chunk rows 4 G + q and 16 + 4 G + q of this lane's group G (k = 8 G + j of the
+// MFMA maps to chunk row 4 G + j (j < 4) / 16 + 4 G + j - 4: any row order works as long as both
+// operands use it; this one keeps a 32-lane read group on 8 consecutive rows); lane_off = the
+// lane's (4 G + q) ROWB + 8 p (tr_lane_off)
+__device__ __forceinline__ int tr_lane_off(int lane, int rowb) {
+  return (4 * (lane >> 4) + ((lane & 15) >> 2)) * rowb + 8 * (lane & 3);
+}
 template <int ROWB>
 __device__ __forceinline__ bf16x8 tr_frag(const lds_char* img, int lane_off, int c0) {
   const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + lane_off + c0 * 2));
-  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + lane_off + 4 * ROWB + c0 * 2));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + lane_off + 16 * ROWB + c0 * 2));
   return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 __device__ __forceinline__ f32x4 mma32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
@@ -1360,20 +1382,20 @@ __device__ __forceinline__ f32x4 mma32(const bf16x8& a, const bf16x8& b, const f
 // kernel, consistent with a biased rounding of the MFMA's C addition).  Straight-line code (one
 // instantiation per wave shape): with a wave-uniform branch between an MFMA and the VALU read of its
 // result the compiler did not count the wait states across the branch (2 instead of >= 7).
-template <int NIV, int NJV, int NA, int NB>
+template <class GI, int NIV, int NJV, int NA, int NB>
 __device__ __forceinline__ void ws_chunk(f32x4 (&acc)[NA][NB], const lds_char* A_, const lds_char* D_, int tro_a,
                                          int tro_d, int i0, int j0) {
   bf16x8 bfr[NJV][3];
 #pragma unroll
   for (int jj = 0; jj < NJV; ++jj)
 #pragma unroll
-    for (int q = 0; q < 3; ++q) bfr[jj][q] = tr_frag<WS_ROWD>(D_ + q * WS_PLD, tro_d, 16 * (j0 + jj));
+    for (int q = 0; q < 3; ++q) bfr[jj][q] = tr_frag<GI::ROWD>(D_ + q * GI::PLD, tro_d, 16 * (j0 + jj));
 #pragma unroll
   for (int ii = 0; ii < NIV; ++ii) {
     __builtin_amdgcn_sched_barrier(0);
     bf16x8 a3[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) a3[q] = tr_frag<WS_ROWA>(A_ + q * WS_PLA, tro_a, 16 * (i0 + ii));
+    for (int q = 0; q < 3; ++q) a3[q] = tr_frag<GI::ROWA>(A_ + q * GI::PLA, tro_a, 16 * (i0 + ii));
     // j-tiles in pairs: two fresh accumulators in flight, added after both chains
 #pragma unroll
     for (int j2 = 0; j2 < NJV; j2 += 2) {
@@ -1400,6 +1422,7 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
                          const float* __restrict__ Xd, const float* __restrict__ Hds, const float* __restrict__ Dd,
                          float* __restrict__ slab, int M, int Tn, int rows_per_z, int Z) {
   using G = WSGeo<KX>;
+  using GI = typename G::Img;
   constexpr int NI = G::NI, NI0 = G::NI0, JX = G::JX, JH = G::JH, JD = G::JD;
   extern __shared__ __attribute__((aligned(16))) char wsm_[];
   lds_char* wsm = (lds_char*)wsm_;
@@ -1424,7 +1447,7 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
   const int j0 = jg == 0 ? 0 : 1 + 3 * jg, nj = jg == 0 ? 4 : 3;
 
   // zero both buffers (pad columns, zero j-tiles of the last part)
-  for (int i = tid; i < 2 * WS_BUF / 16; i += 512) reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(wsm)[i] = u32x4_t{0, 0, 0, 0};
+  for (int i = tid; i < 2 * GI::BUF / 16; i += 512) reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(wsm)[i] = u32x4_t{0, 0, 0, 0};
   __syncthreads();
 
   f32x4 acc[NI0][4];
@@ -1433,9 +1456,11 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // this lane's transposed-read bases: row 8 G + q, column 4 p (bytes)
-  const int trr = 8 * (lane >> 4) + ((lane & 15) >> 2);
-  const int tro_a = trr * WS_ROWA + 8 * (lane & 3), tro_d = trr * WS_ROWD + 8 * (lane & 3);
+  // this lane's transposed-read bases (the D image offset rides in the base VGPR, opaque to the
+  // compiler: folded into the reads' immediates it overflowed their 16 bits and cost a register per read)
+  const int tro_a = tr_lane_off(lane, GI::ROWA);
+  int tro_d = tr_lane_off(lane, GI::ROWD) + GI::IMGD;
+  asm volatile("" : "+v"(tro_d));
 
   // per-thread float4 slots of a 32-row chunk: X (JX), H (JH), D (JD); element e = tid + 512 j:
   // byte offset in the chunk frame (kOOB: none), LDS byte offset (-1: none), H-slot row
@@ -1445,14 +1470,14 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
     const int e = tid + 512 * j, r = e / (KX / 4), c4 = e - r * (KX / 4);
     const bool ok = e < 32 * KX / 4;
     gx[j] = ok ? (r * KX + 4 * c4) * 4 : kOOB;
-    lx[j] = ok ? r * WS_ROWA + 8 * c4 : -1;
+    lx[j] = ok ? r * GI::ROWA + 8 * c4 : -1;
   }
 #pragma unroll
   for (int j = 0; j < JH; ++j) {
     const int e = tid + 512 * j, r = e / (FH / 4), c4 = e - r * (FH / 4);
     const bool ok = e < 32 * FH / 4;
     gh[j] = ok ? (r * FH + 4 * c4) * 4 : kOOB;
-    lh[j] = ok ? r * WS_ROWA + 2 * KX + 8 * c4 : -1;
+    lh[j] = ok ? r * GI::ROWA + 2 * KX + 8 * c4 : -1;
     rhr[j] = ok ? r : 0;
   }
 #pragma unroll
@@ -1460,7 +1485,7 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
     const int e = tid + 512 * j, r = e / 52, c4 = e - r * 52;
     const bool ok = e < 32 * 52 && c4 < nd4;
     gd[j] = ok ? (r * FG + jbase + 4 * c4) * 4 : kOOB;
-    ld_[j] = ok ? WS_IMGD + r * WS_ROWD + 8 * c4 : -1;
+    ld_[j] = ok ? GI::IMGD + r * GI::ROWD + 8 * c4 : -1;
     rd_[j] = ok ? r : 0;
   }
   const int step32 = 32 % Tn;
@@ -1499,14 +1524,14 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
       if (lo >= 0) {
         uint32_t p[3][2];
         split3(v, p);
-        const int pl = lo < WS_IMGD ? WS_PLA : WS_PLD;
+        const int pl = lo < GI::IMGD ? GI::PLA : GI::PLD;
 #pragma unroll
         for (int q = 0; q < 3; ++q)
           *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(base + lo + q * pl) = u32x2_t{p[q][0], p[q][1]};
       }
     };
     auto stage = [&](int buf) {
-      lds_char* base = wsm + buf * WS_BUF;
+      lds_char* base = wsm + buf * GI::BUF;
 #pragma unroll
       for (int j = 0; j < JX; ++j) put(base, lx[j], vx[j]);
 #pragma unroll
@@ -1517,7 +1542,7 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
     // bias column (column KR - 1 of A): 1 in plane h for the primal segment, 0 for the tangent one
     if (tid < 64) {
       const int buf = tid >> 5, r = tid & 31;
-      *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wsm + buf * WS_BUF + r * WS_ROWA + (G::KR - 1) * 2) =
+      *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wsm + buf * GI::BUF + r * GI::ROWA + (G::KR - 1) * 2) =
           seg ? 0 : 0x3f80;
     }
     const int nch = nr > 0 ? (nr + 31) / 32 : 0;
@@ -1529,13 +1554,13 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
     for (int c = 0; c < nch; ++c) {
       const bool more = c + 1 < nch;
       if (more) load(mb + 32 * (c + 1));
-      const lds_char* A_ = wsm + (c & 1) * WS_BUF;
-      const lds_char* D_ = A_ + WS_IMGD;
+      const lds_char* A_ = wsm + (c & 1) * GI::BUF;
+      const lds_char* D_ = A_;  // (+ IMGD in tro_d)
       switch (ni * 8 + nj) {
-        case NI0 * 8 + 4: ws_chunk<NI0, 4>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
-        case NI0 * 8 + 3: ws_chunk<NI0, 3>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
-        case (NI - NI0) * 8 + 4: ws_chunk<NI - NI0, 4>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
-        default: ws_chunk<NI - NI0, 3>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
+        case NI0 * 8 + 4: ws_chunk<GI, NI0, 4>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
+        case NI0 * 8 + 3: ws_chunk<GI, NI0, 3>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
+        case (NI - NI0) * 8 + 4: ws_chunk<GI, NI - NI0, 4>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
+        default: ws_chunk<GI, NI - NI0, 3>(acc, A_, D_, tro_a, tro_d, i0, j0); break;
       }
       if (more) stage((c + 1) & 1);
       __syncthreads();
@@ -1568,7 +1593,7 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
 // exact).  Here FOUR workgroups share a row range and split the 400 gate columns in quarters of 100
 // (7 j-tiles, the last one 4 / 16 real); the quad sits on one XCD (blocks b, b + 8, b + 16, b + 24),
 // so the A rows [x | h_{t-1} | 1] that all four stage come from the same L2.  8 waves (2 per SIMD):
-// the NI x 7 output tiles are dealt out in j-major order (11-12 per wave at K = 100), so a wave keeps
+// the NI x 7 output tiles are dealt out as i-groups x j-groups (<= 4 x 4 per wave), so a wave keeps
 // its accumulators and <= 2 j-tiles' D fragments in registers and streams the A fragments.
 // Prefetch distance two chunks: chunk c + 2's fp32 rows are loaded at the top of chunk c (two
 // register sets alternate), and chunk c + 1's rows are split and stored into the other LDS buffer in
@@ -1594,6 +1619,7 @@ struct WQGeo {
   static constexpr int ni(int g) { return i0(g + 1 > 3 ? 3 : g + 1) - i0(g) + (g == 3 ? NI - i0(3) : 0); }
   static constexpr int j0(int w) { return w < 4 ? 0 : 4; }
   static constexpr int nj(int w) { return w < 4 ? 4 : 3; }
+  using Img = WImg<16 * NI, 16 * WQ_NJ>;
 };
 
 template <int KX>
@@ -1602,6 +1628,7 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
                       const float* __restrict__ Xd, const float* __restrict__ Hds, const float* __restrict__ Dd,
                       float* __restrict__ slab, int M, int Tn, int rows_per_z, int Z) {
   using G = WQGeo<KX>;
+  using GI = typename G::Img;
   constexpr int JX = G::JX, JH = G::JH, NS = G::NS, MAXT = G::MAXT;
   extern __shared__ __attribute__((aligned(16))) char wsm_[];
   lds_char* wsm = (lds_char*)wsm_;
@@ -1620,15 +1647,22 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
   const int mb = z * rows_per_z, me = min(M, mb + rows_per_z);
   const int jbase = WQ_CD * jq;
 
-  for (int i = tid; i < 2 * WS_BUF / 16; i += 512) reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(wsm)[i] = u32x4_t{0, 0, 0, 0};
+  for (int i = tid; i < 2 * GI::BUF / 16; i += 512) reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(wsm)[i] = u32x4_t{0, 0, 0, 0};
   __syncthreads();
 
   f32x4 acc[MAXT];
 #pragma unroll
   for (int a = 0; a < MAXT; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int trr = 8 * (lane >> 4) + ((lane & 15) >> 2);
-  const int tro_a = trr * WS_ROWA + 8 * (lane & 3), tro_d = trr * WS_ROWD + 8 * (lane & 3);
+  // per-buffer lane bases of the transposed reads (A image, D image), opaque to the compiler: with the
+  // buffer and image offsets folded into the reads' immediates they overflowed the 16-bit field
+  int tro_a[2], tro_d[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    tro_a[b] = tr_lane_off(lane, GI::ROWA) + b * GI::BUF;
+    tro_d[b] = tr_lane_off(lane, GI::ROWD) + b * GI::BUF + GI::IMGD;
+    asm volatile("" : "+v"(tro_a[b]), "+v"(tro_d[b]));
+  }
   const int step32 = 32 % Tn;
 
   // staging slot s of this thread: kind (x / h / d) is compile-time in s
@@ -1646,7 +1680,7 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
     if (!ok) r = c4 = 0;
   };
 
-  f32x4 v[2][NS];
+  f32x4 v[NS];
   for (int seg = 0; seg < (Xd ? 2 : 1); ++seg) {
     const float* Xs = seg ? Xd : X;
     const float* Hq = seg ? Hds : Hs;
@@ -1664,42 +1698,35 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
       slot_rc(JX + j, r, c4, ok);
       tm[j] = (mb + r) % Tn;
     }
-    // chunk loads into register set S (rows past me -- or past the range -- read zeros)
-    auto load = [&](auto S_, int m0) {
-      constexpr int S = decltype(S_)::value;
-      const int lim = me - m0;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        int r, c4;
-        bool ok;
-        slot_rc(s, r, c4, ok);
-        ok = ok && r < lim;
-        if (s < JX) {
-          v[S][s] = ld4s(rx, ok ? (r * KX + 4 * c4) * 4 : kOOB, (m0 - mb) * KX * 4);
-        } else if (s < JX + JH) {
-          v[S][s] = ld4s(rh, ok && tm[s - JX] != 0 ? (r * FH + 4 * c4) * 4 : kOOB, (m0 - mb) * FH * 4);
-        } else {
-          v[S][s] = ld4s(rd, ok ? (r * FG + 4 * c4) * 4 : kOOB, (m0 - mb) * FG * 4);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < JH; ++j) {
-        tm[j] += step32;
-        if (tm[j] >= Tn) tm[j] -= Tn;
+    // slot s of the chunk at row m0 into the register set (rows past me -- or past the range -- read
+    // zeros); an H slot's (row mod Tn) then advances to its next chunk
+    auto load_slot = [&](int s, int m0) {
+      int r, c4;
+      bool ok;
+      slot_rc(s, r, c4, ok);
+      ok = ok && r < me - m0;
+      if (s < JX) {
+        v[s] = ld4s(rx, ok ? (r * KX + 4 * c4) * 4 : kOOB, (m0 - mb) * KX * 4);
+      } else if (s < JX + JH) {
+        int& tmj = tm[s - JX];
+        v[s] = ld4s(rh, ok && tmj != 0 ? (r * FH + 4 * c4) * 4 : kOOB, (m0 - mb) * FH * 4);
+        tmj += step32;
+        if (tmj >= Tn) tmj -= Tn;
+      } else {
+        v[s] = ld4s(rd, ok ? (r * FG + 4 * c4) * 4 : kOOB, (m0 - mb) * FG * 4);
       }
     };
-    auto stage = [&](auto S_, lds_char* base, int s) {
-      constexpr int S = decltype(S_)::value;
+    auto stage = [&](lds_char* base, int s) {
       int r, c4;
       bool ok;
       slot_rc(s, r, c4, ok);
       if (!ok) return;
       uint32_t p[3][2];
-      split3(v[S][s], p);
+      split3(v[s], p);
       int lo, pl;
-      if (s < JX) { lo = r * WS_ROWA + 8 * c4; pl = WS_PLA; }
-      else if (s < JX + JH) { lo = r * WS_ROWA + 2 * KX + 8 * c4; pl = WS_PLA; }
-      else { lo = WS_IMGD + r * WS_ROWD + 8 * c4; pl = WS_PLD; }
+      if (s < JX) { lo = r * GI::ROWA + 8 * c4; pl = GI::PLA; }
+      else if (s < JX + JH) { lo = r * GI::ROWA + 2 * KX + 8 * c4; pl = GI::PLA; }
+      else { lo = GI::IMGD + r * GI::ROWD + 8 * c4; pl = GI::PLD; }
 #pragma unroll
       for (int q = 0; q < 3; ++q)
         *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(base + lo + q * pl) = u32x2_t{p[q][0], p[q][1]};
@@ -1708,24 +1735,26 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
     using I1 = std::integral_constant<int, 1>;
     if (tid < 64) {  // bias column KR - 1: 1 in plane h for the primal segment, 0 for the tangent one
       const int buf = tid >> 5, r = tid & 31;
-      *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wsm + buf * WS_BUF + r * WS_ROWA + (G::KR - 1) * 2) =
+      *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wsm + buf * GI::BUF + r * GI::ROWA + (G::KR - 1) * 2) =
           seg ? 0 : 0x3f80;
     }
     const int nch = nr > 0 ? (nr + 31) / 32 : 0;
-    // prologue: chunk 0 staged into buffer 0, chunk 1 in flight in set 1
-    load(I0{}, mb);
+    // prologue: chunk 0 staged into buffer 0, chunk 1 in flight in the register set
 #pragma unroll
-    for (int s = 0; s < NS; ++s) stage(I0{}, wsm, s);
-    load(I1{}, mb + 32);
+    for (int s = 0; s < NS; ++s) load_slot(s, mb);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) stage(wsm, s);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) load_slot(s, mb + 32);
     __syncthreads();
-    // chunk c (S = c & 1): loads of chunk c + 2 into set S, MFMAs on buffer S, chunk c + 1 (set S ^ 1)
-    // split into buffer S ^ 1 in slices between the i-tiles
+    // chunk c (S = c & 1): MFMAs on buffer S; between the i-tiles the set's slots (chunk c + 1) are
+    // split into buffer S ^ 1, each slot reloaded with chunk c + 2 right after (one register set:
+    // a slot's HBM latency hides under one chunk of MFMAs)
     auto chunk = [&](auto S_, int c) {
       constexpr int S = decltype(S_)::value;
-      load(S_, mb + 32 * (c + 2));
-      const lds_char* A_ = wsm + S * WS_BUF;
-      const lds_char* D_ = A_ + WS_IMGD;
-      lds_char* nxt = wsm + (S ^ 1) * WS_BUF;
+      const lds_char* A_ = wsm;  // (+ S BUF in tro_a[S], + S BUF + IMGD in tro_d[S])
+      const lds_char* D_ = wsm;
+      lds_char* nxt = wsm + (S ^ 1) * GI::BUF;
       // one straight-line body per wave (no branch between an MFMA and the VALU read of its
       // result); wave W owns tiles [TS, TE) of the j-major list (tile L = j NI + i).  The staging
       // slices are unconditional: after the last chunk they store the (zero) rows past the range
@@ -1742,23 +1771,23 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
           for (int jj = 0; jj < 2; ++jj)
             if (2 * jh + jj < NJW) {
 #pragma unroll
-              for (int q = 0; q < 3; ++q) bfr[jj][q] = tr_frag<WS_ROWD>(D_ + q * WS_PLD, tro_d, 16 * (J0 + 2 * jh + jj));
+              for (int q = 0; q < 3; ++q) bfr[jj][q] = tr_frag<GI::ROWD>(D_ + q * GI::PLD, tro_d[S], 16 * (J0 + 2 * jh + jj));
             }
           // A fragments one i-tile ahead (two sets) where the registers allow (K <= 36): the LDS
           // latency hides under the MFMAs
           constexpr bool PF = KX <= 36;
           bf16x8 af[2][3];
 #pragma unroll
-          for (int q = 0; q < 3; ++q) af[0][q] = tr_frag<WS_ROWA>(A_ + q * WS_PLA, tro_a, 16 * I0);
+          for (int q = 0; q < 3; ++q) af[0][q] = tr_frag<GI::ROWA>(A_ + q * GI::PLA, tro_a[S], 16 * I0);
 #pragma unroll
           for (int ii = 0; ii < NIW; ++ii) {
             __builtin_amdgcn_sched_barrier(0);
             if (PF && ii + 1 < NIW) {
 #pragma unroll
-              for (int q = 0; q < 3; ++q) af[(ii + 1) & 1][q] = tr_frag<WS_ROWA>(A_ + q * WS_PLA, tro_a, 16 * (I0 + ii + 1));
+              for (int q = 0; q < 3; ++q) af[(ii + 1) & 1][q] = tr_frag<GI::ROWA>(A_ + q * GI::PLA, tro_a[S], 16 * (I0 + ii + 1));
             } else if (!PF && ii > 0) {
 #pragma unroll
-              for (int q = 0; q < 3; ++q) af[ii & 1][q] = tr_frag<WS_ROWA>(A_ + q * WS_PLA, tro_a, 16 * (I0 + ii));
+              for (int q = 0; q < 3; ++q) af[ii & 1][q] = tr_frag<GI::ROWA>(A_ + q * GI::PLA, tro_a[S], 16 * (I0 + ii));
             }
             const bf16x8(&a3)[3] = af[ii & 1];
 #pragma unroll
@@ -1774,7 +1803,10 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
             }
             const int it = jh * NIW + ii;
 #pragma unroll
-            for (int s = it * SPI; s < (it + 1) * SPI && s < NS; ++s) stage(std::integral_constant<int, S ^ 1>{}, nxt, s);
+            for (int s = it * SPI; s < (it + 1) * SPI && s < NS; ++s) {
+              stage(nxt, s);
+              load_slot(s, mb + 32 * (c + 2));
+            }
           }
         };
         jpair(std::integral_constant<int, 0>{});
@@ -2856,15 +2888,14 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
     const int z0 = wgradq_z(M);
     const int rpz = ((M + z0 - 1) / z0 + 31) / 32 * 32;
     const int z = (M + rpz - 1) / rpz;
-    const size_t sm = 2 * WS_BUF;
-    auto go = [&](auto k) {
+    auto go = [&](auto k, size_t sm) {
       allow_lds(reinterpret_cast<const void*>(k));
       hipLaunchKernelGGL(k, dim3(4 * z), dim3(512), sm, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpz, z);
     };
     switch (K) {
-      case 32: go(lstmf_wgrad_q4_kernel<32>); break;
-      case 36: go(lstmf_wgrad_q4_kernel<36>); break;
-      default: go(lstmf_wgrad_q4_kernel<100>); break;
+      case 32: go(lstmf_wgrad_q4_kernel<32>, 2 * WQGeo<32>::Img::BUF); break;
+      case 36: go(lstmf_wgrad_q4_kernel<36>, 2 * WQGeo<36>::Img::BUF); break;
+      default: go(lstmf_wgrad_q4_kernel<100>, 2 * WQGeo<100>::Img::BUF); break;
     }
     launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s);
     return true;
@@ -2873,15 +2904,14 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
     const int z0 = wgrads_z(M);
     const int rpz = ((M + z0 - 1) / z0 + 31) / 32 * 32;
     const int z = (M + rpz - 1) / rpz;
-    const size_t sm = 2 * WS_BUF;
-    auto go = [&](auto k) {
+    auto go = [&](auto k, size_t sm) {
       allow_lds(reinterpret_cast<const void*>(k));
       hipLaunchKernelGGL(k, dim3(2 * z), dim3(512), sm, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpz, z);
     };
     switch (K) {
-      case 32: go(lstmf_wgrad_split_kernel<32>); break;
-      case 36: go(lstmf_wgrad_split_kernel<36>); break;
-      default: go(lstmf_wgrad_split_kernel<100>); break;
+      case 32: go(lstmf_wgrad_split_kernel<32>, 2 * WSGeo<32>::Img::BUF); break;
+      case 36: go(lstmf_wgrad_split_kernel<36>, 2 * WSGeo<36>::Img::BUF); break;
+      default: go(lstmf_wgrad_split_kernel<100>, 2 * WSGeo<100>::Img::BUF); break;
     }
     launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s);
     return true;

@@ -1,7 +1,9 @@
-"""Static check of the gfx950 code objects for the buffer-store data hazard the compiler misses
-(scripts/isa_store_hazard.py): a >8-byte MUBUF store with a register soffset whose data VGPRs the
-next VALU instruction overwrites.  It corrupted a few fp32 BPTT dZ rows per 10^5 at the bench batch
-before r02.  CPU only: hipcc cross-compiles every csrc/*.hip to assembly."""
+"""Static checks of the gfx950 code objects for hazards the compiler misses.
+
+* scripts/isa_store_hazard.py: a >8-byte MUBUF store with a register soffset whose data VGPRs the next
+  VALU instruction overwrites.  It corrupted a few fp32 BPTT dZ rows per 10^5 at the bench batch before r02.
+* scripts/isa_mfma_hazard.py: an MFMA result read across a branch with too few wait states.
+CPU only: hipcc cross-compiles every csrc/*.hip to assembly."""
 import glob
 import os
 import shutil
@@ -16,25 +18,44 @@ CSRC = os.path.join(ROOT, "do-you-really-need-to-pay-2-20-hedge-fund-strategy-re
 HIPCC = "/opt/rocm/bin/hipcc"
 
 
-@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
-def test_no_buffer_store_data_hazard(tmp_path):
-    sys.path.insert(0, os.path.join(ROOT, "scripts"))
-    import isa_store_hazard
-
-    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
-
-    # the SHIPPED kernel flags (-ffp-contract=fast, -munsafe-fp-atomics, -fPIC, ...): the hazard depends
-    # on register allocation, so the scanned assembly must come from the same compile as the library
+@pytest.fixture(scope="module")
+def asm_files(tmp_path_factory):
+    """Every csrc/*.hip assembled with the SHIPPED kernel flags (-ffp-contract=fast, -munsafe-fp-atomics,
+    -fPIC, ...): the hazards depend on register allocation and scheduling, so the scanned assembly must
+    come from the same compile as the library."""
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not installed")
     from hfrep import build_native
 
+    tmp = tmp_path_factory.mktemp("isa")
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
     def asm(src):
-        out = str(tmp_path / (os.path.basename(src) + ".s"))
+        out = str(tmp / (os.path.basename(src) + ".s"))
         subprocess.run([HIPCC] + build_native.kernel_flags(src) + ["--cuda-device-only", "-S", src, "-o", out],
                        check=True, capture_output=True)
         return out
 
     with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
         files = list(ex.map(asm, srcs))
-    hits = [h for f in files for h in isa_store_hazard.scan(f)]
+    yield files
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_no_buffer_store_data_hazard(asm_files):
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import isa_store_hazard
+
+    hits = [h for f in asm_files for h in isa_store_hazard.scan(f)]
     assert not hits, "\n".join(f"{k[:60]}: {a} -> {b}" for k, a, b in hits)
-    shutil.rmtree(tmp_path, ignore_errors=True)
+
+
+def test_no_cross_branch_mfma_read_hazard(asm_files):
+    """scripts/isa_mfma_hazard.py: no MFMA result is read behind a branch with fewer wait states than the
+    compiler's own straight-line requirement for that opcode (a stale accumulator read is timing-dependent:
+    the r02 wgrad case, and the suspect for run-to-run drift in a tangent reverse)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import isa_mfma_hazard
+
+    hits = isa_mfma_hazard.scan(asm_files)
+    assert not hits, "\n".join(f"{k[:60]}: {a} -> {b} ({ws} < {need})" for _, k, a, b, ws, need in hits)
