@@ -78,6 +78,9 @@ def _add_train_args(p):
     p.add_argument("--ckpt-dir", default=None)
     p.add_argument("--ckpt-every", type=int, default=0)
     p.add_argument("--resume", default=None, help="checkpoint path or 'auto'")
+    p.add_argument("--stop-at", type=int, default=None,
+                   help="end this process at that iteration with a checkpoint in --ckpt-dir (a long run split "
+                        "over several processes: rerun with --resume auto)")
     p.add_argument("--no-nan-guard", action="store_true")
     p.add_argument("--graph", action="store_true", help="replay each iteration from a captured hipGraph")
     p.add_argument("--save-dir", default="./trained_generator")
@@ -111,15 +114,32 @@ def build_trainer(a):
     return tr, s
 
 
-def cmd_train(a) -> int:
-    from .train.runner import RunOptions, run
-    from .utils import checkpoint
+def _run_segment(tr, s, a):
+    """Train to ``--stop-at`` (default: the preset's epochs); returns (records, finished).  An early stop
+    leaves a checkpoint of that iteration in ``--ckpt-dir`` for ``--resume auto``."""
+    from .train.runner import RunOptions, checkpoint_now, run
 
-    tr, s = build_trainer(a)
-    opts = RunOptions(epochs=s["epochs"], log_every=s["log_every"], log_path=a.log, echo=not a.quiet,
+    stop = min(a.stop_at, s["epochs"]) if a.stop_at else s["epochs"]
+    if stop < s["epochs"] and not a.ckpt_dir:
+        raise SystemExit("--stop-at before the last iteration needs --ckpt-dir")
+    opts = RunOptions(epochs=stop, log_every=s["log_every"], log_path=a.log, echo=not a.quiet,
                       ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume, nan_guard=not a.no_nan_guard,
                       graph=a.graph)
     recs = run(tr, opts)
+    if tr.iteration < s["epochs"]:
+        checkpoint_now(tr, opts)
+    return recs, tr.iteration >= s["epochs"]
+
+
+def cmd_train(a) -> int:
+    from .utils import checkpoint
+
+    tr, s = build_trainer(a)
+    recs, done = _run_segment(tr, s, a)
+    if not done:
+        if tr.rank == 0:
+            print(json.dumps({"partial": True, "iterations": tr.iteration, "ckpt_dir": a.ckpt_dir}))
+        return 0
     if tr.rank == 0 and not a.no_save:
         prefix = tr.cfg.entry().save_prefix or "GEN"
         path = os.path.join(a.save_dir, f"{prefix}{checkpoint.timestamp()}.pkl")
@@ -222,13 +242,12 @@ def reference_anchor(h5: str | None = None, seed: int = 123, n: int = 1000, wind
 def cmd_parity(a) -> int:
     import torch
 
-    from .train.runner import RunOptions, run
-
     tr, s = build_trainer(a)
-    opts = RunOptions(epochs=s["epochs"], log_every=s["log_every"], log_path=a.log, echo=not a.quiet,
-                      graph=a.graph)
-    run(tr, opts)
+    _, done = _run_segment(tr, s, a)
     if tr.rank != 0:
+        return 0
+    if not done:
+        print(json.dumps({"partial": True, "iterations": tr.iteration, "ckpt_dir": a.ckpt_dir}))
         return 0
     # held-out real windows: a fresh draw from the same panel with another seed
     hold = _dataset(s["data"], s["n_windows"], s["window"], s["features"], s["seed"] + 1000)

@@ -254,6 +254,22 @@ def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[di
     return records
 
 
+def checkpoint_now(trainer, opts: RunOptions) -> str | None:
+    """Checkpoint the current iteration into ``opts.ckpt_dir`` (all ranks call; rank 0 writes), unless
+    the periodic checkpoint of this iteration already exists."""
+    if not opts.ckpt_dir:
+        return None
+    path = os.path.join(opts.ckpt_dir, f"state_{trainer.iteration:09d}.pt")
+    states = _gather_host_rng(trainer)
+    if trainer.rank == 0 and not os.path.exists(path):
+        path = _checkpoint(trainer, opts, states)
+    if trainer.grad_sync is not None and trainer.world > 1:
+        import torch.distributed as dist
+
+        dist.barrier(group=trainer.grad_sync.group)
+    return path
+
+
 def _gather_host_rng(trainer):
     """Every rank's host-RNG state (None with the device counter RNG or a single process)."""
     if trainer.rng.native or trainer.grad_sync is None or trainer.world <= 1:

@@ -72,3 +72,26 @@ def test_clean_cli(data_root, tmp_path):
     common = gold.index.intersection(mine.index)
     assert len(common) == 337
     np.testing.assert_allclose(mine.loc[common].to_numpy(), gold.loc[common].to_numpy(), atol=1e-12)
+
+
+def test_parity_split_over_processes_matches_one_run(tmp_path):
+    """``parity --stop-at N --ckpt-dir D`` then ``--resume auto``: a long parity run split over two
+    processes (the B = 32,768 reference-preset runs that exceed one GPU call) ends with the same
+    W-dist as one uninterrupted process (CPU, smoke preset, synthetic data)."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+
+    def run(*extra):
+        out = subprocess.run([sys.executable, "-m", "hfrep", "parity", "--preset", "smoke", "--epochs", "6", "--quiet",
+                              "--device", "cpu"] + list(extra), cwd=ROOT, env=env, capture_output=True, text=True,
+                             timeout=600)
+        assert out.returncode == 0, out.stderr[-3000:]
+        return json.loads(out.stdout.strip().splitlines()[-1])
+
+    ck = str(tmp_path / "ck")
+    part = run("--stop-at", "3", "--ckpt-dir", ck)
+    assert part == {"partial": True, "iterations": 3, "ckpt_dir": ck}
+    assert os.listdir(ck) == ["state_000000003.pt"]
+    resumed = run("--resume", "auto", "--ckpt-dir", ck)
+    whole = run()
+    assert resumed["iterations"] == whole["iterations"] == 6
+    assert resumed["w_fake_vs_real"] == whole["w_fake_vs_real"]
