@@ -608,11 +608,28 @@ std::tuple<Tensor, Tensor> gp_coef(Tensor g, double weight) {
   const int B = g.size(0);
   const int64_t D = g.numel() / B;
   Tensor v = out_empty_like(g);
-  Tensor pen = at::zeros({}, g.options().dtype(at::kFloat));
+  Tensor pen = out_empty({}, g.options().dtype(at::kFloat));
   Tensor rowpen = out_empty({B}, g.options().dtype(at::kFloat));
   hfrep::launch_gp_coef(dt_of(g), g.data_ptr(), v.data_ptr(), pen.data_ptr<float>(), rowpen.data_ptr<float>(), B, D,
                         (float)weight, cur_stream(g));
   return {pen, v};
+}
+
+// (pack [w0 + w1 + weight pen, w0, w1, pen] fp32, v): gp_coef plus the critic step's loss record, from
+// the W terms w [2] (fp32) of the same step
+std::tuple<Tensor, Tensor> gp_coef_pack(Tensor g, double weight, Tensor w) {
+  CHECK_GPU(g); GUARD(g);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.numel() == 2 && w.is_contiguous() && w.device() == g.device(),
+              "gp_coef_pack: w = the two fp32 W terms on g's device");
+  const int B = g.size(0);
+  const int64_t D = g.numel() / B;
+  Tensor v = out_empty_like(g);
+  Tensor pen = out_empty({}, g.options().dtype(at::kFloat));
+  Tensor pack = out_empty({4}, g.options().dtype(at::kFloat));
+  Tensor rowpen = out_empty({B}, g.options().dtype(at::kFloat));
+  hfrep::launch_gp_coef(dt_of(g), g.data_ptr(), v.data_ptr(), pen.data_ptr<float>(), rowpen.data_ptr<float>(), B, D,
+                        (float)weight, cur_stream(g), w.data_ptr<float>(), pack.data_ptr<float>());
+  return {pack, v};
 }
 
 // (segment losses [2] fp32, dL/dp like p): see csrc/misc.hip gan_loss_kernel
@@ -747,6 +764,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("layernorm_tbwd_(Tensor? dy, Tensor dyd, Tensor xd, Tensor xhat, Tensor rstd, Tensor gamma, "
         "Tensor(a!) ggamma, Tensor(b!) gbeta, bool need_dx) -> (Tensor, Tensor)");
   m.def("gp_coef(Tensor g, float weight) -> (Tensor, Tensor)");
+  m.def("gp_coef_pack(Tensor g, float weight, Tensor w) -> (Tensor, Tensor)");
   m.def("gan_loss(Tensor p, int split, float la, float lb, int kind) -> (Tensor, Tensor)");
   m.def("im2col_causal(Tensor x, int k, int dil) -> Tensor");
   m.def("col2im_causal(Tensor dcols, int k, int dil, int C) -> Tensor");
@@ -786,6 +804,7 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("layernorm_tfwd", &layernorm_tfwd);
   m.impl("layernorm_tbwd_", &layernorm_tbwd_);
   m.impl("gp_coef", &gp_coef);
+  m.impl("gp_coef_pack", &gp_coef_pack);
   m.impl("gan_loss", &gan_loss);
   m.impl("im2col_causal", &im2col_causal);
   m.impl("col2im_causal", &col2im_causal);

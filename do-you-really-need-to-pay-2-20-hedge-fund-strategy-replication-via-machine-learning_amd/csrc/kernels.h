@@ -145,7 +145,7 @@ void launch_gan_loss(int dt, const void* p, int64_t n, int64_t split, float la, 
                      float* partial, float* out, hipStream_t s);
 int gan_loss_partials();
 void launch_gp_coef(int dt, const void* g, void* v, float* pen, float* rowpen, int B, int64_t D, float weight,
-                    hipStream_t s);
+                    hipStream_t s, const float* w = nullptr, float* pack = nullptr);
 void launch_interpolate(int dt, const void* real, const void* fake, const float* alpha, void* out, int B,
                         int64_t D, hipStream_t s);
 void launch_philox_fill(int dt, void* out, int64_t n, uint64_t seed, int64_t* ctr, int dist, hipStream_t s);

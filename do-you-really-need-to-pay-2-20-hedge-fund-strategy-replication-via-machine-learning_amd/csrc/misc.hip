@@ -558,16 +558,27 @@ __global__ void __launch_bounds__(256) gp_coef_kernel(const T* __restrict__ g, T
   if (lane == 0) rowpen[b] = one_m * one_m / B;
 }
 
-__global__ void __launch_bounds__(1024) sum_into_kernel(const float* __restrict__ x, int n, float* __restrict__ out) {
+// pen = sum of the row penalties (fixed order: bitwise reproducible); with w (the critic's two W terms)
+// also the step's loss record pack = [w0 + w1 + weight pen, w0, w1, pen] (no torch glue on the step)
+__global__ void __launch_bounds__(1024) gp_sum_kernel(const float* __restrict__ x, int n, float* __restrict__ out,
+                                                      const float* __restrict__ w, float weight, float* __restrict__ pack) {
   __shared__ float red[16];
   float s = 0.f;
   for (int i = threadIdx.x; i < n; i += 1024) s += x[i];
   s = block_sum<16>(s, red);
-  if (threadIdx.x == 0) out[0] += s;
+  if (threadIdx.x == 0) {
+    out[0] = s;
+    if (pack) {
+      pack[0] = w[0] + w[1] + weight * s;
+      pack[1] = w[0];
+      pack[2] = w[1];
+      pack[3] = s;
+    }
+  }
 }
 
 void launch_gp_coef(int dt, const void* g, void* v, float* pen, float* rowpen, int B, int64_t D, float weight,
-                    hipStream_t s) {
+                    hipStream_t s, const float* w, float* pack) {
   const int grid = (B + 3) / 4;
   if (dt == DT_BF16)
     hipLaunchKernelGGL(gp_coef_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)g, (bf16_t*)v, rowpen, B, D,
@@ -575,7 +586,7 @@ void launch_gp_coef(int dt, const void* g, void* v, float* pen, float* rowpen, i
   else
     hipLaunchKernelGGL(gp_coef_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)g, (float*)v, rowpen, B, D,
                        weight);
-  hipLaunchKernelGGL(sum_into_kernel, dim3(1), dim3(1024), 0, s, rowpen, B, pen);
+  hipLaunchKernelGGL(gp_sum_kernel, dim3(1), dim3(1024), 0, s, rowpen, B, pen, w, weight, pack);
 }
 
 // ------------------------------------------------------------------ GAN losses

@@ -178,14 +178,16 @@ class Dense(Layer):
 
     def etbwd(self, ctx, tctx, dy, dyd, need_dx):
         dzd = Fn.act_backward(dyd, ctx["y"], self.act_code)
-        dz = Fn.act_tangent_backward(dy, dyd, ctx["y"], tctx["zd"], self.act_code)
-        Fn.linear_wgrad_(ctx["x"], dz, self.g("kernel"), self.g("bias") if self.use_bias else None)
+        # dy is None (no primal seed) with a piecewise-linear activation: dz == 0 (f'' = 0), so its weight
+        # gradient term vanishes and dx is the zero adjoint (None) -- nothing is materialised
+        zero_dz = dy is None and self.act_code in (0, 3, 4)
+        if not zero_dz:
+            dz = Fn.act_tangent_backward(dy, dyd, ctx["y"], tctx["zd"], self.act_code)
+            Fn.linear_wgrad_(ctx["x"], dz, self.g("kernel"), self.g("bias") if self.use_bias else None)
         Fn.linear_wgrad_(tctx["xd"], dzd, self.g("kernel"), None)
         if not need_dx:
             return None, None
-        # dy is None (no primal seed) with a linear head: dz == 0, so dx is the zero adjoint (None)
-        dx = None if (dy is None and self.act_code in (0, 3, 4)) else self._dgrad(dz)
-        return dx, self._dgrad(dzd)
+        return (None if zero_dz else self._dgrad(dz)), self._dgrad(dzd)
 
 
 class LSTM(Layer):

@@ -262,6 +262,17 @@ def gp_coef(g: torch.Tensor, weight: float):
     return R.gp_coef(g, weight)
 
 
+def gp_coef_pack(g: torch.Tensor, weight: float, w: torch.Tensor):
+    """(pack, v): gp_coef plus the critic step's loss record pack = [w0 + w1 + weight*pen, w0, w1, pen]
+    (fp32) from the step's two W terms ``w`` -- one native launch pair on the GPU, no torch glue."""
+    if _nat(g) and w.dtype == torch.float32:
+        return _ops().gp_coef_pack(g.contiguous(), float(weight), w.contiguous())
+    pen, v = gp_coef(g, weight)
+    w = w.to(torch.float64 if g.dtype == torch.float64 else torch.float32)
+    pen = pen.to(w.dtype)
+    return torch.stack([w[0] + w[1] + weight * pen, w[0], w[1], pen]), v
+
+
 def interpolate(real: torch.Tensor, fake: torch.Tensor, alpha: torch.Tensor) -> torch.Tensor:
     """alpha (B,) per-sample: alpha*real + (1-alpha)*fake (GAN/MTSS_WGAN_GP.py:197-199)."""
     if _nat(real):

@@ -101,6 +101,7 @@ class GANTrainer:
         self.iteration = 0
         self._d_acc = torch.zeros(4, device=self.device)  # last d_loss terms: total, real, fake, gp
         self._g_acc = torch.zeros(1, device=self.device)
+        self._ones_cache = {}
         self.grad_sync = None  # set by hfrep.parallel.DataParallel
         if world > 1 and process_group is not None:
             from ..parallel.dp import GradSync
@@ -191,15 +192,21 @@ class GANTrainer:
         # theta-gradient of <v, g> as reverse-over-tangent
         with trange("critic/gp_input_grad"):
             sh, tape_h = C.efwd(xh, save=True)
-            g = C.ebwd(tape_h, torch.ones_like(sh), need_dx=True, wgrad=False)
-            pen, v = Fn.gp_coef(g, self.gp_weight)
+            g = C.ebwd(tape_h, self._ones(sh), need_dx=True, wgrad=False)
+            pack, v = Fn.gp_coef_pack(g, self.gp_weight, w)  # [total, W real, W fake, GP]
         with trange("critic/gp_second_order"):
             sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
-            C.etbwd(tape_h, ttape, None, torch.ones_like(sd), hook=self._hook(C))
-        w = w.to(self._acc)
-        w_real, w_fake = w[0], w[1]
-        pen = pen.to(self._acc)
-        return torch.stack([w_real + w_fake + self.gp_weight * pen, w_real, w_fake, pen])
+            C.etbwd(tape_h, ttape, None, self._ones(sd), hook=self._hook(C))
+        return pack.to(self._acc)
+
+    def _ones(self, like):
+        """A persistent all-ones seed shaped like ``like`` (allocated once per shape / dtype: no fill
+        kernel on the step; read-only, so graph replays see the same tensor)."""
+        key = (tuple(like.shape), like.dtype, like.device)
+        t = self._ones_cache.get(key)
+        if t is None:
+            t = self._ones_cache[key] = torch.ones_like(like)
+        return t
 
     # ---- generator ------------------------------------------------------------------------
     def _generator_step(self, noise, gen=None):

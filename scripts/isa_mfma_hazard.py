@@ -103,26 +103,28 @@ def scan_kernel(ins, labels):
     for i, l in enumerate(ins):
         if not l.startswith("v_mfma"):
             continue
-        dst = allregs(operands(l)[0])
+        dst = frozenset(allregs(operands(l)[0]))
         seen = {}
-        stack = [(j, 0, False) for j in succ(ins, labels, i)]
+        stack = [(j, 0, False, dst) for j in succ(ins, labels, i)]
         while stack:
-            j, ws, br = stack.pop()
-            if j is None or j >= len(ins) or ws >= MIN_WS:
+            j, ws, br, live = stack.pop()
+            if j is None or j >= len(ins) or ws >= MIN_WS or not live:
                 continue
-            if seen.get((j, br), MIN_WS + 1) <= ws:
+            if seen.get((j, br, live), MIN_WS + 1) <= ws:
                 continue
-            seen[(j, br)] = ws
+            seen[(j, br, live)] = ws
             lj = ins[j]
             op = lj.split()[0]
-            if not op.startswith("v_mfma") and reads(lj) & dst:
+            if not op.startswith("v_mfma") and reads(lj) & live:
                 out.append((i, j, ws, br))
                 continue
-            if op.startswith("v_mfma") and allregs(operands(lj)[0]) & dst:
+            if op.startswith("v_mfma") and allregs(operands(lj)[0]) & live:
                 continue  # overwritten / accumulated by a later MFMA: that one's readers are checked on their own
+            if op.startswith(("v_", "ds_read", "ds_load", "buffer_load", "global_load", "scratch_load")) and operands(lj):
+                live = live - allregs(operands(lj)[0])  # registers rewritten on this path hold new values
             nxt = succ(ins, labels, j)
             brn = br or op.startswith(("s_branch", "s_cbranch"))
-            stack += [(k, ws + ws_of(lj), brn) for k in nxt]
+            stack += [(k, ws + ws_of(lj), brn, live) for k in nxt]
     return out
 
 

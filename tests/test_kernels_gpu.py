@@ -205,6 +205,12 @@ def test_gp_coef_and_interpolate(cuda, dt):
     rp, rv = R.gp_coef(gr.double(), 10.0)
     assert abs(pen.item() - rp.item()) <= 1e-4 * max(1, abs(rp.item()))
     _close(v, rv, dt)
+    # the critic step's loss record from the same launch pair: [w0 + w1 + 10 pen, w0, w1, pen]
+    w = torch.tensor([0.25, -1.5], device=cuda)
+    pack, v2 = _ops().gp_coef_pack(gr.to(cuda), 10.0, w)
+    assert torch.equal(v2, v) and pack[3].item() == pen.item()
+    want = torch.tensor([0.25 - 1.5 + 10.0 * pen.item(), 0.25, -1.5, pen.item()])
+    assert torch.allclose(pack.cpu(), want, rtol=1e-6, atol=1e-6), (pack, want)
     a, b = torch.rand(64, 24, 32, generator=g).to(dt), torch.rand(64, 24, 32, generator=g).to(dt)
     al = torch.rand(64, generator=g)
     out = _ops().interpolate(a.to(cuda), b.to(cuda), al.to(cuda))
