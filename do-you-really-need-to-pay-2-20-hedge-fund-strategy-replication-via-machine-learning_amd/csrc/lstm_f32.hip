@@ -2549,7 +2549,16 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
         acc[e] = mma32(a[0], bw[e][ks][1], acc[e]);  // hm
         acc[e] = mma32(a[0], bw[e][ks][0], acc[e]);  // hh
       }
-      if (ks >= DS4_K0) stage(std::integral_constant<int, S ^ 1>{}, nxt, ks - DS4_K0);  // (compile-time)
+      if (ks >= DS4_K0) {
+        stage(std::integral_constant<int, S ^ 1>{}, nxt, ks - DS4_K0);  // (compile-time)
+        // in-order issue: the split's VALU only overlaps the matrix pipe when it sits BETWEEN the
+        // MFMAs in program order (12 MFMAs x 16 cycles vs ~24 VALU x 4 cycles per slot)
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+      }
     }
     // output rows 16 cc + 4 g + i, columns 16 (2 w + e) + c16
     const int nr = min(16, M - 16 * cc);
