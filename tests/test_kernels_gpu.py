@@ -954,10 +954,8 @@ def test_narrowf_dgrad(cuda, M, K, N):
 @pytest.mark.parametrize("B,T,K", [(70, 24, 32), (8192 + 45, 6, 32), (64, 7, 35), (40, 5, 36)])
 def test_lstmf_split_forward_vs_exact(cuda, act, B, T, K):
     """The split-recurrent forward (lstmf_fwds_kernel: h_{t-1} U as the exact three-term bf16 split on
-    v_mfma_f32_16x16x32_bf16 for k < 96, fp32 for the tail) and its row-half pipelined form
-    (lstmf_fwdp_kernel, impl 3) vs the exact-fp32 forward and fp64: primal and tangent forward within 2x
-    the exact kernel's error (+ fp32 noise), bitwise run to run, the pipelined kernel bitwise equal to
-    the unpipelined one."""
+    v_mfma_f32_16x16x32_bf16 for k < 96, fp32 for the tail) vs the exact-fp32 forward and fp64: primal and tangent forward within 2x the exact kernel's error (+ fp32
+    noise), bitwise run to run."""
     from hfrep.ops import functional as Fn
 
     H = 100
@@ -975,7 +973,7 @@ def test_lstmf_split_forward_vs_exact(cuda, act, B, T, K):
     out, errs = {}, {}
     prev = ops.set_lstmf_fwd_impl(1)
     try:
-        for impl in (1, 2, 2, 3, 3):
+        for impl in (1, 2, 2):
             ops.set_lstmf_fwd_impl(impl)
             hs, tape = Fn.lstm_layer_fwd(xg, Wg, bg, Ug, act, True)
             hs0, _ = Fn.lstm_layer_fwd(xg, Wg, bg, Ug, act, False)
@@ -988,12 +986,9 @@ def test_lstmf_split_forward_vs_exact(cuda, act, B, T, K):
                           (hds.double().cpu() - th).abs().max().item())
     finally:
         ops.set_lstmf_fwd_impl(prev)
-    print(f"max abs err exact {errs[1]} split {errs[2]} pipelined split {errs[3]}")
-    for impl in (2, 3):
-        for e1, e2 in zip(errs[1], errs[impl]):
-            assert e2 <= 2 * e1 + 2e-6, (impl, errs[1], errs[impl])
-    # the pipelined kernel computes the same products in the same order per element: bitwise equal
-    assert all(torch.equal(a_, b_) for a_, b_ in zip(out[2], out[3])), "pipelined split forward differs from split"
+    print(f"max abs err exact {errs[1]} split {errs[2]}")
+    for e1, e2 in zip(errs[1], errs[2]):
+        assert e2 <= 2 * e1 + 2e-6, (errs[1], errs[2])
 
 
 @pytest.mark.parametrize("act", [2, 1, 0])
