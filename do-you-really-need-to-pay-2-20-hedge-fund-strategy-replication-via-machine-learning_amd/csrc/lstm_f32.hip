@@ -1974,7 +1974,12 @@ lstmf_dgrad_split_kernel(const float* __restrict__ D, const float* __restrict__ 
 // tail [32][4]; the cell update writes its h (or hdot) straight into them.  Everything else -- the
 // gate-interleaved tiles, the quad transpose, the tapes, x W on the exact fp32 MFMA -- is
 // lstmf_fwd_kernel's.
-constexpr int FS_HR = 104;                                // h plane row stride (bf16 elements)
+// Plane row strides for the 16x16x32 A-fragment ds_read_b128 (lane l: row l & 15, k-group l >> 4, i.e.
+// dword S (l & 15) + 4 (l >> 4)): conflict-free over the CDNA4 b128 lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31} (+32) only for S = 56, 72 (mod 64 multiples) / 216, 232, 248 dwords; the r03 strides
+// (52 / 212 dwords) were conflict-free for contiguous 16-lane groups only and 2-way on the real ones
+// (bwds: SQ_LDS_BANK_CONFLICT 1.56x its LDS-active cycles, profiles/r03_bwds/pmc_bptt_B262144.txt)
+constexpr int FS_HR = 112;                                // h plane row stride (bf16 elements): 56 dwords
 constexpr int FS_HPL = 32 * FS_HR * 2;                    // bytes per h plane (32 rows)
 constexpr int FS_HB = 3 * FS_HPL + 32 * 4 * 4;            // one h buffer: 3 planes + fp32 tail [32][4]
 
@@ -2231,7 +2236,7 @@ lstmf_fwds_kernel(const float* __restrict__ x, const float* __restrict__ W, cons
 // word per plane), row stride 424 (conflict-free ds_read_b128).  B[k][j] = U[j][(k & 3) H + (k >> 2)],
 // k >= 400 zero: 312 registers per wave, 252 of them pinned in AGPRs.  One tape register set: a cell's
 // loads for the other half's next use are issued as soon as it has consumed the set.
-constexpr int BS_LZ = 424;             // dz plane row stride (bf16 elements)
+constexpr int BS_LZ = 432;             // dz plane row stride (bf16 elements): 216 dwords
 constexpr int BS_PL = 32 * BS_LZ * 2;  // bytes per dz plane (32 rows)
 
 template <int ACT>
@@ -2439,7 +2444,7 @@ lstmf_bwds_kernel(const float* __restrict__ dH, const float* __restrict__ tape, 
 // (row stride 424 elements: conflict-free ds_read_b128 A fragments) in slices between the second half
 // of the k-steps, so the split's VALU issue interleaves with the wave's MFMAs.  One barrier per chunk;
 // each chunk's output tiles are final (no partial tiles, no cross-wave reduction).
-constexpr int DS4_RS = 424;                   // LDS image row stride (bf16 elements): >= 416, conflict-free b128
+constexpr int DS4_RS = 432;                   // LDS image row stride (bf16 elements): >= 416, conflict-free b128
 constexpr int DS4_PL = 16 * DS4_RS * 2;       // bytes per plane image (16 rows)
 constexpr int DS4_BUF = 3 * DS4_PL;           // one buffer: three planes
 constexpr int DS4_SLOTS = (16 * 100 + 255) / 256;  // float4 staging slots per thread per chunk (7)
