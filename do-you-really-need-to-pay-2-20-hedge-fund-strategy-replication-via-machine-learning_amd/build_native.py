@@ -102,17 +102,25 @@ def _compile(src, obj, flags, headers):
     return obj, True
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
-    os.makedirs(BUILD_DIR, exist_ok=True)
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True, variant: str | None = None,
+          extra: list[str] | None = None) -> str:
+    """Build the library.  ``variant`` / ``extra``: an A/B build of the same sources with extra kernel
+    flags (e.g. ``-DHFREP_TBWD_DXGEN=1``) into ``variants/<variant>/_hfrep_native.so`` (objects under
+    ``build/native_<variant>``), loaded through ``HFREP_NATIVE_LIB``; the default build is untouched."""
+    out_so = OUT_SO if not variant else os.path.join(os.path.dirname(HERE), "variants", variant, "_hfrep_native.so")
+    bdir = BUILD_DIR if not variant else BUILD_DIR + "_" + variant
+    os.makedirs(bdir, exist_ok=True)
+    os.makedirs(os.path.dirname(out_so), exist_ok=True)
     kern, bind, link = _flags()
+    kern = kern + list(extra or [])
     hips, cpps, headers = _sources()
     if force:
-        for f in os.listdir(BUILD_DIR):
-            os.remove(os.path.join(BUILD_DIR, f))
+        for f in os.listdir(bdir):
+            os.remove(os.path.join(bdir, f))
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
-    tasks = [(s, os.path.join(BUILD_DIR, os.path.basename(s) + ".o"), kern + EXTRA_FLAGS.get(os.path.basename(s), []))
+    tasks = [(s, os.path.join(bdir, os.path.basename(s) + ".o"), kern + EXTRA_FLAGS.get(os.path.basename(s), []))
              for s in hips]
-    tasks += [(s, os.path.join(BUILD_DIR, os.path.basename(s) + ".o"), bind) for s in cpps]
+    tasks += [(s, os.path.join(bdir, os.path.basename(s) + ".o"), bind + list(extra or [])) for s in cpps]
     changed = False
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_compile, s, o, f, headers) for s, o, f in tasks]
@@ -121,29 +129,32 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
             o, c = fut.result()
             objs.append(o)
             changed |= c
-    if changed or not os.path.exists(OUT_SO) or force:
-        tmp = OUT_SO + ".tmp"
+    OUT = out_so
+    if changed or not os.path.exists(OUT) or force:
+        tmp = OUT + ".tmp"
         cmd = [_hipcc()] + objs + link + ["-o", tmp]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
-        os.replace(tmp, OUT_SO)
-        meta = {"arch": ARCH, "sources": [os.path.basename(s) for s in hips + cpps]}
-        with open(OUT_SO + ".json", "w") as fh:
+        os.replace(tmp, OUT)
+        meta = {"arch": ARCH, "sources": [os.path.basename(s) for s in hips + cpps], "extra": list(extra or [])}
+        with open(OUT + ".json", "w") as fh:
             json.dump(meta, fh)
         if verbose:
-            print(f"[hfrep.build_native] linked {OUT_SO} ({len(objs)} objects)")
+            print(f"[hfrep.build_native] linked {OUT} ({len(objs)} objects)")
     elif verbose:
-        print(f"[hfrep.build_native] up to date: {OUT_SO}")
-    return OUT_SO
+        print(f"[hfrep.build_native] up to date: {OUT}")
+    return OUT
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--variant", default=None, help="A/B build name (variants/<name>/_hfrep_native.so)")
+    ap.add_argument("--extra", default="", help="extra kernel flags of the variant build (one string)")
     a = ap.parse_args(argv)
-    build(force=a.force, jobs=a.jobs)
+    build(force=a.force, jobs=a.jobs, variant=a.variant, extra=a.extra.split() if a.extra else None)
 
 
 if __name__ == "__main__":

@@ -480,7 +480,11 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm2_tbwd(optional<Tensor> dH, optio
   // the in-kernel generated head adjoint is only combined with the dX-free instantiation: the
   // DX + GEN tangent reverse gave run-to-run different rows (profiles/r01_fwd5/README.md); with W
   // the head adjoint is materialised instead (the native op can never reach that instantiation)
+#if defined(HFREP_TBWD_DXGEN) && HFREP_TBWD_DXGEN  // (variant builds for root-cause experiments only)
+  const bool gen = head && hfrep::lstm2_head_fusion();
+#else
   const bool gen = head && hfrep::lstm2_head_fusion() && K == 0;
+#endif
   optional<Tensor> dHm = dH;
   Tensor dHd;
   if (head && !gen) {  // materialise for the v2 kernels

@@ -1116,6 +1116,19 @@ typedef short bf16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4 mma16k16(const bf16x4& a, const bf16x4& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
+// gfx950 forwards an MFMA accumulator to the next MFMA's SrcC only between SAME opcodes: a
+// v_mfma_f32_16x16x16_bf16 reading the result of a v_mfma_f32_16x16x32_bf16 as SrcC reads registers 0-1
+// stale below 5 wait states, the reverse pair registers 2-3 (scripts/probes/mfma_srcc_probe.hip,
+// profiles/r03_race) -- and LLVM puts as few as 1 (scripts/isa_mfma_srcc.py).  That was the run-to-run
+// nondeterminism of rows 4 g + {0, 1} in the bf16 tangent reverse / two-step-prefetch forward
+// (profiles/r02_det).  xdl_switch() sits between the two kinds of MFMA of one accumulator chain: no
+// instruction crosses it and the chain's last MFMA is >= 5 wait states behind the first of the other
+// kind (operand loads are issued before it).
+__device__ __forceinline__ void xdl_switch() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 struct Slot8 {  // 8 bf16 of one 16x16-layout lane: block m = 0, 1 (rows 16 m + 4 (lane >> 4) + i)
   uint2 m0, m1;
   __device__ __forceinline__ float get(int m, int i) const {
@@ -1327,6 +1340,7 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
               if constexpr (TAIL) {
                 const bf16x4 a = *reinterpret_cast<const bf16x4*>(rowz + 32 * NK + 4 * g4);
                 const bf16x4 ad = *reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4);
+                xdl_switch();
                 ah[m] = mma16k16(a, ut4, ah[m]);
                 ahd[m] = mma16k16(ad, ut4, ahd[m]);
                 if constexpr (DX) {
@@ -1341,8 +1355,11 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
                 ahd[m] = mma16(*reinterpret_cast<const bf16x8*>(drow + 32 * ks), ut[ks], ahd[m]);
               }
               if constexpr (TAIL) {
-                ah[m] = mma16k16(*reinterpret_cast<const bf16x4*>(rowz + 32 * NK + 4 * g4), ut4, ah[m]);
-                ahd[m] = mma16k16(*reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4), ut4, ahd[m]);
+                const bf16x4 a = *reinterpret_cast<const bf16x4*>(rowz + 32 * NK + 4 * g4);
+                const bf16x4 ad = *reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4);
+                xdl_switch();
+                ah[m] = mma16k16(a, ut4, ah[m]);
+                ahd[m] = mma16k16(ad, ut4, ahd[m]);
               }
             }
           }
@@ -1411,8 +1428,11 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
               axd[m] = mma16(*reinterpret_cast<const bf16x8*>(rowd + 8 * g4 + 32 * ks), wt[ks], axd[m]);
             }
             if constexpr (TAIL) {
-              ax[m] = mma16k16(*reinterpret_cast<const bf16x4*>(rowz + 32 * NK + 4 * g4), wt4, ax[m]);
-              axd[m] = mma16k16(*reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4), wt4, axd[m]);
+              const bf16x4 a = *reinterpret_cast<const bf16x4*>(rowz + 32 * NK + 4 * g4);
+              const bf16x4 ad = *reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4);
+              xdl_switch();
+              ax[m] = mma16k16(a, wt4, ax[m]);
+              axd[m] = mma16k16(ad, wt4, axd[m]);
             }
           }
         }
@@ -1679,11 +1699,6 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[q][m] = mma16(a, wf[q][ks], acc[q][m]);
           }
-          if constexpr (KS::TAIL) {  // 16-wide tail: lane holds A[row][32 NF + 4 (lane >> 4) + j]
-            const bf16x4 a = *reinterpret_cast<const bf16x4*>(xcur + (16 * m + (lane & 15)) * LX + 32 * NKXM + 4 * g4);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q][m] = mma16k16(a, wf4[q], acc[q][m]);
-          }
           const bf16_t* hrow = hcur + (16 * m + (lane & 15)) * LH + 8 * g4;
 #pragma unroll
           for (int ks = 0; ks < NKH; ++ks) {
@@ -1691,10 +1706,22 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[q][m] = mma16(a, uf[q][ks], acc[q][m]);
           }
-          if constexpr (HS::TAIL) {
-            const bf16x4 a = *reinterpret_cast<const bf16x4*>(hcur + (16 * m + (lane & 15)) * LH + 32 * NKH + 4 * g4);
+          // the 16-wide tails (lane holds A[row][32 NF + 4 (lane >> 4) + j]) after both 32-wide chains:
+          // one opcode switch per accumulator (xdl_switch); the two tails then chain on the same opcode
+          // (16x16x16 -> 16x16x16 forwards: scripts/probes/mfma_srcc_probe.hip).  (Merging both tails into
+          // one zero-padded 16x16x32 step needs no switch but spilled more at K = 100: bf16 384.3 vs 376.9 ms)
+          if constexpr (KS::TAIL || HS::TAIL) {
+            const bf16x4 ax4 = *reinterpret_cast<const bf16x4*>(xcur + (16 * m + (lane & 15)) * LX + 32 * NKXM + 4 * g4);
+            const bf16x4 ah4 = *reinterpret_cast<const bf16x4*>(hcur + (16 * m + (lane & 15)) * LH + 32 * NKH + 4 * g4);
+            xdl_switch();
+            if constexpr (KS::TAIL) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q][m] = mma16k16(a, uf4[q], acc[q][m]);
+              for (int q = 0; q < 4; ++q) acc[q][m] = mma16k16(ax4, wf4[q], acc[q][m]);
+            }
+            if constexpr (HS::TAIL) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) acc[q][m] = mma16k16(ah4, uf4[q], acc[q][m]);
+            }
           }
         }
 #pragma unroll
@@ -2033,7 +2060,15 @@ void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const 
     const size_t sm = Tb4Geo<100>::smem;
     if (dX) {
       // DX + GEN (generated head adjoint with the fused input gradient) is not instantiated: it gave
-      // run-to-run different rows; callers materialise the head adjoint when they want dX
+      // run-to-run different rows; callers materialise the head adjoint when they want dX.
+      // HFREP_TBWD_DXGEN=1: a variant build that dispatches it (root-cause experiments only,
+      // scripts/gpu_race.sh)
+#if defined(HFREP_TBWD_DXGEN) && HFREP_TBWD_DXGEN
+      HFREP_TBWD4_LAUNCH(true, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
+                         (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, W, (bf16_t*)dX, (bf16_t*)dXd, B, Tn, K, hd,
+                         hdd, hw)
+      return;
+#endif
       if (hw) {
         fprintf(stderr, "launch_lstm2_tbwd: generated head adjoint with dX is not supported\n");
         abort();

@@ -10,7 +10,11 @@ from hfrep.ops import functional as Fn  # noqa: E402
 
 dev = torch.device("cuda:0")
 H = 100
-for (B, T, K, act) in [(256, 24, 32, 1), (256, 24, 100, 1), (512, 24, 32, 2), (512, 24, 100, 2), (70, 24, 35, 2)]:
+# usage: python scripts/dbg_determinism.py [BATCH_SCALE [REPEATS]]   (row counts x BATCH_SCALE)
+SCALE = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+shapes = [(256, 24, 32, 1), (256, 24, 100, 1), (512, 24, 32, 2), (512, 24, 100, 2), (70, 24, 35, 2), (64, 24, 32, 0)]
+for (B, T, K, act) in [(B * SCALE + (B % 7 if SCALE > 1 else 0), T, K, a) for (B, T, K, a) in shapes for _ in range(REPS)]:
     g = torch.Generator(device=dev).manual_seed(0)
     mk = lambda *s, sc=0.5: (torch.randn(*s, device=dev, generator=g) * sc).to(torch.bfloat16)
     x, xd, dH = mk(B, T, K), mk(B, T, K), mk(B, T, H)

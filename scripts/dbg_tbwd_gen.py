@@ -9,8 +9,9 @@ import hfrep  # noqa: E402,F401
 from hfrep.ops import functional as Fn  # noqa: E402
 
 dev = torch.device("cuda:0")
-H, T, K, act = 100, 24, 100, 2
-for B in (32, 64, 256):
+# usage: python scripts/dbg_tbwd_gen.py [K ...]   (default K = 100; the r01 failures were at K = 32 / 35)
+H, T, act = 100, 24, 2
+for K, B in [(k, b) for k in ([int(a) for a in sys.argv[1:]] or [100]) for b in (32, 64, 256)]:
     g = torch.Generator(device=dev).manual_seed(0)
     mk = lambda *s, sc=0.5: (torch.randn(*s, device=dev, generator=g) * sc).to(torch.bfloat16)
     x, xd = mk(B, T, K), mk(B, T, K)
@@ -39,4 +40,4 @@ for B in (32, 64, 256):
                 idx = (diff > 0).nonzero()
                 out[n + "_where"] = (sorted(set(idx[:, 0].tolist()))[:8], sorted(set(idx[:, 1].tolist()))[:8],
                                      sorted(set(idx[:, 2].tolist()))[:12])
-        print(B, "DX" if WW is not None else "noDX", "mat run-to-run", out0, out, flush=True)
+        print(K, B, "DX" if WW is not None else "noDX", "mat run-to-run", out0, out, flush=True)

@@ -18,6 +18,7 @@ import re
 import sys
 from collections import defaultdict
 
+MEASURED = {"v_mfma_f32_16x16x16_bf16": 6, "v_mfma_f32_16x16x32_bf16": 7}
 MIN_WS = 20  # no gfx950 MFMA needs more (16-pass XDL write -> VALU read: 19 wait states)
 
 
@@ -139,6 +140,11 @@ def scan(paths):
                 found.append((p, k, ins[i], ins[j], ws, br))
                 if not br:
                     need[op] = min(need[op], ws)
+    # the compiler's straight-line minimum can only drop to the hardware need when that opcode has
+    # straight-line readers at its minimum somewhere; cap it by the measured need (probes/mfma_raw_probe.hip,
+    # probes/mfma_pk_probe.hip: v_mov / packed-fp32 readers, first clean wait-state count)
+    for op, m in MEASURED.items():
+        need[op] = min(need[op], m)
     return [(p, k, a, b, ws, need[a.split()[0]]) for p, k, a, b, ws, br in found if br and ws < need[a.split()[0]]]
 
 

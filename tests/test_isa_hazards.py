@@ -3,6 +3,9 @@
 * scripts/isa_store_hazard.py: a >8-byte MUBUF store with a register soffset whose data VGPRs the next
   VALU instruction overwrites.  It corrupted a few fp32 BPTT dZ rows per 10^5 at the bench batch before r02.
 * scripts/isa_mfma_hazard.py: an MFMA result read across a branch with too few wait states.
+* scripts/isa_mfma_srcc.py: an MFMA accumulator chained into an MFMA of the OTHER bf16 opcode (16x16x32 <->
+  16x16x16) as SrcC with < 5 wait states: gfx950 does not forward between the two, LLVM assumes it does;
+  the cause of the r01/r02 run-to-run nondeterminism of the bf16 tangent reverse (profiles/r03_race).
 CPU only: hipcc cross-compiles every csrc/*.hip to assembly."""
 import glob
 import os
@@ -59,3 +62,15 @@ def test_no_cross_branch_mfma_read_hazard(asm_files):
 
     hits = isa_mfma_hazard.scan(asm_files)
     assert not hits, "\n".join(f"{k[:60]}: {a} -> {b} ({ws} < {need})" for _, k, a, b, ws, need in hits)
+
+
+def test_no_cross_opcode_mfma_srcc_hazard(asm_files):
+    """scripts/isa_mfma_srcc.py: every v_mfma_f32_16x16x32_bf16 <-> v_mfma_f32_16x16x16_bf16 SrcC hand-over in
+    straight-line code has >= 5 wait states (measured need, scripts/probes/mfma_srcc_probe.hip); the kernels
+    separate the two kinds with xdl_switch() (csrc/lstm2.hip)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import isa_mfma_srcc
+
+    _, hits = isa_mfma_srcc.scan(asm_files)
+    assert not hits, "\n".join(f"{os.path.basename(p)}:{ln} {(fn or '?')[:60]}: {a} -> {b} ({ws} < {need})"
+                               for p, ln, fn, a, b, ws, need in hits)
