@@ -477,14 +477,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm2_tbwd(optional<Tensor> dH, optio
   TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstm2_tape_elems(B, Tn) && ttape.numel() == tape.numel(), "tape size");
   GUARD(tape);
   const int K = check_dx_W(W, H);
-  // the in-kernel generated head adjoint is only combined with the dX-free instantiation: the
-  // DX + GEN tangent reverse gave run-to-run different rows (profiles/r01_fwd5/README.md); with W
-  // the head adjoint is materialised instead (the native op can never reach that instantiation)
-#if defined(HFREP_TBWD_DXGEN) && HFREP_TBWD_DXGEN  // (variant builds for root-cause experiments only)
+  // the in-kernel generated head adjoint, with or without the fused input gradient (DX + GEN was parked
+  // in r01-r02 for run-to-run drift; the cause was the cross-opcode MFMA SrcC hazard fixed in r03,
+  // profiles/r03_race/README.md)
   const bool gen = head && hfrep::lstm2_head_fusion();
-#else
-  const bool gen = head && hfrep::lstm2_head_fusion() && K == 0;
-#endif
   optional<Tensor> dHm = dH;
   Tensor dHd;
   if (head && !gen) {  // materialise for the v2 kernels

@@ -2059,23 +2059,11 @@ void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const 
     const int g = persistent_grid(B, 1);
     const size_t sm = Tb4Geo<100>::smem;
     if (dX) {
-      // DX + GEN (generated head adjoint with the fused input gradient) is not instantiated: it gave
-      // run-to-run different rows; callers materialise the head adjoint when they want dX.
-      // HFREP_TBWD_DXGEN=1: a variant build that dispatches it (root-cause experiments only,
-      // scripts/gpu_race.sh)
-#if defined(HFREP_TBWD_DXGEN) && HFREP_TBWD_DXGEN
+      // (DX + GEN -- generated head adjoint with the fused input gradient -- was parked in r01-r02 for
+      // run-to-run drift: the cross-opcode MFMA SrcC hazard, fixed by xdl_switch; profiles/r03_race)
       HFREP_TBWD4_LAUNCH(true, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
                          (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, W, (bf16_t*)dX, (bf16_t*)dXd, B, Tn, K, hd,
                          hdd, hw)
-      return;
-#endif
-      if (hw) {
-        fprintf(stderr, "launch_lstm2_tbwd: generated head adjoint with dX is not supported\n");
-        abort();
-      }
-      HFREP_TBWD4_ACT(true, false, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
-                      (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, W, (bf16_t*)dX, (bf16_t*)dXd, B, Tn, K, hd,
-                      hdd, hw)
     } else
       HFREP_TBWD4_LAUNCH(false, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
                          (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, (const float*)nullptr, (bf16_t*)nullptr,

@@ -431,12 +431,10 @@ def lstm_layer_tbwd(dH, dHd, tape, ttape, U, act: int, W=None):
         return (dZ, dZd) if W is None else (dZ, dZd, linear_dgrad(dZ, W), linear_dgrad(dZd, W))
     if isinstance(tape, torch.Tensor):
         heads = [a for a in (dH, dHd) if isinstance(a, OuterAdjoint)]
-        # the in-kernel generated head adjoint is used without the fused input gradient only: the
-        # DX + generated-dH instantiation of the v4 tangent reverse read stale accumulator values
-        # (rows 16 + 4 g + {0, 1} of a tile, run-to-run different; scripts/dbg_tbwd_gen.py).
-        # HFREP_TBWD_DXGEN=1 with a variant library built with -DHFREP_TBWD_DXGEN=1: dispatch it
-        # anyway (root-cause experiments, scripts/gpu_race.sh)
-        if (W is None or os.environ.get("HFREP_TBWD_DXGEN") == "1") and heads and all(a is None or (isinstance(a, OuterAdjoint) and a.w is heads[0].w)
+        # the in-kernel generated head adjoint, also with the fused input gradient (the DX + GEN
+        # tangent reverse drifted run to run in r01-r02: a cross-opcode MFMA SrcC hazard, fixed in r03,
+        # profiles/r03_race/README.md)
+        if heads and all(a is None or (isinstance(a, OuterAdjoint) and a.w is heads[0].w)
                                        for a in (dH, dHd)):
             w = heads[0].w.reshape(-1).contiguous()
             dZ, dZd, dX, dXd = _ops().lstm2_tbwd(None, None, tape, ttape, U, int(act), W,
