@@ -34,6 +34,14 @@ for r in range(reps):
     z2 = Fn.lstm_layer_tbwd(dH, dH, tape, t1[1], U, act)   # the second tangent tape
     rev = [int((a_ != b_).sum().item()) for a_, b_ in zip(z0, z1)]
     via = [int((a_ != b_).sum().item()) for a_, b_ in zip(z0, z2)]
+    dh = (t0[0].float() - t1[0].float()).abs()
+    ih = (dh > 0).nonzero()
+    if ih.numel():
+        from collections import Counter
+        print(dict(hd_maxdiff=dh.max().item(), hd_ndiff=int(ih.shape[0]),
+                   hd_row_mod32=Counter((ih[:, 0] % 32).tolist()).most_common(12),
+                   hd_steps=Counter(ih[:, 1].tolist()).most_common(6), hd_units=Counter(ih[:, 2].tolist()).most_common(8),
+                   hd_row_blocks=len(set((ih[:, 0] // 32).tolist()))), flush=True)
     d = (z0[0].float() - z1[0].float()).abs()
     idx = (d > 0).nonzero()
     if idx.numel():

@@ -8,7 +8,9 @@
 // followed by VALU writes of the same registers -- assumed safe by the ISA rule (<= 8 bytes), never
 // measured.  Each mode: one asm block per lane and rep, fixed registers:
 //   v_mov v40..43 <- data; buffer_store_<kind> v40[..], v44, s[desc], <soff> offen; v_mov v40..43 <- 0xdeadbeef
-// then every stored slot is checked.  Mode 8 overwrites the voffset register v44 instead of the data.
+// then every stored slot is checked.  Mode 8 overwrites the voffset register v44 instead of the data;
+// modes 9 / 10: a non-temporal 16- / 8-byte store followed at once by an LDS READ into its data registers
+// (the data wave's LDS -> HBM tile copy pattern; the LDS holds 0xdeadbeef).
 //
 // build: hipcc -O3 --offload-arch=gfx950 scripts/probes/store_hazard_probe.hip -o scripts/probes/store_hazard_probe
 #include <hip/hip_runtime.h>
@@ -27,6 +29,10 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 //       8 short, SGPR soffset, the VOFFSET register overwritten next
 template <int MODE>
 __global__ void store_k(unsigned* out, int reps) {
+  __shared__ unsigned lds[256 * 4];  // 0xdeadbeef everywhere: what a late data read of modes 9 / 10 would store
+  for (int i = threadIdx.x; i < 256 * 4; i += blockDim.x) lds[i] = 0xdeadbeefu;
+  __syncthreads();
+  const unsigned lds_a = (unsigned)(size_t)(lds + 4 * threadIdx.x);
   const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
   const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7ffffff0, 0x00020000);
   for (int r = 0; r < reps; ++r) {
@@ -50,8 +56,14 @@ __global__ void store_k(unsigned* out, int reps) {
       asm volatile(PRE "v_add_u32 v44, %3, v44\nbuffer_store_short v40, v44, %2, 0 offen\n" POST ::"v"(val), "v"(voff), "s"(rs), "s"(soff) : CLOB);
     else if constexpr (MODE == 7)
       asm volatile(PRE "v_add_u32 v44, %3, v44\nbuffer_store_dwordx2 v[40:41], v44, %2, 0 offen\n" POST ::"v"(val), "v"(voff), "s"(rs), "s"(soff) : CLOB);
-    else
+    else if constexpr (MODE == 8)
       asm volatile(PRE "buffer_store_short v40, v44, %2, %3 offen\n" POSTA ::"v"(val), "v"(voff), "s"(rs), "s"(soff) : CLOB);
+    else if constexpr (MODE == 9)  // 16-byte store, then an LDS read into the data registers (no wait)
+      asm volatile(PRE "v_add_u32 v44, %3, v44\nbuffer_store_dwordx4 v[40:43], v44, %2, 0 offen nt\nds_read_b128 v[40:43], %4\ns_waitcnt lgkmcnt(0)\n"
+                   ::"v"(val), "v"(voff), "s"(rs), "s"(soff), "v"(lds_a) : CLOB);
+    else  // 8-byte store, then an LDS read into the data registers
+      asm volatile(PRE "v_add_u32 v44, %3, v44\nbuffer_store_dwordx2 v[40:41], v44, %2, 0 offen nt\nds_read_b64 v[40:41], %4\ns_waitcnt lgkmcnt(0)\n"
+                   ::"v"(val), "v"(voff), "s"(rs), "s"(soff), "v"(lds_a) : CLOB);
   }
 }
 
@@ -66,7 +78,7 @@ __global__ void check_k(const unsigned* out, int n, int mode, unsigned long long
     case 0: case 6: case 8: ok = (s[0] & 0xffffu) == (want & 0xffffu); break;
     case 1: ok = (s[0] & 0xffffu) == (want >> 16); break;
     case 2: ok = s[0] == want; break;
-    case 3: case 7: ok = s[0] == want && s[1] == want; break;
+    case 3: case 7: case 10: ok = s[0] == want && s[1] == want; break;
     default: ok = s[0] == want && s[1] == want && s[2] == want && s[3] == want; break;
   }
   if (!ok) atomicAdd(bad, 1ull);
@@ -83,7 +95,8 @@ static void run(unsigned* d, unsigned long long* bad, int blocks, int reps) {
   (void)hipMemcpy(&h, bad, sizeof(h), hipMemcpyDeviceToHost);
   static const char* names[] = {"short sgpr-soff", "short_d16_hi sgpr-soff", "dword sgpr-soff", "dwordx2 sgpr-soff",
                                 "dwordx4 sgpr-soff", "dwordx4 soff0", "short soff0", "dwordx2 soff0",
-                                "short sgpr-soff, voffset overwritten"};
+                                "short sgpr-soff, voffset overwritten", "dwordx4 nt soff0, then ds_read_b128 into the data",
+                                "dwordx2 nt soff0, then ds_read_b64 into the data"};
   printf("{\"mode\": %d, \"store\": \"%s\", \"bad\": %llu, \"stores\": %d}\n", MODE, names[MODE], h, n);
   fflush(stdout);
 }
@@ -93,7 +106,13 @@ int main(int argc, char** argv) {
   unsigned* d;
   unsigned long long* bad;
   if (hipMalloc(&d, (size_t)blocks * 256 * reps * 16) != hipSuccess || hipMalloc(&bad, 8) != hipSuccess) return 1;
+  const bool lds_only = argc > 3 && atoi(argv[3]) == 1;
   for (int it = 0; it < 3; ++it) {
+    if (lds_only) {
+      run<9>(d, bad, blocks, reps);
+      run<10>(d, bad, blocks, reps);
+      continue;
+    }
     run<0>(d, bad, blocks, reps);
     run<1>(d, bad, blocks, reps);
     run<2>(d, bad, blocks, reps);
@@ -103,6 +122,8 @@ int main(int argc, char** argv) {
     run<6>(d, bad, blocks, reps);
     run<7>(d, bad, blocks, reps);
     run<8>(d, bad, blocks, reps);
+    run<9>(d, bad, blocks, reps);
+    run<10>(d, bad, blocks, reps);
   }
   (void)hipFree(d);
   (void)hipFree(bad);

@@ -607,22 +607,50 @@ def test_lstm2_head_adjoint_in_kernel(cuda):
         for seeds, mats in (((None, oad), (None, dHdm)), ((oa, oad), (dHm, dHdm))):
             t1 = Fn.lstm_layer_tbwd(seeds[0], seeds[1], tape, ttape, U, act, W=Wx)
             t2 = Fn.lstm_layer_tbwd(mats[0], mats[1], tape, ttape, U, act, W=Wx)
-            # run-to-run bitwise (the generated-adjoint DX instantiation was not: stale accumulator
-            # reads; it is no longer dispatched, functional.lstm_layer_tbwd)
+            # run-to-run bitwise (the generated-adjoint DX instantiation was not in r01-r02: stale
+            # accumulator reads from the cross-opcode MFMA SrcC hazard, profiles/r03_race)
             t1b = Fn.lstm_layer_tbwd(seeds[0], seeds[1], tape, ttape, U, act, W=Wx)
             assert all(torch.equal(a, c) for a, c in zip(t1, t1b))
             # (the GEN and tensor-fed instantiations may contract the gate math differently: 1-ulp
             # bf16 differences that the recurrence carries back, so compare at bf16 tolerance)
             for a, c in zip(t1, t2):
                 _close(a, c.double(), torch.bfloat16)
-    # the native op itself can never reach the DX + generated-head instantiation: with W it
-    # materialises the head adjoint (bindings.cpp lstm2_tbwd) -> bitwise the tensor-fed launch
+    # the native op with W and the head runs the DX + generated-head instantiation (shipped since the
+    # r03 SrcC fix): bitwise the tensor-fed launch here, and run to run
     ops = _ops()
     o1 = ops.lstm2_tbwd(None, None, tape, ttape, U, act, W, d, dd, w.reshape(-1))
     o2 = ops.lstm2_tbwd(dHm, dHdm, tape, ttape, U, act, W)
     assert all(torch.equal(a, c) for a, c in zip(o1, o2))
     o3 = ops.lstm2_tbwd(None, None, tape, ttape, U, act, W, d, dd, w.reshape(-1))
     assert all(torch.equal(a, c) for a, c in zip(o1, o3))
+
+
+@pytest.mark.parametrize("act", [1, 2])
+def test_lstm2_tbwd_bitwise_large_batch(cuda, act):
+    """The bf16 tangent reverse run twice on ONE pair of tapes at B = 32 772 is bitwise equal, with a
+    tensor-fed adjoint and with the generated head adjoint + fused dX.  Before the r03 fix of the
+    cross-opcode MFMA SrcC hazard (a 16x16x16 tail chained onto a 16x16x32 accumulator 1-4 wait states
+    after it) act = sigmoid differed in ~2e5 dZ elements per run, rows 4 g + {0, 1} of a 32-row block
+    (profiles/r03_race/README.md)."""
+    from hfrep.ops import functional as Fn
+
+    H, T, K, B = 100, 24, 32, 32772
+    g = torch.Generator(device=cuda).manual_seed(0)
+    mk = lambda *s_, sc=0.5: (torch.randn(*s_, device=cuda, generator=g) * sc).to(torch.bfloat16)
+    x, xd, dH = mk(B, T, K), mk(B, T, K), mk(B, T, H)
+    W = torch.randn(K, 4 * H, device=cuda, generator=g) * 0.1
+    U = torch.randn(H, 4 * H, device=cuda, generator=g) * 0.1
+    b = torch.randn(4 * H, device=cuda, generator=g) * 0.1
+    _, tape = Fn.lstm_layer_fwd(x, W, b, U, act, True)
+    _, ttape = Fn.lstm_layer_tfwd(xd, W, tape, U, act)
+    z0 = Fn.lstm_layer_tbwd(dH, dH, tape, ttape, U, act)
+    for _ in range(2):
+        z1 = Fn.lstm_layer_tbwd(dH, dH, tape, ttape, U, act)
+        assert all(torch.equal(a, c) for a, c in zip(z0, z1))
+    oa = Fn.OuterAdjoint(mk(B, 1), torch.randn(T * H, 1, device=cuda, generator=g) * 0.1, (B, T, H))
+    y0 = Fn.lstm_layer_tbwd(oa, oa, tape, ttape, U, act, W=W)
+    y1 = Fn.lstm_layer_tbwd(oa, oa, tape, ttape, U, act, W=W)
+    assert all(torch.equal(a, c) for a, c in zip(y0, y1))
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
