@@ -26,6 +26,19 @@ def env_rank() -> tuple[int, int, int]:
             int(os.environ.get("WORLD_SIZE", 1)))
 
 
+def nccl_graph_safe_env() -> None:
+    """Environment for RCCL collectives inside hipGraph captures; set before the process group exists.
+
+    ProcessGroupNCCL recycles its completion events through a cache.  A collective captured into a
+    graph can then RE-RECORD (inside the capture) the event of an eager warmup collective that the
+    watchdog thread still holds; the watchdog's next ``hipEventQuery`` on it fails with
+    hipErrorCapturedEvent ("operation not permitted on an event last recorded in a capturing
+    stream") and the watchdog terminates the process -- tests/test_gpu_rccl.py::
+    test_rccl_grad_sync_in_graph failed this way once in six round-3 runs.  Without the cache every
+    work owns its events, and captured collectives are never enqueued to the watchdog."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
+
 def init_distributed(backend: str | None = None, timeout_s: float = 600.0):
     """Initialise the default process group from the environment (env://).
 
@@ -47,6 +60,7 @@ def init_distributed(backend: str | None = None, timeout_s: float = 600.0):
         torch.cuda.set_device(local_rank)
         # surface RCCL errors as Python exceptions instead of hanging a collective forever
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        nccl_graph_safe_env()
     if not dist.is_initialized():
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":

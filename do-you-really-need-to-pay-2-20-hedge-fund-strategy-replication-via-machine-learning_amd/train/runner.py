@@ -106,6 +106,10 @@ class GraphedStep:
         if t.grad_sync is not None:
             t.grad_sync.finish_()
         torch.cuda.synchronize()
+        if t.grad_sync is not None and t.grad_sync.world > 1:
+            # let the ProcessGroupNCCL watchdog (100 ms loop) retire the warmup collectives before any
+            # collective is recorded into the capture (see parallel/dp.py:nccl_graph_safe_env)
+            time.sleep(0.3)
         it = t.iteration
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):

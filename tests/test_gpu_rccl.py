@@ -31,6 +31,9 @@ def _worker(port, graph, key, q):
 
         os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
         os.environ["HFREP_GRAPH_DP"] = "1"
+        from hfrep.parallel.dp import nccl_graph_safe_env
+
+        nccl_graph_safe_env()  # (before the process group: RCCL events are not recycled into captures)
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
