@@ -279,3 +279,17 @@ def test_bench_refuses_gpus_world_mismatch():
     p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--steps", "1"],
                        capture_output=True, text=True, env=env, timeout=300)
     assert p.returncode == 2 and "WORLD_SIZE" in p.stderr
+
+
+def test_nccl_graph_safe_env_defaults(monkeypatch):
+    """RCCL collectives captured into hipGraphs need ProcessGroupNCCL's event cache off (a captured
+    collective could re-record a cached event the watchdog still polls: hipErrorCapturedEvent); the
+    default is set, an explicit user setting wins."""
+    from hfrep.parallel.dp import nccl_graph_safe_env
+
+    monkeypatch.delenv("TORCH_NCCL_CUDA_EVENT_CACHE", raising=False)
+    nccl_graph_safe_env()
+    assert os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] == "0"
+    monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "1")
+    nccl_graph_safe_env()
+    assert os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] == "1"
