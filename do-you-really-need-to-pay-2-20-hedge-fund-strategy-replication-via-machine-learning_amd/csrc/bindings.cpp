@@ -70,8 +70,9 @@ Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act, optional<Tens
   GUARD(x);
   const int M = x.size(0), K = x.size(1), N = W.size(1);
   if (out.has_value())
-    TORCH_CHECK(out->is_cuda() && out->is_contiguous() && out->scalar_type() == x.scalar_type() && out->numel() == (int64_t)M * N,
-                "linear: out must be a contiguous (M, N) tensor of x's dtype");
+    TORCH_CHECK(out->is_cuda() && out->device() == x.device() && out->is_contiguous() &&
+                    out->scalar_type() == x.scalar_type() && out->numel() == (int64_t)M * N,
+                "linear: out must be a contiguous (M, N) tensor of x's dtype on x's device");
   Tensor y = out.has_value() ? out->view({M, N}) : out_empty({M, N}, x.options());
   if (hfrep::skinny_supported(K, N))
     hfrep::launch_skinny_fwd(dt_of(x), x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
@@ -401,11 +402,8 @@ static int check_dx_W(const optional<Tensor>& W, int H) {
 }
 
 // Flatten -> Dense(1) critic-head adjoint: dH[b, t, h] = head_d[b] * head_w[t H + h] (head_d (B, 1) bf16,
-// head_w (T H) fp32 = the Dense kernel).  Generated inside the reverse kernels when they support it
-// (hfrep::lstm2_head_fusion), otherwise materialised here with the skinny-dgrad rounding.
-static Tensor head_outer(const Tensor& d, const Tensor& w, int64_t B, int64_t Tn, int64_t H) {
-  return (d.reshape({B, 1, 1}).to(at::kFloat) * w.reshape({1, Tn, H})).to(d.scalar_type());
-}
+// head_w (T H) fp32 = the Dense kernel), generated inside the reverse kernels with the skinny-dgrad
+// rounding (bf16(float(d) * w)): the (B, T, H) tensor is never materialised.
 static void check_head(const optional<Tensor>& d, const Tensor& w, const Tensor& like, int64_t B, int64_t Tn, int64_t H) {
   if (!d.has_value()) return;
   CHECK_GPU(*d); same_dt(*d, like);
@@ -428,11 +426,10 @@ std::tuple<Tensor, Tensor> lstm2_bwd(optional<Tensor> dH_, Tensor tape, Tensor U
   const int K = check_dx_W(W, H);
   GUARD(tape);
   TORCH_CHECK(need_dz || K, "lstm2_bwd: nothing to compute (need_dz=False without W)");
-  const bool gen = !dH_ && hfrep::lstm2_head_fusion();
-  Tensor dH = dH_ ? *dH_ : (gen ? Tensor() : head_outer(*head_d, *head_w, B, Tn, H));
+  const bool gen = !dH_;
   Tensor dZ = out_empty({need_dz ? B : 0, Tn, 4 * H}, tape.options());
   Tensor dX = out_empty({K ? B : 0, Tn, K}, tape.options());
-  hfrep::launch_lstm2_bwd(gen ? nullptr : dH.data_ptr(), tape.data_ptr(), U.data_ptr<float>(),
+  hfrep::launch_lstm2_bwd(gen ? nullptr : dH_->data_ptr(), tape.data_ptr(), U.data_ptr<float>(),
                           need_dz ? dZ.data_ptr() : nullptr, K ? W->data_ptr<float>() : nullptr,
                           K ? dX.data_ptr() : nullptr, K, B, Tn, H, (int)act, cur_stream(tape),
                           gen ? head_d->data_ptr() : nullptr, gen ? head_w->data_ptr<float>() : nullptr);
@@ -480,18 +477,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lstm2_tbwd(optional<Tensor> dH, optio
   // the in-kernel generated head adjoint, with or without the fused input gradient (DX + GEN was parked
   // in r01-r02 for run-to-run drift; the cause was the cross-opcode MFMA SrcC hazard fixed in r03,
   // profiles/r03_race/README.md)
-  const bool gen = head && hfrep::lstm2_head_fusion();
-  optional<Tensor> dHm = dH;
-  Tensor dHd;
-  if (head && !gen) {  // materialise for the v2 kernels
-    if (head_d) dHm = head_outer(*head_d, *head_w, B, Tn, H);
-    dHd = head_dd ? head_outer(*head_dd, *head_w, B, Tn, H) : at::zeros({B, Tn, H}, tape.options());
-  } else if (!head) {
-    dHd = *dHd_;
-  }
+  const bool gen = head;
   Tensor dZ = out_empty({B, Tn, 4 * H}, tape.options()), dZd = out_empty({B, Tn, 4 * H}, tape.options());
   Tensor dX = out_empty({K ? B : 0, Tn, K}, tape.options()), dXd = out_empty({K ? B : 0, Tn, K}, tape.options());
-  hfrep::launch_lstm2_tbwd(gen ? nullptr : ptr_or_null(dHm), gen ? nullptr : dHd.data_ptr(), tape.data_ptr(),
+  hfrep::launch_lstm2_tbwd(gen ? nullptr : ptr_or_null(dH), gen ? nullptr : dHd_->data_ptr(), tape.data_ptr(),
                            ttape.data_ptr(), U.data_ptr<float>(), dZ.data_ptr(), dZd.data_ptr(),
                            K ? W->data_ptr<float>() : nullptr, K ? dX.data_ptr() : nullptr, K ? dXd.data_ptr() : nullptr,
                            K, B, Tn, H, (int)act, cur_stream(tape), gen ? ptr_or_null(head_d) : nullptr,
@@ -675,8 +664,9 @@ Tensor sample_windows(Tensor data, int64_t batch, int64_t seed, Tensor ctr, at::
   std::vector<int64_t> shape(data.sizes().begin(), data.sizes().end());
   shape[0] = batch;
   if (dst.has_value())
-    TORCH_CHECK(dst->is_cuda() && dst->is_contiguous() && dst->scalar_type() == out_dtype && dst->sizes() == at::IntArrayRef(shape),
-                "sample_windows: dst must be a contiguous (batch, ...) tensor of out_dtype");
+    TORCH_CHECK(dst->is_cuda() && dst->device() == data.device() && dst->is_contiguous() && dst->scalar_type() == out_dtype &&
+                    dst->sizes() == at::IntArrayRef(shape),
+                "sample_windows: dst must be a contiguous (batch, ...) tensor of out_dtype on data's device");
   Tensor out = dst.has_value() ? *dst : out_empty(shape, data.options().dtype(out_dtype));
   const int64_t N = data.size(0), D = data.numel() / N;
   hfrep::launch_sample_windows(dt_of(out), data.data_ptr<float>(), N, D, out.data_ptr(), (int)batch, (uint64_t)seed,
@@ -729,7 +719,7 @@ void clip_(Tensor p, double c) {
 }  // namespace
 
 TORCH_LIBRARY(hfrep, m) {
-  m.def("linear(Tensor x, Tensor W, Tensor? b, int act, Tensor? out=None) -> Tensor");
+  m.def("linear(Tensor x, Tensor W, Tensor? b, int act, Tensor(a!)? out=None) -> Tensor");  // writes into out when given
   m.def("linear_dgrad(Tensor dz, Tensor W) -> Tensor");
   m.def("linear_wgrad_(Tensor x, Tensor dz, Tensor(a!) gW, Tensor(b!)? gb, int shiftT=0) -> ()");
   m.def("lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor(a!) gW, Tensor(b!) gU, Tensor(c!)? gb, Tensor? xd=None, Tensor? hds=None, Tensor? dZd=None, int impl=0) -> ()");
@@ -770,7 +760,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("col2im_causal(Tensor dcols, int k, int dil, int C) -> Tensor");
   m.def("interpolate(Tensor real, Tensor fake, Tensor alpha) -> Tensor");
   m.def("philox_fill_(Tensor(a!) out, int seed, Tensor(b!) ctr, int dist) -> ()");
-  m.def("sample_windows(Tensor data, int batch, int seed, Tensor(a!) ctr, ScalarType out_dtype, Tensor? dst=None) -> Tensor");
+  m.def("sample_windows(Tensor data, int batch, int seed, Tensor(a!) ctr, ScalarType out_dtype, Tensor(b!)? dst=None) -> Tensor");
   m.def("rmsprop_(Tensor(a!) p, Tensor g, Tensor(b!) ms, float lr, float rho, float eps, float clip, float gscale) -> ()");
   m.def("adam_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, float lr, float b1, float b2, float eps, float clip, float gscale) -> ()");
   m.def("nadam_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor m_cache, float lr, float b1, float b2, float eps, float gscale) -> ()");

@@ -22,7 +22,7 @@ bool launch_lstm_tbwd(int dt, const void* dH, const void* dHd, const void* gates
 
 // ---- lstm2.hip (bf16, fused input projection, blocked tapes; H == 100, K <= 128) ----
 size_t lstm2_tape_elems(int B, int Tn);
-void lstm2_read_stamps(uint64_t* out, int n);  // diagnostic forward phase timers (HFREP_LSTM_DBG & 64)
+void lstm2_read_stamps(uint64_t* out, int n);  // diagnostic BPTT phase timers (HFREP_LSTM_DBG & 128)
 bool lstm2_supported(int H, int K);
 void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float* U, void* hs, void* tape, int B, int Tn,
                       int K, int H, int act, hipStream_t s);
@@ -30,8 +30,7 @@ void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const voi
                        int Tn, int K, int H, int act, hipStream_t s);
 // W / dX non-null: the input gradient dX = dZ W^T (K columns) is produced by the same launch
 // head_d / head_dd + hw: dH (dHdot) = d[b] * hw[t H + h] generated in-kernel (Flatten -> Dense(1) head
-// adjoint; needs lstm2_head_fusion()); otherwise dH / dHd tensors (nullptr = zeros)
-bool lstm2_head_fusion();
+// adjoint); otherwise dH / dHd tensors (nullptr = zeros)
 void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, const float* W, void* dX, int K,
                       int B, int Tn, int H, int act, hipStream_t s, const void* head_d = nullptr,
                       const float* hw = nullptr);
@@ -58,8 +57,8 @@ bool launch_lstmf_tbwd(const float* dH, const float* dHd, const float* tape, con
 // gU += Hprev^T dZ (+ Hdprev^T dZd), gb += colsum dZ, through per-workgroup slabs in ws
 // (lstmf_wgrad_workspace_floats) and one fixed-order reduce
 bool lstmf_wgrad_supported(int K, int H, int N);
-// impl: 0 = default (HFREP_LSTMF_WGRAD, else the split for K <= 36 and exact for K = 100), 1 = exact-fp32
-// MFMA, 2 = the three-term bf16 split
+// impl: 0 = default (exact under HFREP_FP32_EXACT=1, else the pair split for K <= 36 and the quad split for K = 100), 1 = exact-fp32
+// MFMA, 2 = the three-term bf16 split (pair), 3 = the three-term bf16 split (quad)
 size_t lstmf_wgrad_workspace_floats(int M, int K, int impl = 0);
 bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
                         float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl = 0);
@@ -67,9 +66,9 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
 bool lstmf_dgrad_supported(int N, int KO);
 // forward kernel selection: 1 = exact-fp32 everywhere, 2 = split recurrent product for K <= 36 (default);
 // returns the previous setting
-int set_lstmf_fwd_impl(int v);
-int set_lstmf_bwd_impl(int v);  // 1 / 2: exact-fp32 BPTT kernels, else the split-recurrent one
-// impl: 0 = default (HFREP_LSTMF_DGRAD_IMPL, else the exact-fp32 MFMA kernel), 1 = exact, 2 = three-term bf16 split
+int set_lstmf_fwd_impl(int v);  // 1: exact-fp32 forward everywhere, 2: the split-recurrent one for K <= 36
+int set_lstmf_bwd_impl(int v);  // 2: the exact-fp32 BPTT kernel, 3: the split-recurrent one
+// impl: 0 = default (exact under HFREP_FP32_EXACT=1, else the LDS-staged split for KO > 64), 1 = exact, 3 = three-term bf16 split
 bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl = 0);
 
 // ---- gemm.hip ----

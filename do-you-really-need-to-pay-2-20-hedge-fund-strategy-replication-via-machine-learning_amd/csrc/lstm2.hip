@@ -17,14 +17,14 @@
 //
 // Contracts are identical to ops/reference.py (lstm_seq_*), with zx = x W + b folded in.
 //
-// File map (the production kernels are the v3 / v4 ones; v2 stays for A/B runs and as the
-// phase-timer build of the forward: HFREP_LSTM_FWD / _BWD / _TBWD = 2 select it):
+// File map:
 //   buffer descriptors, tile movers, tape slot I/O ........ shared device helpers
-//   lstm_fwd2 / lstm_tfwd2 / lstm_bwd2 / lstm_tbwd2 ........ v2: 32x32x16 MFMA, 32 units per wave
+//   lstm_tfwd2 .............................................. v2 tangent forward (32x32x16, 32 units per
+//                                                            wave): dispatched for act = sigmoid only
 //   lstm_bwd3 ............................................... BPTT: 4 recurrence + 4 data waves
 //   lstm_tbwd4 .............................................. tangent reverse: 16x16x32, 7 + 1 waves
 //   lstm_fwd4 ............................................... forward + tangent forward: 16x16x32
-//   host side ............................................... launchers, version switches
+//   host side ............................................... launchers
 // Every v3 / v4 kernel: one persistent workgroup per CU walking 32-row tiles, 2 waves per SIMD
 // (<= 256 VGPRs, no spills), row-major tiles moved HBM <-> LDS by the data waves, tapes in the
 // blocked 32x32-accumulator layout, buffer-descriptor (range-checked) global accesses.
@@ -344,12 +344,9 @@ __device__ __forceinline__ void store_dx(const f32x16& ax, rsrc_t rd, int Tn, in
 
 }  // namespace
 
-// ==========================================================================================
-// forward (+ optional tape):  z_t = x_t W + b + h_{t-1} U
-// ==========================================================================================
-// diagnostic phase timers (HFREP_LSTM_DBG & 64 -> an ST=true instantiation of the forward
-// kernel): s_memtime deltas per phase summed per wave, read back by lstm2_read_stamps().  Only
-// the diagnostic build executes them; its absolute time is not a benchmark.
+// diagnostic phase timers (HFREP_LSTM_DBG & 128 -> an ST=true instantiation of the BPTT kernel):
+// s_memtime deltas per phase summed per wave, read back by lstm2_read_stamps().  Only the
+// diagnostic build executes them; its absolute time is not a benchmark.
 __device__ unsigned long long g_lstm_stamps[4096 * 8];
 #define HFREP_STAMP(i)                                     \
   if constexpr (ST) {                                      \
@@ -359,130 +356,6 @@ __device__ unsigned long long g_lstm_stamps[4096 * 8];
     st_acc[i] += _t - st_last;                             \
     st_last = _t;                                          \
   }
-
-template <int H, int ACT, int KX, int TILES, bool ST = false>
-__global__ void __launch_bounds__(256 * TILES)
-lstm_fwd2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
-                 const float* __restrict__ U, bf16_t* __restrict__ hs, bf16_t* __restrict__ tape, int B, int Tn,
-                 int K_rt, int dbg) {
-  constexpr int act = ACT;
-  using P = MF<bf16_t>;
-  constexpr int G = 4 * H, NKH = (H + 15) / 16, LH = NKH * 16 + 8, KPADH = NKH * 16;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int K = KX ? KX : K_rt;
-  const int KP = (K + 15) & ~15, LX = KP + 8, NKX = KP / 16;
-  // TILES row tiles of 32 share the staged W^T; the 4 waves of tile `tile` own its x / h buffers
-  const int tile = threadIdx.x >> 8, ltid = threadIdx.x & 255;
-  bf16_t* Wt = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* xb = Wt + G * LX + tile * (2 * 32 * LX + 2 * 32 * LH);
-  bf16_t* hb = xb + 2 * 32 * LX;
-  const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) & 3;
-  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index as a scalar (uniform offsets)
-  const int u = w * 32 + (lane & 31);
-  const bool uok = u < H;
-  const int uc = uok ? u : H - 1;
-  const int nrb = (B + 31) / 32, ngrp = (nrb + TILES - 1) / TILES;
-
-  // per-workgroup prologue, amortised over every row block this persistent workgroup owns
-  stage_wt(Wt, W, K, G, LX);
-  for (int i = ltid; i < 2 * 32 * LX; i += 256) xb[i] = 0;
-  typename P::frag ub[4][NKH];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-#pragma unroll
-    for (int ks = 0; ks < NKH; ++ks)
-      ub[q][ks] = P::make([&](int k) {
-        const float v = U[min(k, H - 1) * G + q * H + uc];
-        return (uok && k < H) ? v : 0.f;
-      }, ks, lane);
-    __builtin_amdgcn_sched_barrier(0);  // one gate's loads in flight at a time: bounded prologue live range
-  }
-  float bq[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) bq[q] = (uok && bias) ? bias[q * H + u] : 0.f;
-  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
-  if constexpr (ST) st_last = __builtin_amdgcn_s_memtime();
-
-  (void)dbg;
-  for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
-  const int rb = grp * TILES + tile, row0 = rb * 32;  // a trailing tile past B only joins the barriers
-  const rsrc_t rx = tile_rsrc(x, row0, B, Tn, K), rh = tile_rsrc(hs, row0, B, Tn, H);
-  const rsrc_t rt = tape_rsrc(tape, rb, nrb, Tn);  // zero records: no tape / idle tile
-  for (int i = ltid; i < 2 * 32 * LH; i += 256) hb[i] = 0;
-  float c[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) c[r] = 0.f;
-  XPref pf;
-  __syncthreads();
-  x_load<KX>(pf, rx, Tn, 0, true, K, ltid);
-  x_store_lds<KX>(pf, xb, K, LX, ltid);
-  __syncthreads();
-
-  for (int t = 0; t < Tn; ++t) {
-    const bf16_t* xcur = xb + (t & 1) * 32 * LX;
-    const bf16_t* hcur = hb + (t & 1) * 32 * LH;
-    bf16_t* hnext = hb + ((t + 1) & 1) * 32 * LH;
-    HFREP_STAMP(7)
-    // loads before stores: the x wait at the end of the step then covers only older traffic
-    x_load<KX>(pf, rx, Tn, t + 1, t + 1 < Tn, K, ltid);
-    HFREP_STAMP(0)
-    tile8_store<H>(hcur, LH, rh, Tn, t - 1, t > 0, ltid);
-    HFREP_STAMP(1)
-    f32x16 acc[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = zero16();
-    const bf16_t* xrow = xcur + (lane & 31) * LX;
-    for (int kx = 0; kx < NKX; ++kx) {
-      const typename P::frag a = P::lda(xrow, kx, lane);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = P::mma(a, P::lda(Wt + (q * H + uc) * LX, kx, lane), acc[q]);
-    }
-    HFREP_STAMP(2)
-    const bf16_t* hrow = hcur + (lane & 31) * LH;
-#pragma unroll
-    for (int ks = 0; ks < NKH; ++ks) {
-      const typename P::frag a = P::lda(hrow, ks, lane);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = P::mma(a, ub[q][ks], acc[q]);
-    }
-    HFREP_STAMP(3)
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {  // two halves of 8 rows: 20 packing registers, not 40
-      uint32_t pk[TAPE_SLOTS][4];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = half * 8 + i;
-        const int rr = acc32_row(r, lane);
-        const float ig = sigmoidf_(acc[0][r] + bq[0]), fg = sigmoidf_(acc[1][r] + bq[1]);
-        const float gg = act_f(act, acc[2][r] + bq[2]), og = sigmoidf_(acc[3][r] + bq[3]);
-        float cn = fg * c[r] + ig * gg;
-        float h = og * act_f(act, cn);
-        if (!uok) { cn = 0.f; h = 0.f; }
-        c[r] = cn;
-        if (u < KPADH) hnext[rr * LH + u] = f2bf(h);
-        put4(pk[0], i, ig); put4(pk[1], i, fg); put4(pk[2], i, gg); put4(pk[3], i, og); put4(pk[4], i, cn);
-      }
-      const int to = tape_off(t, wu) + half * SLOT_HALF;
-#pragma unroll
-      for (int s = 0; s < TAPE_SLOTS; ++s) st_slot(rt, uok, lane * 8, to + s * SLOT_ELEMS, pk[s]);
-    }
-    HFREP_STAMP(4)
-    if (t + 1 < Tn) x_store_lds<KX>(pf, xb + ((t + 1) & 1) * 32 * LX, K, LX, ltid);
-    HFREP_STAMP(5)
-    lds_barrier();  // step hand-off: LDS only, stores stay in flight
-    HFREP_STAMP(6)
-  }
-  tile8_store<H>(hb + (Tn & 1) * 32 * LH, LH, rh, Tn, Tn - 1, true, ltid);
-  __syncthreads();  // LDS is re-initialised for the next row block
-  }
-  if constexpr (ST) {
-    if (lane == 0) {
-      const int slot = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-      if (slot < 4096)
-        for (int i = 0; i < 8; ++i) g_lstm_stamps[slot * 8 + i] = st_acc[i];
-    }
-  }
-}
 
 // ==========================================================================================
 // tangent forward at the taped primal point: zdot_t = xdot_t W + hdot_{t-1} U
@@ -600,137 +473,6 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
     lds_barrier();  // step hand-off: LDS only, stores stay in flight
   }
   tile8_store<H>(hb + (Tn & 1) * 32 * LH, LH, rh, Tn, Tn - 1, true, ltid);
-  __syncthreads();
-  }
-}
-
-// ==========================================================================================
-// BPTT: dZ (B,T,4H) row-major from dH (B,T,H) and the tape
-// ==========================================================================================
-template <int H, int ACT, int TILES, bool DX>
-__global__ void __launch_bounds__(256 * TILES)
-lstm_bwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape, const float* __restrict__ U,
-                 bf16_t* __restrict__ dZ, const float* __restrict__ W, bf16_t* __restrict__ dX, int B, int Tn, int K,
-                 int dbg) {
-  constexpr int act = ACT;
-  using P = MF<bf16_t>;
-  constexpr int G = 4 * H, NKG = (G + 15) / 16, LG = NKG * 16 + 8, NKH = (H + 15) / 16, LH = NKH * 16 + 8;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tile = threadIdx.x >> 8, ltid = threadIdx.x & 255;
-  bf16_t* zb = reinterpret_cast<bf16_t*>(smem) + tile * (2 * 32 * LG + 2 * 32 * LH);  // [2][32][LG]
-  bf16_t* dhb = zb + 2 * 32 * LG;                                                     // [2][32][LH]
-  const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) & 3;
-  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index as a scalar (uniform offsets)
-  const int u = w * 32 + (lane & 31);
-  const bool uok = u < H;
-  const int nrb = (B + 31) / 32, ngrp = (nrb + TILES - 1) / TILES;
-
-  typename P::frag ut[NKG];
-#pragma unroll
-  for (int ks = 0; ks < NKG; ++ks)
-    ut[ks] = P::make([&](int k) {
-      const float v = U[(uok ? u : H - 1) * G + min(k, G - 1)];
-      return (uok && k < G) ? v : 0.f;
-    }, ks, lane);
-  const int kc = w * 32 + (lane & 31);
-  const bool xw = DX && w * 32 < K;  // this wave produces dx columns (wave-uniform)
-  typename P::frag wt[DX ? NKG : 1];
-  if constexpr (DX) make_wt<NKG>(wt, W, K, G, kc, lane);
-  for (int i = ltid; i < 2 * 32 * LG; i += 256) zb[i] = 0;
-
-  (void)dbg;
-  const int lo = lane * 8;
-  for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
-  const int rb = grp * TILES + tile, row0 = rb * 32;
-  const int nr = min(32, B - row0);  // valid rows of this tile
-  const rsrc_t rdh = tile_rsrc(dH, row0, B, Tn, H), rz = tile_rsrc(dZ, row0, B, Tn, G);
-  const rsrc_t rdx = tile_rsrc(DX ? dX : nullptr, row0, B, Tn, DX ? K : 1), rt = tape_rsrc(tape, rb, nrb, Tn);
-  float dc[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) dc[r] = 0.f;
-  __syncthreads();
-  {
-    Tile8<H> d0;
-    d0.load(rdh, Tn, Tn - 1, true, ltid);
-    d0.to_lds(dhb + ((Tn - 1) & 1) * 32 * LH, LH, ltid);
-  }
-  Slot16 tg[4], cc, cp;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) tg[s] = ld_slot(rt, uok, lo, tape_off(Tn - 1, wu) + s * SLOT_ELEMS);
-  cc = ld_slot(rt, uok, lo, tape_off(Tn - 1, wu) + 4 * SLOT_ELEMS);
-  cp = ld_slot(rt, uok && Tn > 1, lo, tape_off(max(Tn - 2, 0), wu) + 4 * SLOT_ELEMS);
-  __syncthreads();
-
-  for (int t = Tn - 1; t >= 0; --t) {
-    const bf16_t* zprev = zb + ((t + 1) & 1) * 32 * LG;  // dz_{t+1}
-    bf16_t* zcur = zb + (t & 1) * 32 * LG;               // dz_t
-    const bf16_t* dhcur = dhb + (t & 1) * 32 * LH;
-    // prefetch step t-1 (tape gates(t-1), cell(t-2), dH(t-1)) BEFORE this step's stores, so that
-    // its wait at the end of the step does not cover them
-    const bool pv = t > 0;
-    Slot16 ng[4], ncp;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) ng[s] = ld_slot(rt, uok && pv, lo, tape_off(max(t - 1, 0), wu) + s * SLOT_ELEMS);
-    ncp = ld_slot(rt, uok && t > 1, lo, tape_off(max(t - 2, 0), wu) + 4 * SLOT_ELEMS);
-    Tile8<H> ndh;
-    ndh.load(rdh, Tn, t - 1, pv, ltid);
-    // dZ == nullptr (zero records): the caller needs only dX (gradient-penalty input gradient,
-    // generator step) and the stores are dropped
-    tile16_store<G>(zprev, LG, rz, Tn, t + 1, t < Tn - 1, ltid);
-    f32x16 acc = zero16(), ax = zero16();
-    if (t < Tn - 1) {
-      const bf16_t* arow = zprev + (lane & 31) * LG;
-      if (xw) {
-#pragma unroll
-        for (int ks = 0; ks < NKG; ++ks) {
-          const typename P::frag a = P::lda(arow, ks, lane);
-          acc = P::mma(a, ut[ks], acc);
-          if constexpr (DX) ax = P::mma(a, wt[ks], ax);
-        }
-      } else {
-#pragma unroll
-        for (int ks = 0; ks < NKG; ++ks) acc = P::mma(P::lda(arow, ks, lane), ut[ks], acc);
-      }
-    }
-    if constexpr (DX) store_dx(ax, rdx, Tn, t + 1, xw && t < Tn - 1, nr, K, kc, lane);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rr = acc32_row(r, lane);
-      const float ig = tg[0].get(r), fg = tg[1].get(r), gg = tg[2].get(r), og = tg[3].get(r);
-      const float c = cc.get(r), cpv = cp.get(r);
-      const float dht = (uok ? bf2f(dhcur[rr * LH + u]) : 0.f) + acc[r];
-      const float ca = act_f(act, c);
-      const float dov = dht * ca;
-      const float dct = dc[r] + dht * og * act_dy(act, ca);
-      dc[r] = uok ? dct * fg : 0.f;
-      float z0 = dct * gg * ig * (1.f - ig);
-      float z1 = dct * cpv * fg * (1.f - fg);
-      float z2 = dct * ig * act_dy(act, gg);
-      float z3 = dov * og * (1.f - og);
-      if (uok) {
-        bf16_t* zr = zcur + rr * LG + u;
-        zr[0] = f2bf(z0); zr[H] = f2bf(z1); zr[2 * H] = f2bf(z2); zr[3 * H] = f2bf(z3);
-      }
-    }
-    if (pv) {
-      ndh.to_lds(dhb + ((t - 1) & 1) * 32 * LH, LH, ltid);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) tg[s] = ng[s];
-      cc = cp;
-      cp = ncp;
-    }
-    lds_barrier();  // step hand-off: LDS only, stores stay in flight
-  }
-  tile16_store<G>(zb, LG, rz, Tn, 0, true, ltid);
-  if constexpr (DX) {
-    f32x16 ax = zero16();
-    if (xw) {
-      const bf16_t* arow = zb + (lane & 31) * LG;
-#pragma unroll
-      for (int ks = 0; ks < NKG; ++ks) ax = P::mma(P::lda(arow, ks, lane), wt[ks], ax);
-    }
-    store_dx(ax, rdx, Tn, 0, xw, nr, K, kc, lane);
-  }
   __syncthreads();
   }
 }
@@ -901,191 +643,6 @@ lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape,
       if (slot < 4096)
         for (int i = 0; i < 8; ++i) g_lstm_stamps[slot * 8 + i] = st_acc[i];
     }
-  }
-}
-
-// ==========================================================================================
-// reverse of the tangent system: (dZ, dZd) from (dH?, dHd), primal tape and tangent tape
-// ==========================================================================================
-template <int H, int ACT, int TILES, bool DX>
-__global__ void __launch_bounds__(256 * TILES)
-lstm_tbwd2_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd, const bf16_t* __restrict__ tape,
-                  const bf16_t* __restrict__ ttape, const float* __restrict__ U, bf16_t* __restrict__ dZ,
-                  bf16_t* __restrict__ dZd, const float* __restrict__ W, bf16_t* __restrict__ dX,
-                  bf16_t* __restrict__ dXd, int B, int Tn, int K) {
-  static_assert(TILES == 1, "tbwd2: one row tile per workgroup (LDS)");
-  constexpr int act = ACT;
-  const int ltid = threadIdx.x;
-  using P = MF<bf16_t>;
-  constexpr int G = 4 * H, NKG = (G + 15) / 16, LG = NKG * 16 + 8, NKH = (H + 15) / 16, LH = NKH * 16 + 8;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* zb = reinterpret_cast<bf16_t*>(smem);  // [2][32][LG]
-  bf16_t* zdb = zb + 2 * 32 * LG;                 // [2][32][LG]
-  bf16_t* dhb = zdb + 2 * 32 * LG;                // [2][32][LH]  (dH)
-  bf16_t* dhdb = dhb + 2 * 32 * LH;               // [2][32][LH]  (dHdot)
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index as a scalar (uniform offsets)
-  const int u = w * 32 + (lane & 31);
-  const bool uok = u < H;
-  const int nrb = (B + 31) / 32;
-
-  typename P::frag ut[NKG];
-#pragma unroll
-  for (int ks = 0; ks < NKG; ++ks)
-    ut[ks] = P::make([&](int k) {
-      const float v = U[(uok ? u : H - 1) * G + min(k, G - 1)];
-      return (uok && k < G) ? v : 0.f;
-    }, ks, lane);
-  const int kc = w * 32 + (lane & 31);
-  const bool xw = DX && w * 32 < K;  // this wave produces dx / dxdot columns (wave-uniform)
-  typename P::frag wt[DX ? NKG : 1];
-  if constexpr (DX) make_wt<NKG>(wt, W, K, G, kc, lane);
-  for (int i = threadIdx.x; i < 2 * 32 * LG; i += 256) { zb[i] = 0; zdb[i] = 0; }
-  for (int i = threadIdx.x; i < 2 * 32 * LH; i += 256) dhb[i] = 0;
-
-  const int lo = lane * 8;
-  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
-  const int row0 = rb * 32;
-  const int nr = min(32, B - row0);  // valid rows of this tile
-  // dH == nullptr (no primal output seed): zero records, the tile loads read zeros
-  const rsrc_t rdh = tile_rsrc(dH, row0, B, Tn, H), rdhd = tile_rsrc(dHd, row0, B, Tn, H);
-  const rsrc_t rz = tile_rsrc(dZ, row0, B, Tn, G), rzd = tile_rsrc(dZd, row0, B, Tn, G);
-  const rsrc_t rdx = tile_rsrc(DX ? dX : nullptr, row0, B, Tn, DX ? K : 1);
-  const rsrc_t rdxd = tile_rsrc(DX ? dXd : nullptr, row0, B, Tn, DX ? K : 1);
-  const rsrc_t rt = tape_rsrc(tape, rb, nrb, Tn), rtt = tape_rsrc(ttape, rb, nrb, Tn);
-  float ac[16], acd[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { ac[r] = 0.f; acd[r] = 0.f; }
-  __syncthreads();
-  {
-    Tile8<H> d0, d1;
-    d0.load(rdh, Tn, Tn - 1, true, ltid);
-    d1.load(rdhd, Tn, Tn - 1, true, ltid);
-    d0.to_lds(dhb + ((Tn - 1) & 1) * 32 * LH, LH, ltid);
-    d1.to_lds(dhdb + ((Tn - 1) & 1) * 32 * LH, LH, ltid);
-  }
-  // c_t and cdot_t carried (loaded at the previous iteration as "prev")
-  Slot16 cc = ld_slot(rt, uok, lo, tape_off(Tn - 1, wu) + 4 * SLOT_ELEMS);
-  Slot16 cdc = ld_slot(rtt, uok, lo, tape_off(Tn - 1, wu) + 4 * SLOT_ELEMS);
-  __syncthreads();
-
-  for (int t = Tn - 1; t >= 0; --t) {
-    const int cb = t & 1, nb = (t + 1) & 1;
-    const bool pv = t > 0;
-    // loads first (next step's dH / dHd tiles, this step's tapes), then this tile's pending
-    // dz / dzdot stores: the tape wait below then covers no store of this step
-    // (the DX variant has no registers for the dH / dHd prefetch: it loads them at the end)
-    Tile8<H> ndh, ndhd;
-    if constexpr (!DX) {
-      ndh.load(rdh, Tn, t - 1, pv, ltid);
-      ndhd.load(rdhd, Tn, t - 1, pv, ltid);
-    }
-    Slot16 tg[4], zd[4], cp, cdp;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      tg[s] = ld_slot(rt, uok, lo, tape_off(t, wu) + s * SLOT_ELEMS);
-      zd[s] = ld_slot(rtt, uok, lo, tape_off(t, wu) + s * SLOT_ELEMS);
-    }
-    cp = ld_slot(rt, uok && pv, lo, tape_off(max(t - 1, 0), wu) + 4 * SLOT_ELEMS);
-    cdp = ld_slot(rtt, uok && pv, lo, tape_off(max(t - 1, 0), wu) + 4 * SLOT_ELEMS);
-    tile16_store<G>(zb + nb * 32 * LG, LG, rz, Tn, t + 1, t < Tn - 1, ltid);
-    tile16_store<G>(zdb + nb * 32 * LG, LG, rzd, Tn, t + 1, t < Tn - 1, ltid);
-    f32x16 ah = zero16(), ahd = zero16(), ax = zero16(), axd = zero16();
-    if (t < Tn - 1) {
-      const bf16_t* arow = zb + nb * 32 * LG + (lane & 31) * LG;
-      const bf16_t* drow = zdb + nb * 32 * LG + (lane & 31) * LG;
-      if (xw) {
-#pragma unroll
-        for (int ks = 0; ks < NKG; ++ks) {
-          const typename P::frag a = P::lda(arow, ks, lane), ad = P::lda(drow, ks, lane);
-          ah = P::mma(a, ut[ks], ah);
-          ahd = P::mma(ad, ut[ks], ahd);
-          if constexpr (DX) {
-            ax = P::mma(a, wt[ks], ax);
-            axd = P::mma(ad, wt[ks], axd);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int ks = 0; ks < NKG; ++ks) {
-          ah = P::mma(P::lda(arow, ks, lane), ut[ks], ah);
-          ahd = P::mma(P::lda(drow, ks, lane), ut[ks], ahd);
-        }
-      }
-    }
-    if constexpr (DX) {
-      store_dx(ax, rdx, Tn, t + 1, xw && t < Tn - 1, nr, K, kc, lane);
-      store_dx(axd, rdxd, Tn, t + 1, xw && t < Tn - 1, nr, K, kc, lane);
-    }
-    const bf16_t* dh_t = dhb + cb * 32 * LH;
-    const bf16_t* dhd_t = dhdb + cb * 32 * LH;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rr = acc32_row(r, lane);
-      const float ig = tg[0].get(r), fg = tg[1].get(r), gg = tg[2].get(r), og = tg[3].get(r);
-      const float c = cc.get(r), cpv = cp.get(r), cd = cdc.get(r), cdpv = cdp.get(r);
-      const float zdi = zd[0].get(r), zdf = zd[1].get(r), zdg = zd[2].get(r), zdo = zd[3].get(r);
-      const float si = ig * (1.f - ig), sf = fg * (1.f - fg), so = og * (1.f - og);
-      const float sg = act_dy(act, gg);
-      const float idot = si * zdi, fdot = sf * zdf, gdot = sg * zdg, odot = so * zdo;
-      const float ca = act_f(act, c);
-      const float e1 = act_dy(act, ca), e2 = act_d2y(act, ca);
-      const float a_h = (uok ? bf2f(dh_t[rr * LH + u]) : 0.f) + ah[r];
-      const float a_hd = (uok ? bf2f(dhd_t[rr * LH + u]) : 0.f) + ahd[r];
-      const float a_od = a_hd * ca;
-      const float a_o = a_h * ca + a_hd * e1 * cd;
-      const float a_cd = acd[r] + a_hd * og * e1;
-      const float a_c = ac[r] + a_h * og * e1 + a_hd * (odot * e1 + og * e2 * cd);
-      const float a_fd = a_cd * cpv, a_id = a_cd * gg, a_gd = a_cd * ig;
-      const float a_f = a_c * cpv + a_cd * cdpv;
-      const float a_i = a_c * gg + a_cd * gdot;
-      const float a_g = a_c * ig + a_cd * idot;
-      ac[r] = uok ? a_c * fg + a_cd * fdot : 0.f;
-      acd[r] = uok ? a_cd * fg : 0.f;
-      const float s2i = si * (1.f - 2.f * ig), s2f = sf * (1.f - 2.f * fg), s2o = so * (1.f - 2.f * og);
-      const float s2g = act_d2y(act, gg);
-      if (uok) {
-        bf16_t* zr = zb + cb * 32 * LG + rr * LG + u;
-        bf16_t* dr = zdb + cb * 32 * LG + rr * LG + u;
-        zr[0] = f2bf(a_i * si + a_id * s2i * zdi);
-        zr[H] = f2bf(a_f * sf + a_fd * s2f * zdf);
-        zr[2 * H] = f2bf(a_g * sg + a_gd * s2g * zdg);
-        zr[3 * H] = f2bf(a_o * so + a_od * s2o * zdo);
-        dr[0] = f2bf(a_id * si);
-        dr[H] = f2bf(a_fd * sf);
-        dr[2 * H] = f2bf(a_gd * sg);
-        dr[3 * H] = f2bf(a_od * so);
-      }
-    }
-    if constexpr (DX) {
-      ndh.load(rdh, Tn, t - 1, pv, ltid);
-      ndhd.load(rdhd, Tn, t - 1, pv, ltid);
-    }
-    if (pv) {
-      ndh.to_lds(dhb + nb * 32 * LH, LH, ltid);
-      ndhd.to_lds(dhdb + nb * 32 * LH, LH, ltid);
-      cc = cp;
-      cdc = cdp;
-    }
-    lds_barrier();  // step hand-off: LDS only, stores stay in flight
-  }
-  tile16_store<G>(zb, LG, rz, Tn, 0, true, ltid);
-  tile16_store<G>(zdb, LG, rzd, Tn, 0, true, ltid);
-  if constexpr (DX) {
-    f32x16 ax = zero16(), axd = zero16();
-    if (xw) {
-      const bf16_t* arow = zb + (lane & 31) * LG;
-      const bf16_t* drow = zdb + (lane & 31) * LG;
-#pragma unroll
-      for (int ks = 0; ks < NKG; ++ks) {
-        ax = P::mma(P::lda(arow, ks, lane), wt[ks], ax);
-        axd = P::mma(P::lda(drow, ks, lane), wt[ks], axd);
-      }
-    }
-    store_dx(ax, rdx, Tn, 0, xw, nr, K, kc, lane);
-    store_dx(axd, rdxd, Tn, 0, xw, nr, K, kc, lane);
-  }
-  __syncthreads();
   }
 }
 
@@ -1825,17 +1382,13 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 // ==========================================================================================
 size_t lstm2_tape_elems(int B, int Tn) { return (size_t)((B + 31) / 32) * Tn * NW2 * TAPE_SLOTS * SLOT_ELEMS; }
 
-static size_t fwd_smem(int H, int K, int tiles) {
+static size_t tfwd2_smem(int H, int K) {
   const int KP = (K + 15) & ~15, LX = KP + 8, LH = ((H + 15) / 16) * 16 + 8;
-  return (size_t)(4 * H * LX + tiles * (2 * 32 * LX + 2 * 32 * LH)) * 2;
+  return (size_t)(4 * H * LX + 2 * 32 * LX + 2 * 32 * LH) * 2;
 }
-static size_t bwd_smem(int H, int tiles) {
+static size_t bwd_smem(int H) {
   const int LG = ((4 * H + 15) / 16) * 16 + 8, LH = ((H + 15) / 16) * 16 + 8;
-  return (size_t)tiles * (2 * 32 * LG + 2 * 32 * LH) * 2;
-}
-static size_t tbwd_smem(int H) {
-  const int LG = ((4 * H + 15) / 16) * 16 + 8, LH = ((H + 15) / 16) * 16 + 8;
-  return (size_t)(4 * 32 * LG + 4 * 32 * LH) * 2;
+  return (size_t)(2 * 32 * LG + 2 * 32 * LH) * 2;
 }
 constexpr size_t LDS_MAX = 160 * 1024;
 
@@ -1849,14 +1402,18 @@ static void allow_big_lds(const void* kernel) {
 }
 
 // persistent grid: one workgroup per CU (the kernels run at one or two waves per SIMD), each looping
-// over groups of `tiles` row blocks so the W^T staging and the register-resident U fragments are
-// paid once per CU
-static int persistent_grid(int B, int tiles) {
-  const int ngrp = ((B + 31) / 32 + tiles - 1) / tiles, cus = device_cu_count();
-  return ngrp < cus ? ngrp : cus;
+// over row blocks so the weight fragments are loaded once per CU
+static int persistent_grid(int B) {
+  const int nrb = (B + 31) / 32, cus = device_cu_count();
+  return nrb < cus ? nrb : cus;
 }
 
-bool lstm2_supported(int H, int K) { return H == 100 && K >= 1 && K <= 128 && fwd_smem(H, K, 1) <= LDS_MAX; }
+static size_t fwd4_smem(int H, int K, bool tape) {  // generous: the 32-rounded extents (>= the tail-split ones)
+  const int LX = ((K + 31) & ~31) + 8, LH = ((H + 31) / 32) * 32 + 8;
+  return (size_t)(2 * 32 * LX + 2 * 32 * LH + (tape ? 2 * FW4_STAGE : 0) + 8) * 2;  // + trash
+}
+
+bool lstm2_supported(int H, int K) { return H == 100 && K >= 1 && K <= 128 && fwd4_smem(H, K, true) <= LDS_MAX; }
 
 template <typename Kern, typename... Args>
 static void launch(Kern k, int grid, int threads, size_t smem, hipStream_t s, Args... args) {
@@ -1864,20 +1421,9 @@ static void launch(Kern k, int grid, int threads, size_t smem, hipStream_t s, Ar
   hipLaunchKernelGGL(k, dim3(grid), dim3(threads), smem, s, args...);
 }
 
-// act (0 linear, 1 sigmoid, 2 tanh) and the input width K are template parameters: the cell
-// activation switch and the x-tile index arithmetic would otherwise sit in the hottest loop.
-// K in {32, 100} (the model's widths) get two 32-row tiles per workgroup (8 waves, W^T shared).
-#define HFREP_FWD_LAUNCH(KERNEL, KXV, TL, ...)                                                  \
-  switch (act) {                                                                                 \
-    case 0: launch(KERNEL<100, 0, KXV, TL>, __VA_ARGS__); break;                                 \
-    case 1: launch(KERNEL<100, 1, KXV, TL>, __VA_ARGS__); break;                                 \
-    default: launch(KERNEL<100, 2, KXV, TL>, __VA_ARGS__); break;                                \
-  }
-
-// row tiles per workgroup for the fwd / bwd kernels (HFREP_LSTM_TILES=1 or 2, default 2)
-// timing-only ablation mask for the forward kernel (HFREP_LSTM_DBG; 0 in every real run):
-// 1 no tape store, 2 no h store, 4 no x load, 8 no MFMA, 16 no h LDS write, 32 no step barrier
-// (v4 forward: 1, 2, 4 and 256 = every step's tape stores to step 0's slots, i.e. L2-resident)
+// timing-only ablation mask of the forward kernel (HFREP_LSTM_DBG; 0 in every real run):
+// 1 no tape store, 2 no h store, 4 no x load, 256 every step's tape stores to step 0's slots
+// (L2-resident); 128 selects the BPTT phase-timer build
 static int lstm_dbg() {
   static int d = -1;
   if (d < 0) {
@@ -1887,27 +1433,8 @@ static int lstm_dbg() {
   return d;
 }
 
-static int lstm_tiles() {
-  static int t = 0;
-  if (!t) {
-    const char* e = getenv("HFREP_LSTM_TILES");
-    t = (e && atoi(e) == 1) ? 1 : 2;
-  }
-  return t;
-}
-
-static int lstm_fwd_version() {  // HFREP_LSTM_FWD=2: the v2 forward / tangent forward (A/B only)
-  static int v = 0;
-  if (!v) {
-    const char* e = getenv("HFREP_LSTM_FWD");
-    v = (e && atoi(e) == 2) ? 2 : 4;
-  }
-  return v;
-}
-static size_t fwd4_smem(int H, int K, bool tape) {  // generous: the 32-rounded extents (>= the tail-split ones)
-  const int LX = ((K + 31) & ~31) + 8, LH = ((H + 31) / 32) * 32 + 8;
-  return (size_t)(2 * 32 * LX + 2 * 32 * LH + (tape ? 2 * FW4_STAGE : 0) + 8) * 2;  // + trash
-}
+// act (0 linear, 1 sigmoid, 2 tanh) and the input width K are template parameters: the cell
+// activation switch and the x-tile index arithmetic would otherwise sit in the hottest loop.
 #define HFREP_FWD4_ACT(KXV, TP, TN, ...)                                                          \
   switch (act) {                                                                                 \
     case 0: launch(lstm_fwd4_kernel<100, 0, KXV, TP, TN>, __VA_ARGS__); break;                   \
@@ -1926,55 +1453,37 @@ static size_t fwd4_smem(int H, int K, bool tape) {  // generous: the 32-rounded 
 void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float* U, void* hs, void* tape, int B, int Tn,
                       int K, int H, int act, hipStream_t s) {
   const bf16_t* xp = (const bf16_t*)x;
-  if (lstm_fwd_version() == 4 && !(lstm_dbg() & 64)) {
-    const int g = persistent_grid(B, 1);
-    const size_t sm = fwd4_smem(H, K, tape != nullptr);
-    if (tape)
-      HFREP_FWD4_K(true, false, g, 512, sm, s, xp, W, b, U, (const bf16_t*)nullptr, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
-    else
-      HFREP_FWD4_K(false, false, g, 512, sm, s, xp, W, b, U, (const bf16_t*)nullptr, (bf16_t*)hs, (bf16_t*)nullptr, B,
-                   Tn, K, lstm_dbg())
-    return;
-  }
-  if (K == 100 && (lstm_dbg() & 64) && act == 2) {  // diagnostic phase-timer build
-    launch(lstm_fwd2_kernel<100, 2, 100, 2, true>, persistent_grid(B, 2), 512, fwd_smem(H, K, 2), s, xp, W, b, U,
-           (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg() & ~64);
-    return;
-  }
-  if ((K == 32 || K == 100) && lstm_tiles() == 2 && fwd_smem(H, K, 2) <= LDS_MAX) {
-    const int g = persistent_grid(B, 2);
-    const size_t sm = fwd_smem(H, K, 2);
-    if (K == 32) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 32, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
-    else HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 100, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
-  } else if ((K == 35 || K == 36) && lstm_tiles() == 2) {  // reference (F=35) / production (F=36) panels
-    const int g = persistent_grid(B, 2);
-    const size_t sm = fwd_smem(H, K, 2);
-    if (K == 35) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 35, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
-    else HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 36, 2, g, 512, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
-  } else {
-    const int g = persistent_grid(B, 1);
-    const size_t sm = fwd_smem(H, K, 1);
-    if (K == 32) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 32, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
-    else if (K == 100) HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 100, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
-    else HFREP_FWD_LAUNCH(lstm_fwd2_kernel, 0, 1, g, 256, sm, s, xp, W, b, U, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
-  }
+  const int g = persistent_grid(B);
+  const size_t sm = fwd4_smem(H, K, tape != nullptr);
+  if (tape)
+    HFREP_FWD4_K(true, false, g, 512, sm, s, xp, W, b, U, (const bf16_t*)nullptr, (bf16_t*)hs, (bf16_t*)tape, B, Tn, K, lstm_dbg())
+  else
+    HFREP_FWD4_K(false, false, g, 512, sm, s, xp, W, b, U, (const bf16_t*)nullptr, (bf16_t*)hs, (bf16_t*)nullptr, B, Tn, K,
+                 lstm_dbg())
 }
+
+#define HFREP_TFWD2_K(...)                                                                       \
+  switch (K) {                                                                                   \
+    case 32: launch(lstm_tfwd2_kernel<100, 1, 32, 1>, __VA_ARGS__); break;                      \
+    case 35: launch(lstm_tfwd2_kernel<100, 1, 35, 1>, __VA_ARGS__); break;                      \
+    case 36: launch(lstm_tfwd2_kernel<100, 1, 36, 1>, __VA_ARGS__); break;                      \
+    case 100: launch(lstm_tfwd2_kernel<100, 1, 100, 1>, __VA_ARGS__); break;                    \
+    default: launch(lstm_tfwd2_kernel<100, 1, 0, 1>, __VA_ARGS__); break;                       \
+  }
+
 void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const void* tape, void* hds, void* ttape, int B,
                        int Tn, int K, int H, int act, hipStream_t s) {
   const bf16_t* xp = (const bf16_t*)xd;
-  if (lstm_fwd_version() == 4) {
-    const int g = persistent_grid(B, 1);
-    HFREP_FWD4_K(true, true, g, 512, fwd4_smem(H, K, true), s, xp, W, (const float*)nullptr, U, (const bf16_t*)tape,
-                 (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K, lstm_dbg())
+  const int g = persistent_grid(B);
+  if (act == 1) {
+    // act = sigmoid: lstm_fwd4_kernel<.., TAN = true> differs run to run in rows 30 / 31 of a few row
+    // blocks at B = 32772 (profiles/r03_race/README.md); the v2 tangent forward is bitwise there
+    // (tests/test_kernels_gpu.py test_lstm2_tfwd_bitwise_large_batch).  Off the MTSS critic's path (tanh).
+    HFREP_TFWD2_K(g, 256, tfwd2_smem(H, K), s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
     return;
   }
-  const int g = persistent_grid(B, 1);
-  const size_t sm = fwd_smem(H, K, 1);
-  if (K == 32) HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 32, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
-  else if (K == 35) HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 35, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
-  else if (K == 36) HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 36, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
-  else if (K == 100) HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 100, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
-  else HFREP_FWD_LAUNCH(lstm_tfwd2_kernel, 0, 1, g, 256, sm, s, xp, W, U, (const bf16_t*)tape, (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K)
+  HFREP_FWD4_K(true, true, g, 512, fwd4_smem(H, K, true), s, xp, W, (const float*)nullptr, U, (const bf16_t*)tape,
+               (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K, lstm_dbg())
 }
 
 #define HFREP_BWD3_ACT(DXV, GV, ...)                                                           \
@@ -1986,59 +1495,23 @@ void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const voi
 #define HFREP_BWD3_LAUNCH(DXV, ...)                                                            \
   if (hw) HFREP_BWD3_ACT(DXV, true, __VA_ARGS__) else HFREP_BWD3_ACT(DXV, false, __VA_ARGS__)
 
-#define HFREP_BWD_LAUNCH(KERNEL, TL, DXV, ...)                                                  \
-  switch (act) {                                                                                 \
-    case 0: launch(KERNEL<100, 0, TL, DXV>, __VA_ARGS__); break;                                 \
-    case 1: launch(KERNEL<100, 1, TL, DXV>, __VA_ARGS__); break;                                 \
-    default: launch(KERNEL<100, 2, TL, DXV>, __VA_ARGS__); break;                                \
-  }
-
-static int lstm_tbwd_version();
-static int lstm_bwd_version() {  // HFREP_LSTM_BWD=2: the single-role v2 BPTT (A/B only)
-  static int v = 0;
-  if (!v) {
-    const char* e = getenv("HFREP_LSTM_BWD");
-    v = (e && atoi(e) == 2) ? 2 : 3;
-  }
-  return v;
-}
-
-bool lstm2_head_fusion() { return lstm_bwd_version() == 3 && lstm_tbwd_version() == 4; }
-
 void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, const float* W, void* dX, int K,
                       int B, int Tn, int H, int act, hipStream_t s, const void* head_d, const float* hw) {
   const bf16_t* dh = (const bf16_t*)dH;
   const bf16_t* tp = (const bf16_t*)tape;
   const bf16_t* hd = (const bf16_t*)head_d;
-  if (lstm_bwd_version() == 3) {
-    const int g = persistent_grid(B, 1);
-    const size_t sm = bwd_smem(H, 1);
-    if (dX && act == 2 && !hw && (lstm_dbg() & 128)) {  // diagnostic phase-timer build
-      launch(lstm_bwd3_kernel<100, 2, true, false, true>, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn,
-             K, hd, hw);
-      return;
-    }
-    if (dX)
-      HFREP_BWD3_LAUNCH(true, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn, K, hd, hw)
-    else
-      HFREP_BWD3_LAUNCH(false, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, (const float*)nullptr, (bf16_t*)nullptr, B, Tn, 0,
-                        hd, hw)
+  const int g = persistent_grid(B);
+  const size_t sm = bwd_smem(H);
+  if (dX && act == 2 && !hw && (lstm_dbg() & 128)) {  // diagnostic phase-timer build
+    launch(lstm_bwd3_kernel<100, 2, true, false, true>, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn,
+           K, hd, hw);
     return;
   }
-  if (dX)  // fused input gradient: U^T and W^T fragments in registers -> one row tile per workgroup
-    HFREP_BWD_LAUNCH(lstm_bwd2_kernel, 1, true, persistent_grid(B, 1), 256, bwd_smem(H, 1), s, dh, tp, U, (bf16_t*)dZ,
-                     W, (bf16_t*)dX, B, Tn, K, lstm_dbg())
-  else  // (two row tiles per workgroup spill the U^T fragments at 256 VGPRs: measured slower)
-    HFREP_BWD_LAUNCH(lstm_bwd2_kernel, 1, false, persistent_grid(B, 1), 256, bwd_smem(H, 1), s, dh, tp, U, (bf16_t*)dZ,
-                     (const float*)nullptr, (bf16_t*)nullptr, B, Tn, 0, lstm_dbg())
-}
-static int lstm_tbwd_version() {  // HFREP_LSTM_TBWD=2: the v2 tangent reverse (A/B only)
-  static int v = 0;
-  if (!v) {
-    const char* e = getenv("HFREP_LSTM_TBWD");
-    v = (e && atoi(e) == 2) ? 2 : 4;
-  }
-  return v;
+  if (dX)
+    HFREP_BWD3_LAUNCH(true, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn, K, hd, hw)
+  else
+    HFREP_BWD3_LAUNCH(false, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, (const float*)nullptr, (bf16_t*)nullptr, B, Tn, 0,
+                      hd, hw)
 }
 
 #define HFREP_TBWD4_ACT(DXV, GV, ...)                                                          \
@@ -2055,29 +1528,18 @@ void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const 
                        hipStream_t s, const void* head_d, const void* head_dd, const float* hw) {
   const bf16_t* hd = (const bf16_t*)head_d;
   const bf16_t* hdd = (const bf16_t*)head_dd;
-  if (lstm_tbwd_version() == 4) {
-    const int g = persistent_grid(B, 1);
-    const size_t sm = Tb4Geo<100>::smem;
-    if (dX) {
-      // (DX + GEN -- generated head adjoint with the fused input gradient -- was parked in r01-r02 for
-      // run-to-run drift: the cross-opcode MFMA SrcC hazard, fixed by xdl_switch; profiles/r03_race)
-      HFREP_TBWD4_LAUNCH(true, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
-                         (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, W, (bf16_t*)dX, (bf16_t*)dXd, B, Tn, K, hd,
-                         hdd, hw)
-    } else
-      HFREP_TBWD4_LAUNCH(false, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
-                         (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, (const float*)nullptr, (bf16_t*)nullptr,
-                         (bf16_t*)nullptr, B, Tn, 0, hd, hdd, hw)
-    return;
-  }
+  const int g = persistent_grid(B);
+  const size_t sm = Tb4Geo<100>::smem;
+  // (DX + GEN -- generated head adjoint with the fused input gradient -- was parked in r01-r02 for
+  // run-to-run drift: the cross-opcode MFMA SrcC hazard, fixed by xdl_switch; profiles/r03_race)
   if (dX)
-    HFREP_BWD_LAUNCH(lstm_tbwd2_kernel, 1, true, persistent_grid(B, 1), 256, tbwd_smem(H), s, (const bf16_t*)dH,
-                     (const bf16_t*)dHd, (const bf16_t*)tape, (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, W,
-                     (bf16_t*)dX, (bf16_t*)dXd, B, Tn, K)
+    HFREP_TBWD4_LAUNCH(true, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
+                       (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, W, (bf16_t*)dX, (bf16_t*)dXd, B, Tn, K, hd,
+                       hdd, hw)
   else
-    HFREP_BWD_LAUNCH(lstm_tbwd2_kernel, 1, false, persistent_grid(B, 1), 256, tbwd_smem(H), s, (const bf16_t*)dH,
-                     (const bf16_t*)dHd, (const bf16_t*)tape, (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd,
-                     (const float*)nullptr, (bf16_t*)nullptr, (bf16_t*)nullptr, B, Tn, 0)
+    HFREP_TBWD4_LAUNCH(false, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
+                       (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, (const float*)nullptr, (bf16_t*)nullptr,
+                       (bf16_t*)nullptr, B, Tn, 0, hd, hdd, hw)
 }
 
 void lstm2_read_stamps(uint64_t* out, int n) {

@@ -416,6 +416,15 @@ __device__ __forceinline__ void bwdf_tape_load(f32x4& tg, float& tcp, float& tdh
   tcp = ld1(rt, (tok && prev) ? ocp : kOOB, 0);
   tdh = ld1(rdh, tok ? p1 : kOOB, 0);
 }
+// the same loads with the per-lane part of each offset in voffset (tl / tcl / vp) and the uniform part
+// (step and slot) in soffset: no per-cell offset arithmetic on the VALU (the split BPTT is VALU-bound,
+// profiles/r03_end/pmc_fp32.txt).  Out-of-range lanes: voffset kOOB (the range check is on voffset)
+__device__ __forceinline__ void bwdf_tape_load_u(f32x4& tg, float& tcp, float& tdh, rsrc_t rt, rsrc_t rdh, int tl, int tcl,
+                                                 int vp, int sg, int sc, int sd, bool tok, bool prev) {
+  tg = ld4s(rt, tok ? tl : kOOB, sg);
+  tcp = ld1(rt, (tok && prev) ? tcl : kOOB, sc);
+  tdh = ld1(rdh, tok ? vp : kOOB, sd);
+}
 // the dz tile (32 rows x [q][u'], u' < 100) -> dZ[:, t, :] (row-major, 4H per row) in 16-byte chunks:
 // threads 0..199 own chunk (tid % 100) of rows 2 k + tid / 100 (k < 16); the row step lives in the
 // uniform soffset, so a thread holds one LDS and one global base (rows past B: voffset out of range)
@@ -448,127 +457,11 @@ __device__ __forceinline__ void bwdf_store16(const float* zt, rsrc_t rz, int Tn,
   }
 }
 
-template <int ACT>
-__global__ void __launch_bounds__(256, 1)
-lstmf_bwd_kernel(const float* __restrict__ dH, const float* __restrict__ tape, const float* __restrict__ U,
-                 float* __restrict__ dZ, int B, int Tn) {
-  extern __shared__ __attribute__((aligned(16))) float fsm[];
-  float* zt = fsm;                  // dz_{t+1} tile [32][BZ_LR]: [q][u'] per row
-  float* ht = zt + 32 * BZ_LR;      // dh_rec tile [32][BH_LR]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int q = lane & 3, g = lane >> 4, j4 = (lane & 15) >> 2, c16 = lane & 15;
-  const int ub = FUW * w + j4;
-  const int nrb = (B + 31) / 32;
-  // U^T fragments: B[k = 4 u' + g][col c16 of output tile nt] = U[16 nt + c16][g H + u']
-  float ut[2][FH];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int j = 16 * (2 * w + e) + c16;
-    const bool ok = j < FH;
-#pragma unroll
-    for (int k = 0; k < FH; ++k) {
-      const float v = U[(ok ? j : 0) * FG + g * FH + k];
-      ut[e][k] = ok ? v : 0.f;
-      asm volatile("" : "+a"(ut[e][k]));
-    }
-  }
-  const int hr = (4 * g + q) * BH_LR + ub, zw = (4 * g + q) * BZ_LR + ub;  // (+16 m rows, + 4 n units)
-  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
-    const int row0 = rb * 32;
-    const rsrc_t rdh = ftile_rsrc(dH, row0, B, Tn, FH), rt = ftape_rsrc(tape, rb, nrb, Tn);
-    const rsrc_t rz = ftile_rsrc(dZ, row0, B, Tn, FG);
-    const int nr = min(32, B - row0);
-    BwdfStore st;
-    st.set(tid, Tn);
-    int vp1[2];
-#pragma unroll
-    for (int m = 0; m < 2; ++m) vp1[m] = ((16 * m + 4 * g + q) * Tn * FH + ub) * 4;
-    const int tl = ftape_lane(w, lane), tcl = ftape_cell(w, lane);
-    float dc[2][FNT], tc[2][FNT];
-    f32x4 tg[2][FNT];
-    float tcp[2][FNT], tdh[2][FNT];
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < FNT; ++n) {
-        const bool tok = !(w == 3 && n >= 4);
-        const int T1 = Tn - 1;
-        dc[m][n] = 0.f;
-        tc[m][n] = ld1(rt, tok ? tcl + T1 * FT_STEP * 4 + ftape_slot(m, n) : kOOB, 0);  // c_{T-1}
-        bwdf_tape_load(tg[m][n], tcp[m][n], tdh[m][n], rt, rdh, tl + T1 * FT_STEP * 4 + ftape_slot(m, n),
-                       tcl + (T1 - 1) * FT_STEP * 4 + ftape_slot(m, n), vp1[m] + T1 * FH * 4 + 16 * n, tok, T1 > 0);
-      }
-    for (int i = tid; i < 32 * BZ_LR; i += 256) zt[i] = 0.f;  // dz_T = 0
-    __syncthreads();
-    for (int t = Tn - 1; t >= 0; --t) {
-      // ---- phase A: dZ_{t+1} out of the tile; dh_rec = dz_{t+1} U^T ----
-      if (t < Tn - 1) st.store(zt, rz, Tn, t + 1, nr);
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-        const float* ar = zt + (16 * m + c16) * BZ_LR + g * BZ_KQ;
-#pragma unroll
-        for (int jj = 0; jj < FH / 4; ++jj) {
-          const f32x4 a4 = *reinterpret_cast<const f32x4*>(ar + 4 * jj);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            acc[0] = mma4(a4[s], ut[0][4 * jj + s], acc[0]);
-            acc[1] = mma4(a4[s], ut[1][4 * jj + s], acc[1]);
-          }
-          if ((jj & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int col = 16 * (2 * w + e) + c16;
-          if (2 * w + e < 7) {  // (wave 3's second tile is past the 112-unit tile: uniform skip)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ht[(16 * m + 4 * g + i) * BH_LR + col] = acc[e][i];
-          }
-        }
-      }
-      lds_barrier();
-      // ---- phase B: cell adjoints -> dz_t tile; then step t-1's tape loads ----
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {
-#pragma unroll
-        for (int n = 0; n < FNT; ++n) {
-          const bool tok = !(w == 3 && n >= 4);
-          const float ig = tg[m][n][0], fg = tg[m][n][1], gg = tg[m][n][2], og = tg[m][n][3];
-          const float dht = tdh[m][n] + ht[hr + 16 * m * BH_LR + 4 * n];
-          const float ca = act_f(ACT, tc[m][n]);
-          const float dov = dht * ca;
-          const float dct = dc[m][n] + dht * og * act_dy(ACT, ca);
-          dc[m][n] = tok ? dct * fg : 0.f;
-          float z4[4];
-          z4[0] = dct * gg * ig * (1.f - ig);
-          z4[1] = dct * tcp[m][n] * fg * (1.f - fg);
-          z4[2] = dct * ig * act_dy(ACT, gg);
-          z4[3] = dov * og * (1.f - og);
-          if (tok) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) zt[zw + 16 * m * BZ_LR + k * BZ_KQ + 4 * n] = z4[k];
-          }
-          tc[m][n] = tcp[m][n];  // c_{t-1} is the next step's c
-          const int tp = t > 0 ? t - 1 : 0;
-          bwdf_tape_load(tg[m][n], tcp[m][n], tdh[m][n], rt, rdh, tl + tp * FT_STEP * 4 + ftape_slot(m, n),
-                         tcl + (tp - 1) * FT_STEP * 4 + ftape_slot(m, n), vp1[m] + tp * FH * 4 + 16 * n, tok && t > 0,
-                         tp > 0);
-          __builtin_amdgcn_sched_barrier(0);  // consume-then-reload per cell: one register set
-        }
-      }
-      lds_barrier();
-    }
-    st.store(zt, rz, Tn, 0, nr);
-    __syncthreads();  // (the tile is re-zeroed for the next row block)
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // BPTT with a role split and a row-half pipeline (8 waves, two per SIMD).
 //
-// lstmf_bwd_kernel runs the step's MFMA phase (dh_rec = dz_{t+1} U^T) and its VALU phase (the cell
-// adjoints) back to back in the same four waves, so the matrix pipe idles through every VALU phase:
+// A BPTT that runs the step's MFMA phase (dh_rec = dz_{t+1} U^T) and its VALU phase (the cell
+// adjoints) back to back in the same four waves leaves the matrix pipe idle through every VALU phase:
 // 400 MFMAs = 12.8 k cycles of pipe time per wave and step against ~24 k measured.  A single wave
 // cannot overlap them (in-order issue; the scheduler keeps the cell math in clumps between MFMA
 // runs), so here the roles go to different waves that share a SIMD:
@@ -738,165 +631,6 @@ lstmf_bwdp_kernel(const float* __restrict__ dH, const float* __restrict__ tape, 
 // tangent reverse (fp32): (dZ, dZdot) of the reverse-over-tangent pass (ops/reference.py
 // lstm_seq_tbwd) from the primal and tangent tapes of lstmf_fwd<TAPE> / lstmf_fwd<TAN>
 // ==========================================================================================
-// The BPTT's two-phase step with two adjoint streams: phase A runs dz_{t+1} U^T and dzdot_{t+1} U^T
-// (800 MFMAs per wave) from two dz tiles, phase B the second-order cell adjoints per (row, unit).
-// dZ / dZdot leave through the tiles' coalesced row-major stores during the next phase A.
-// Register budget: a cell carries 16 values here (c, cdot, two adjoint carries, the gate and zdot
-// quads, c_{t-1}, cdot_{t-1}, dH, dHd), so the kernel walks 16-ROW tiles (one accumulator half of a
-// 32-row tape block: 7 cells per lane) to stay inside the register file without spills.
-template <int ACT>
-__global__ void __launch_bounds__(256, 1)
-lstmf_tbwd_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, const float* __restrict__ tape,
-                  const float* __restrict__ ttape, const float* __restrict__ U, float* __restrict__ dZ,
-                  float* __restrict__ dZd, int B, int Tn) {
-  extern __shared__ __attribute__((aligned(16))) float fsm[];
-  float* zt = fsm;                 // dz_{t+1}      [16][BZ_LR]
-  float* zdt = zt + 16 * BZ_LR;    // dzdot_{t+1}
-  float* ht = zdt + 16 * BZ_LR;    // dz_{t+1} U^T  [16][BH_LR]
-  float* hdt = ht + 16 * BH_LR;    // dzdot_{t+1} U^T
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int q = lane & 3, g = lane >> 4, j4 = (lane & 15) >> 2, c16 = lane & 15;
-  const int ub = FUW * w + j4;
-  const int nrb32 = (B + 31) / 32, nt16 = (B + 15) / 16;
-  float ut[2][FH];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int j = 16 * (2 * w + e) + c16;
-    const bool ok = j < FH;
-#pragma unroll
-    for (int k = 0; k < FH; ++k) {
-      const float v = U[(ok ? j : 0) * FG + g * FH + k];
-      ut[e][k] = ok ? v : 0.f;
-      asm volatile("" : "+a"(ut[e][k]));
-    }
-  }
-  const int hr = (4 * g + q) * BH_LR + ub, zw = (4 * g + q) * BZ_LR + ub;
-  for (int tb16 = blockIdx.x; tb16 < nt16; tb16 += gridDim.x) {
-    const int row0 = tb16 * 16, mh = tb16 & 1;  // tape block tb16 / 2, accumulator half mh
-    const int nr = min(16, B - row0);
-    const rsrc_t rdh = make_rsrc(dH ? dH + (size_t)row0 * Tn * FH : nullptr, dH ? nr * Tn * FH * 4 : 0);
-    const rsrc_t rdhd = make_rsrc(dHd ? dHd + (size_t)row0 * Tn * FH : nullptr, dHd ? nr * Tn * FH * 4 : 0);
-    const rsrc_t rt = ftape_rsrc(tape, tb16 >> 1, nrb32, Tn), rtt = ftape_rsrc(ttape, tb16 >> 1, nrb32, Tn);
-    const rsrc_t rz = make_rsrc(dZ + (size_t)row0 * Tn * FG, nr * Tn * FG * 4);
-    const rsrc_t rzd = make_rsrc(dZd + (size_t)row0 * Tn * FG, nr * Tn * FG * 4);
-    const int vp1 = ((4 * g + q) * Tn * FH + ub) * 4;
-    const int tl = ftape_lane(w, lane) + mh * FNT * FT_SLOT * 4, tcl = ftape_cell(w, lane) + mh * FNT * FT_SLOT * 4;
-    // per cell: carried c_t, cdot_t, c-bar, cdot-bar; step loads: gates, zdot (t), c_{t-1},
-    // cdot_{t-1}, dH, dHd (t)
-    float tc[FNT], tcd[FNT], acn[FNT], acdn[FNT];
-    f32x4 tg[FNT], tz[FNT];
-    float tcp[FNT], tcdp[FNT], tdh[FNT], tdhd[FNT];
-    auto load_step = [&](int n, int tt, bool on) {
-      const bool tok = on && !(w == 3 && n >= 4);
-      const int og = tl + tt * FT_STEP * 4 + ftape_slot(0, n), ocp = tcl + (tt - 1) * FT_STEP * 4 + ftape_slot(0, n);
-      tg[n] = ld4(rt, tok ? og : kOOB);
-      tz[n] = ld4(rtt, tok ? og : kOOB);
-      tcp[n] = ld1(rt, (tok && tt > 0) ? ocp : kOOB, 0);
-      tcdp[n] = ld1(rtt, (tok && tt > 0) ? ocp : kOOB, 0);
-      tdh[n] = ld1(rdh, tok ? vp1 + tt * FH * 4 + 16 * n : kOOB, 0);
-      tdhd[n] = ld1(rdhd, tok ? vp1 + tt * FH * 4 + 16 * n : kOOB, 0);
-    };
-#pragma unroll
-    for (int n = 0; n < FNT; ++n) {
-      const bool tok = !(w == 3 && n >= 4);
-      const int oc = tcl + (Tn - 1) * FT_STEP * 4 + ftape_slot(0, n);
-      acn[n] = 0.f;
-      acdn[n] = 0.f;
-      tc[n] = ld1(rt, tok ? oc : kOOB, 0);
-      tcd[n] = ld1(rtt, tok ? oc : kOOB, 0);
-      load_step(n, Tn - 1, true);
-    }
-    for (int i = tid; i < 2 * 16 * BZ_LR; i += 256) zt[i] = 0.f;  // dz_T = dzdot_T = 0
-    __syncthreads();
-    for (int t = Tn - 1; t >= 0; --t) {
-      // ---- phase A ----
-      if (t < Tn - 1) {
-        bwdf_store16(zt, rz, Tn, t + 1, nr, tid);
-        bwdf_store16(zdt, rzd, Tn, t + 1, nr, tid);
-      }
-      {
-        f32x4 acc[2][2];
-#pragma unroll
-        for (int a = 0; a < 2; ++a) acc[a][0] = acc[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const float* ar = zt + c16 * BZ_LR + g * BZ_KQ;
-        const float* adr = zdt + c16 * BZ_LR + g * BZ_KQ;
-#pragma unroll
-        for (int jj = 0; jj < FH / 4; ++jj) {
-          const f32x4 a4 = *reinterpret_cast<const f32x4*>(ar + 4 * jj);
-          const f32x4 d4 = *reinterpret_cast<const f32x4*>(adr + 4 * jj);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            acc[0][0] = mma4(a4[s], ut[0][4 * jj + s], acc[0][0]);
-            acc[0][1] = mma4(a4[s], ut[1][4 * jj + s], acc[0][1]);
-            acc[1][0] = mma4(d4[s], ut[0][4 * jj + s], acc[1][0]);
-            acc[1][1] = mma4(d4[s], ut[1][4 * jj + s], acc[1][1]);
-          }
-          if ((jj & 1) == 1) __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int col = 16 * (2 * w + e) + c16;
-          if (2 * w + e < 7) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              ht[(4 * g + i) * BH_LR + col] = acc[0][e][i];
-              hdt[(4 * g + i) * BH_LR + col] = acc[1][e][i];
-            }
-          }
-        }
-      }
-      lds_barrier();
-      // ---- phase B ----
-#pragma unroll
-      for (int n = 0; n < FNT; ++n) {
-        const bool tok = !(w == 3 && n >= 4);
-        const float i_ = tg[n][0], f_ = tg[n][1], g_ = tg[n][2], o_ = tg[n][3];
-        const float zdi = tz[n][0], zdf = tz[n][1], zdg = tz[n][2], zdo = tz[n][3];
-        const float c = tc[n], cd = tcd[n], cp = tcp[n], cdp = tcdp[n];
-        const float si = i_ * (1.f - i_), sf = f_ * (1.f - f_), so = o_ * (1.f - o_), sg = act_dy(ACT, g_);
-        const float idot = si * zdi, fdot = sf * zdf, gdot = sg * zdg, odot = so * zdo;
-        const float ca = act_f(ACT, c), d1 = act_dy(ACT, ca), d2 = act_d2y(ACT, ca);
-        const int hi = hr + 4 * n;
-        const float a_h = tdh[n] + ht[hi], a_hd = tdhd[n] + hdt[hi];
-        const float a_od = a_hd * ca;
-        const float a_o = a_h * ca + a_hd * d1 * cd;
-        const float a_cd = acdn[n] + a_hd * o_ * d1;
-        const float a_c = acn[n] + a_h * o_ * d1 + a_hd * (odot * d1 + o_ * d2 * cd);
-        const float a_fd = a_cd * cp, a_id = a_cd * g_, a_gd = a_cd * i_;
-        const float a_f = a_c * cp + a_cd * cdp;
-        const float a_i = a_c * g_ + a_cd * gdot;
-        const float a_g = a_c * i_ + a_cd * idot;
-        acn[n] = tok ? a_c * f_ + a_cd * fdot : 0.f;
-        acdn[n] = tok ? a_cd * f_ : 0.f;
-        const float s2i = si * (1.f - 2.f * i_), s2f = sf * (1.f - 2.f * f_), s2o = so * (1.f - 2.f * o_);
-        const float s2g = act_d2y(ACT, g_);
-        float zd4[4], z4[4];
-        zd4[0] = a_id * si; zd4[1] = a_fd * sf; zd4[2] = a_gd * sg; zd4[3] = a_od * so;
-        z4[0] = a_i * si + a_id * s2i * zdi;
-        z4[1] = a_f * sf + a_fd * s2f * zdf;
-        z4[2] = a_g * sg + a_gd * s2g * zdg;
-        z4[3] = a_o * so + a_od * s2o * zdo;
-        if (tok) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            zt[zw + k * BZ_KQ + 4 * n] = z4[k];
-            zdt[zw + k * BZ_KQ + 4 * n] = zd4[k];
-          }
-        }
-        tc[n] = cp;
-        tcd[n] = cdp;
-        load_step(n, t > 0 ? t - 1 : 0, t > 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      lds_barrier();
-    }
-    bwdf_store16(zt, rz, Tn, 0, nr, tid);
-    bwdf_store16(zdt, rzd, Tn, 0, nr, tid);
-    __syncthreads();
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // tangent reverse with the role split of lstmf_bwdp_kernel: 32-row tiles whose 16-row halves are
 // pipelined (P1(t): cells of rows 0-15 || MFMAs of rows 16-31; P2(t): cells of rows 16-31 ||
@@ -1849,117 +1583,7 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// fp32 input gradient on the bf16 matrix pipe: dX = dZ W^T with the exact three-term split
-// ------------------------------------------------------------------------------------------
-// Same split as lstmf_wgrad_split_kernel (a = h + m + l by truncation, six products
-// lh + hl + mm + mh + hm + hh on v_mfma_f32_16x16x32_bf16, dropped terms <= 2^-24 of each product).
-// The reduction (k = 400 gate columns) is 13 k-steps of 32 (k 400..415 zero); 8 waves, wave w owns
-// k-steps w and w + 8 (waves 5..7 only w), so its W^T fragments -- all three planes, every output
-// tile: 2 x NT x 3 x 4 VGPRs -- stay in registers for the whole kernel.  Per 16-row tile every lane
-// loads its 8 contiguous dZ values per k-step straight from HBM (one tile ahead) and splits them in
-// registers; the waves' partial tiles meet in LDS (double-buffered, one barrier per tile) and are
-// summed in fixed wave order.  Each partial is at most 12 MFMAs from zero, so the MFMA's own C
-// accumulation is used (no long-running sum here).  Straight-line MFMA -> LDS-store code per wave
-// kind (two k-steps or one): no branch between an MFMA and the read of its result.
-constexpr int DS_KS = 13;
-template <int NT, int NKS>
-__device__ __forceinline__ void dgs_tile(f32x4* part, const bf16x8 (&bw)[2][NT][3], const f32x4 (&ra)[2][2],
-                                         int lane) {
-  f32x4 acc[NT];
-#pragma unroll
-  for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < NKS; ++s) {
-    uint32_t p0[3][2], p1[3][2];
-    split3(ra[s][0], p0);
-    split3(ra[s][1], p1);
-    bf16x8 a[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      a[q] = __builtin_bit_cast(bf16x8, make_uint4(p0[q][0], p0[q][1], p1[q][0], p1[q][1]));
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      f32x4 t = acc[n];
-      t = mma32(a[2], bw[s][n][0], t);  // lh
-      t = mma32(a[0], bw[s][n][2], t);  // hl
-      t = mma32(a[1], bw[s][n][1], t);  // mm
-      t = mma32(a[1], bw[s][n][0], t);  // mh
-      t = mma32(a[0], bw[s][n][1], t);  // hm
-      acc[n] = mma32(a[0], bw[s][n][0], t);  // hh
-    }
-  }
-#pragma unroll
-  for (int n = 0; n < NT; ++n) part[n * 64 + lane] = acc[n];
-}
-
-template <int NT>
-__global__ void __launch_bounds__(512, 1)
-lstmf_dgrad_split_kernel(const float* __restrict__ D, const float* __restrict__ W, float* __restrict__ X, int M, int KO,
-                         int rows_per_wg) {
-  extern __shared__ __attribute__((aligned(16))) f32x4 dpart[];  // [2][8 waves][NT][64 lanes]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, c16 = lane & 15;
-  const int mb = blockIdx.x * rows_per_wg, nrows = min(M, mb + rows_per_wg) - mb;
-  if (nrows <= 0) return;  // uniform over the workgroup
-  const int nks = w + 8 < DS_KS ? 2 : 1;
-  // W^T fragments (B operand: lane holds k = 32 ks + 8 g .. + 7 of output column 16 n + c16), split
-  bf16x8 bw[2][NT][3];
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int ks = w + 8 * s, col = 16 * n + c16, k0 = 32 * ks + 8 * g;
-      f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
-      if (ks < DS_KS && col < KO && k0 < FG) {
-        v0 = *reinterpret_cast<const f32x4*>(W + (size_t)col * FG + k0);
-        v1 = *reinterpret_cast<const f32x4*>(W + (size_t)col * FG + k0 + 4);
-      }
-      uint32_t p0[3][2], p1[3][2];
-      split3(v0, p0);
-      split3(v1, p1);
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        bw[s][n][q] = __builtin_bit_cast(bf16x8, make_uint4(p0[q][0], p0[q][1], p1[q][0], p1[q][1]));
-    }
-  const rsrc_t rd = make_rsrc(D + (size_t)mb * FG, nrows * FG * 4);
-  const rsrc_t rx = make_rsrc(X + (size_t)mb * KO, nrows * KO * 4);
-  const int nt16 = (nrows + 15) / 16;
-  // this lane's A operand: row r0 + c16, k = 32 ks + 8 g .. + 7 (k >= 400: zeros)
-  auto load = [&](f32x4 (&ra)[2][2], int r0) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ks = w + 8 * s, k0 = 32 * ks + 8 * g;
-      const bool ok = ks < DS_KS && k0 < FG && r0 + c16 < nrows;
-      const int vo = ok ? ((r0 + c16) * FG + k0) * 4 : kOOB;
-      ra[s][0] = ld4(rd, vo);
-      ra[s][1] = ld4(rd, ok ? vo + 16 : kOOB);
-    }
-  };
-  f32x4 ra[2][2][2];
-  load(ra[0], 0);
-  for (int c = 0; c < nt16; ++c) {
-    const int cur = c & 1;
-    if (c + 1 < nt16) load(ra[cur ^ 1], 16 * (c + 1));
-    f32x4* part = dpart + ((cur * 8 + w) * NT) * 64;
-    if (nks == 2)
-      dgs_tile<NT, 2>(part, bw, ra[cur], lane);
-    else
-      dgs_tile<NT, 1>(part, bw, ra[cur], lane);
-    __syncthreads();
-    // fixed-order sum of the 8 waves' partials; thread e owns (n, lane') = (e >> 6, e & 63)
-    const f32x4* pb = dpart + (cur * 8) * NT * 64;
-    for (int e = tid; e < NT * 64; e += 512) {
-      f32x4 v = pb[e];
-#pragma unroll
-      for (int ww = 1; ww < 8; ++ww) v += pb[ww * NT * 64 + e];
-      const int n = e >> 6, ln = e & 63, col = 16 * n + (ln & 15), row = 16 * c + 4 * (ln >> 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) st1(v[i], rx, col < KO && row + i < nrows ? ((row + i) * KO + col) * 4 : kOOB, 0);
-    }
-  }
-}
+constexpr int DS_KS = 13;  // the 400 gate columns as 13 k-steps of 32 (k = 400..415 zero)
 
 // ==========================================================================================
 // forward / tangent forward with the recurrent product on the bf16 pipe (K <= 36 layers)
@@ -2309,8 +1933,8 @@ lstmf_bwds_kernel(const float* __restrict__ dH, const float* __restrict__ tape, 
         dc[m][n] = 0.f;
         tc[m][n] = ld1(rt, tok ? tcl + T1 * FT_STEP * 4 + ftape_slot(m, n) : kOOB, 0);  // c_{T-1}
       }
-      bwdf_tape_load(tg[n], tcp[n], tdh[n], rt, rdh, tl + T1 * FT_STEP * 4 + ftape_slot(0, n),
-                     tcl + (T1 - 1) * FT_STEP * 4 + ftape_slot(0, n), vp1[0] + T1 * FH * 4 + 16 * n, tok, T1 > 0);
+      bwdf_tape_load_u(tg[n], tcp[n], tdh[n], rt, rdh, tl, tcl, vp1[0], T1 * FT_STEP * 4 + ftape_slot(0, n),
+                       max(T1 - 1, 0) * FT_STEP * 4 + ftape_slot(0, n), T1 * FH * 4 + 16 * n, tok, T1 > 0);
     }
     // dz_T = 0 (planes, pad columns k >= 400 included), dh_rec(T - 1) = 0
     for (int i = tid; i < 3 * BS_PL / 16; i += 256)
@@ -2353,13 +1977,12 @@ lstmf_bwds_kernel(const float* __restrict__ dH, const float* __restrict__ tape, 
         *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(pd + pp * ps) = u32x2_t{p[pp][0], p[pp][1]};
       tc[m][n] = tcp[n];  // c_{t-1} is the next step's c
       if constexpr (m == 0) {  // next use: B(1, t)
-        bwdf_tape_load(tg[n], tcp[n], tdh[n], rt, rdh, tl + t * FT_STEP * 4 + ftape_slot(1, n),
-                       tcl + (t - 1) * FT_STEP * 4 + ftape_slot(1, n), vp1[1] + t * FH * 4 + 16 * n, tok, t > 0);
+        bwdf_tape_load_u(tg[n], tcp[n], tdh[n], rt, rdh, tl, tcl, vp1[1], t * FT_STEP * 4 + ftape_slot(1, n),
+                         max(t - 1, 0) * FT_STEP * 4 + ftape_slot(1, n), t * FH * 4 + 16 * n, tok, t > 0);
       } else {  // next use: B(0, t - 1)
         const int tp = t > 0 ? t - 1 : 0;
-        bwdf_tape_load(tg[n], tcp[n], tdh[n], rt, rdh, tl + tp * FT_STEP * 4 + ftape_slot(0, n),
-                       tcl + (tp - 1) * FT_STEP * 4 + ftape_slot(0, n), vp1[0] + tp * FH * 4 + 16 * n, tok && t > 0,
-                       tp > 0);
+        bwdf_tape_load_u(tg[n], tcp[n], tdh[n], rt, rdh, tl, tcl, vp1[0], tp * FT_STEP * 4 + ftape_slot(0, n),
+                         max(tp - 1, 0) * FT_STEP * 4 + ftape_slot(0, n), tp * FH * 4 + 16 * n, tok && t > 0, tp > 0);
       }
     };
     // one half-phase: dz rows of half MA out to HBM, the cells of half 1 - MA at step t, and rows MA of
@@ -2719,13 +2342,21 @@ template <int KX>
 constexpr size_t fwds_smem() {
   return (size_t)(2 * 32 * FGeo<KX>::LR) * 4 + 2 * FS_HB + 16;
 }
-// HFREP_LSTMF_FWD=1: the exact-fp32 forward everywhere (A / B); default: the split-recurrent forward
-// for the K <= 36 layers (lstmf_fwds_kernel)
+// Precision modes of the fp32 path.  Default: the fp32-accurate kernels -- products of the recurrences
+// (K <= 36 forwards, BPTT), both weight gradients and the K = 100 input gradient as the three-term bf16
+// split (each fp32 operand = h + m + l by truncation, six of the nine products on the bf16 MFMA with
+// fp32 accumulation; error <= 2x the exact kernel's vs fp64, tests/test_kernels_gpu.py).
+// HFREP_FP32_EXACT=1: every product on the exact-fp32 MFMA (v_mfma_f32_16x16x4_f32, an fmaf chain).
+static bool fp32_exact() {
+  static const bool v = [] {
+    const char* e = getenv("HFREP_FP32_EXACT");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+// forward: 1 exact, 2 the split-recurrent forward for the K <= 36 layers (lstmf_fwds_kernel)
 static std::atomic<int>& fwdf_impl() {
-  static std::atomic<int> v{[] {
-    const char* e = getenv("HFREP_LSTMF_FWD");
-    return e ? atoi(e) : 2;
-  }()};
+  static std::atomic<int> v{fp32_exact() ? 1 : 2};
   return v;
 }
 static int fwdf_version() { return fwdf_impl().load(std::memory_order_relaxed); }
@@ -2787,13 +2418,9 @@ bool launch_lstmf_tfwd(const float* xd, const float* W, const float* U, const fl
   return fwdf_k<true, true>(K, act, xd, W, nullptr, U, tape, hds, ttape, B, Tn, s);
 }
 
-// HFREP_LSTMF_BWD=1: the unpipelined two-phase kernel; 2: the exact-fp32 role split (A / B
-// comparisons); default 3: the split-recurrent BPTT (lstmf_bwds_kernel)
+// BPTT: 2 the exact-fp32 role split (lstmf_bwdp_kernel), 3 the split-recurrent BPTT (lstmf_bwds_kernel)
 static std::atomic<int>& bwdf_impl() {
-  static std::atomic<int> v{[] {
-    const char* e = getenv("HFREP_LSTMF_BWD");
-    return e ? atoi(e) : 3;
-  }()};
+  static std::atomic<int> v{fp32_exact() ? 2 : 3};
   return v;
 }
 template <int ACT>
@@ -2801,15 +2428,15 @@ void bwdf_launch(const float* dH, const float* tape, const float* U, float* dZ, 
   const int ver = bwdf_impl().load(std::memory_order_relaxed);
   const int nrb = (B + 31) / 32, cus = device_cu_count();
   const size_t sm = (size_t)(32 * BZ_LR + 32 * BH_LR + 4 * BZ_KQ) * 4;
-  if (ver != 1 && ver != 2) {
+  if (ver != 2) {
     auto k = lstmf_bwds_kernel<ACT>;
     allow_lds(reinterpret_cast<const void*>(k));
     hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(256), sm + 16 + 3 * BS_PL, s, dH, tape, U, dZ, B, Tn);
     return;
   }
-  auto k = ver == 1 ? lstmf_bwd_kernel<ACT> : lstmf_bwdp_kernel<ACT>;
+  auto k = lstmf_bwdp_kernel<ACT>;
   allow_lds(reinterpret_cast<const void*>(k));
-  hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(ver == 1 ? 256 : 512), sm, s, dH, tape, U, dZ, B, Tn);
+  hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(512), sm, s, dH, tape, U, dZ, B, Tn);
 }
 static_assert((32 * BZ_LR + 32 * BH_LR + 4 * BZ_KQ) * 4 + 16 + 3 * BS_PL <= F_LDS_MAX, "split BPTT LDS");
 int set_lstmf_bwd_impl(int v) { return bwdf_impl().exchange(v); }
@@ -2827,20 +2454,7 @@ bool launch_lstmf_bwd(const float* dH, const float* tape, const float* U, float*
 template <int ACT>
 void tbwdf_launch(const float* dH, const float* dHd, const float* tape, const float* ttape, const float* U, float* dZ,
                   float* dZd, int B, int Tn, hipStream_t s) {
-  // HFREP_LSTMF_TBWD=1: the 16-row two-phase kernel (A / B comparison); default: role split
-  static const int ver = [] {
-    const char* e = getenv("HFREP_LSTMF_TBWD");
-    return e ? atoi(e) : 2;
-  }();
   const int cus = device_cu_count();
-  if (ver == 1) {
-    auto k = lstmf_tbwd_kernel<ACT>;
-    allow_lds(reinterpret_cast<const void*>(k));
-    const size_t sm = (size_t)(2 * 16 * BZ_LR + 2 * 16 * BH_LR) * 4;
-    const int nt16 = (B + 15) / 16;
-    hipLaunchKernelGGL(k, dim3(nt16 < cus ? nt16 : cus), dim3(256), sm, s, dH, dHd, tape, ttape, U, dZ, dZd, B, Tn);
-    return;
-  }
   auto k = lstmf_tbwdp_kernel<ACT>;
   allow_lds(reinterpret_cast<const void*>(k));
   const size_t sm = (size_t)(2 * 32 * BZ_LR + 2 * 32 * BH_LR + 4 * BZ_KQ) * 4;
@@ -2865,16 +2479,11 @@ static int wgradf_grid(int M) {
 }
 bool lstmf_wgrad_supported(int K, int H, int N) { return H == FH && N == FG && (K == 32 || K == 36 || K == 100); }
 
-// HFREP_LSTMF_WGRAD=1 / 2 / 3: force the exact-fp32 MFMA kernel / the three-term bf16 split (pair) /
-// the split quad; default (0): the pair split for K <= 36 (12.1 -> 9.8 ms at 12.6 M rows), the quad
-// for K = 100 (16.4 -> 15.3 ms; the pair kernel's 28-tile waves spill there: 52.8 ms; profiles/r03_split)
-static int wgradf_version() {
-  static const int v = [] {
-    const char* e = getenv("HFREP_LSTMF_WGRAD");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
+// impl 1 / 2 / 3: the exact-fp32 MFMA kernel / the three-term bf16 split (pair) / the split quad;
+// default (0): exact under HFREP_FP32_EXACT, else the pair split for K <= 36 (12.1 -> 9.8 ms at 12.6 M
+// rows), the quad for K = 100 (16.4 -> 15.3 ms; the pair kernel's 28-tile waves spill there: 52.8 ms;
+// profiles/r03_split)
+static int wgradf_version() { return fp32_exact() ? 1 : 0; }
 // split kernel: Z row ranges x 2 column halves, one workgroup per CU
 static int wgrads_z(int M) {
   const int chunks = (M + 31) / 32, half = device_cu_count() / 2;
@@ -2944,22 +2553,14 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
 
 bool lstmf_dgrad_supported(int N, int KO) { return N == FG && KO >= 1 && KO <= 16 * FNT; }
 
-// HFREP_LSTMF_DGRAD_IMPL=1 / 2 / 3: the exact-fp32 MFMA kernel / the partial-sum split kernel (slower
-// than exact: 5.76 vs 4.69 ms at 6.3 M rows, KO = 100 -- 16-row tiles with a barrier and an 8-wave
-// reduction each do not hide the dZ stream; profiles/r02_split) / the LDS-staged split kernel
-// lstmf_dgrad_s4_kernel; default (0): s4 for KO > 64, exact otherwise (s4 keeps one wave busy per
-// 32 output columns, so KO = 32 leaves three SIMDs idle; profiles/r03_split)
-static int dgradf_version() {
-  static const int v = [] {
-    const char* e = getenv("HFREP_LSTMF_DGRAD_IMPL");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
+// impl 1 / 3: the exact-fp32 MFMA kernel / the LDS-staged split kernel lstmf_dgrad_s4_kernel; default
+// (0): exact under HFREP_FP32_EXACT, else s4 for KO > 64 and exact otherwise (s4 keeps one wave busy
+// per 32 output columns, so KO = 32 leaves three SIMDs idle; profiles/r03_split)
+static int dgradf_version() { return fp32_exact() ? 1 : 0; }
 
 bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl) {
   if (!lstmf_dgrad_supported(N, KO) || M <= 0) return false;
-  const int dv = impl >= 1 && impl <= 3 ? impl : dgradf_version();
+  const int dv = impl == 1 || impl == 3 ? impl : dgradf_version();
   if (dv == 3 || (dv == 0 && KO > 64)) {
     const int chunks = (M + 15) / 16, cus = device_cu_count();
     const int grid = chunks < cus ? chunks : cus;
@@ -2972,28 +2573,6 @@ bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, 
       case 2: go(lstmf_dgrad_s4_kernel<2>); break;
       case 3: go(lstmf_dgrad_s4_kernel<3>); break;
       default: go(lstmf_dgrad_s4_kernel<4>); break;
-    }
-    return true;
-  }
-  if (dv == 2) {
-    const int chunks = (M + 15) / 16, cus = device_cu_count();
-    int grid = chunks < cus ? chunks : cus;
-    const int min_grid = (int)(((long long)M * FG * 4 + (1ll << 31) - 1) / (1ll << 31));
-    if (grid < min_grid) grid = min_grid;
-    const int rpw = (chunks + grid - 1) / grid * 16;
-    const int z = (M + rpw - 1) / rpw;
-    auto go = [&](auto k, int nt) {
-      allow_lds(reinterpret_cast<const void*>(k));
-      hipLaunchKernelGGL(k, dim3(z), dim3(512), (size_t)2 * 8 * nt * 64 * 16, s, D, W, X, M, KO, rpw);
-    };
-    switch ((KO + 15) / 16) {
-      case 1: go(lstmf_dgrad_split_kernel<1>, 1); break;
-      case 2: go(lstmf_dgrad_split_kernel<2>, 2); break;
-      case 3: go(lstmf_dgrad_split_kernel<3>, 3); break;
-      case 4: go(lstmf_dgrad_split_kernel<4>, 4); break;
-      case 5: go(lstmf_dgrad_split_kernel<5>, 5); break;
-      case 6: go(lstmf_dgrad_split_kernel<6>, 6); break;
-      default: go(lstmf_dgrad_split_kernel<7>, 7); break;
     }
     return true;
   }

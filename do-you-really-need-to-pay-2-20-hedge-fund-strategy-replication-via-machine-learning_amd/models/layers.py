@@ -94,45 +94,16 @@ class Layer:
     def ebwd(self, ctx, dy, need_dx: bool, wgrad: bool = True):
         raise NotImplementedError
 
-    # generic tangent implementation via torch.func over the composed forward (used only by
-    # layers without a dedicated primitive, e.g. LayerNorm inside a GP critic)
-    @torch.enable_grad()
+    # tangent (forward-mode) and its reverse at the taped point: the GP's reverse-over-tangent pass
+    # (docs/ARCHITECTURE.md §1); every concrete layer implements both with native primitives
     def etfwd(self, ctx, xd):
-        x = ctx["x"]
-        _, yd = torch.func.jvp(lambda q: self.forward(q), (x,), (xd,))
-        return yd, {"xd": xd}
+        raise NotImplementedError
 
-    @torch.enable_grad()
     def etbwd(self, ctx, tctx, dy, dyd, need_dx: bool):
-        if dy is None:
-            dy = torch.zeros_like(dyd)
-        x = ctx["x"].detach().requires_grad_(True)
-        xd = tctx["xd"].detach().requires_grad_(True)
-        names = [s.name for s in self.specs]
-        ps = [self.p(n).detach().requires_grad_(True) for n in names]
-
-        def fun(q, qd, *params):
-            saved = self._override
-            self._override = dict(zip(names, params))
-            try:
-                return torch.func.jvp(lambda z: self.forward(z), (q,), (qd,))
-            finally:
-                self._override = saved
-
-        self._override = None
-        y, yd = fun(x, xd, *ps)
-        outs = torch.autograd.grad([y, yd], [x, xd] + ps, [dy, dyd], allow_unused=True)
-        for n, gr in zip(names, outs[2:]):
-            if gr is not None:
-                self.g(n).add_(gr)
-        return (outs[0], outs[1]) if need_dx else (None, None)
-
-    _override = None
+        raise NotImplementedError
 
     def w(self, name):
-        """Parameter as seen by ``forward`` (supports the functional override above)."""
-        if self._override is not None:
-            return self._override[name]
+        """Parameter as seen by ``forward`` (the autograd reference path)."""
         return self.p(name)
 
 

@@ -66,14 +66,13 @@ def linear(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: int,
     return y if out is None else out.copy_(y)
 
 
-# fp32 dZ (.., 400) @ W^T with W (K <= 112, 400): the LSTM layers' input gradient, on the
-# register-resident k-split kernel of csrc/lstm_f32.hip (HFREP_LSTMF_DGRAD=0: hipBLASLt, A/B only)
-_LSTMF_DGRAD = os.environ.get("HFREP_LSTMF_DGRAD", "1") != "0"
+# fp32 dZ (.., 400) @ W^T with W (K <= 112, 400): the LSTM layers' input gradient, on the native
+# kernels of csrc/lstm_f32.hip (lstmf_dgrad_s4 split / lstmf_dgrad exact)
 
 
 def linear_dgrad(dz: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     """dz @ W^T (input gradient)."""
-    if (_LSTMF_DGRAD and dz.dtype == torch.float32 and W.dtype == torch.float32 and dz.shape[-1] == 400
+    if (dz.dtype == torch.float32 and W.dtype == torch.float32 and dz.shape[-1] == 400
             and W.shape[0] <= 112 and _nat(dz)):
         return _ops().lstmf_dgrad(_2d(dz.contiguous()), W.contiguous()).reshape(*dz.shape[:-1], W.shape[0])
     if _nat(dz) and W.shape[1] > 4 and _blas_fp32(dz, dz.numel() // dz.shape[-1], W.shape[1], W.shape[0]):
@@ -290,12 +289,9 @@ def _use_lstm2(x: torch.Tensor, U: torch.Tensor) -> bool:
             and not _native.fallback_allowed())
 
 
-_LSTMF = os.environ.get("HFREP_LSTMF", "1") != "0"  # 0: the fp32 path falls back to zx GEMM + v1 (A/B only)
-
-
 def _use_lstmf(x: torch.Tensor, U: torch.Tensor, act: int) -> bool:
     """fp32 fused-projection kernels (csrc/lstm_f32.hip): H = 100, K in {32, 35, 36, 100}."""
-    return (_LSTMF and x.dtype == torch.float32 and _nat(x) and not _native.fallback_allowed()
+    return (x.dtype == torch.float32 and _nat(x) and not _native.fallback_allowed()
             and bool(_ops().lstmf_supported(int(U.shape[0]), int(x.shape[-1]), int(act))))
 
 
@@ -396,7 +392,7 @@ def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None, impl: int = 
     split exactly into three bf16 terms, six products on the bf16 matrix pipe; default for K <= 36,
     ``impl=2``) or the exact-fp32 MFMA kernel lstmf_wgrad_kernel (default for K = 100, ``impl=1``);
     otherwise per-product calls."""
-    f32 = (dZ.dtype == torch.float32 and _LSTMF and x.shape[-1] in (32, 35, 36, 100) and hs.shape[-1] == 100
+    f32 = (dZ.dtype == torch.float32 and x.shape[-1] in (32, 35, 36, 100) and hs.shape[-1] == 100
            and dZ.shape[-1] == 400)
     if f32 and x.shape[-1] == 35 and _nat(dZ):
         # the reference's 35-feature windows (GAN/MTSS_WGAN_GP.py:101): one zero column makes the rows

@@ -76,6 +76,9 @@ class GradSync:
         self.group, self.world, self.buckets = group, world, buckets
         self.backend = dist.get_backend(group) if group is not None else None
         self._pending = []
+        # the newest async work: RCCL runs a group's collectives on one stream in issue order, so its
+        # completion implies every earlier one's (graph capture waits for it, drain_)
+        self._last = None
 
     def all_reduce_(self, flat_grad: torch.Tensor) -> None:
         if self.world <= 1:
@@ -98,7 +101,9 @@ class GradSync:
         if self.world <= 1:
             return
         if self.backend == "nccl":
-            self._pending.append(dist.all_reduce(grad_slice, op=dist.ReduceOp.AVG, group=self.group, async_op=True))
+            w = dist.all_reduce(grad_slice, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+            self._pending.append(w)
+            self._last = w
         else:
             self._pending.append((dist.all_reduce(grad_slice, op=dist.ReduceOp.SUM, group=self.group,
                                                   async_op=True), grad_slice))
@@ -113,6 +118,29 @@ class GradSync:
                 w.wait()
         self._pending = []
         return n
+
+    def drain_(self, timeout_s: float = 120.0) -> bool:
+        """Block the host until the newest async collective (hence every earlier one of the group) has
+        COMPLETED on the device (``Work.is_completed``: its end event has been reached), so no eager
+        collective is in flight when a hipGraph capture starts.  Deterministic -- no timing assumption
+        about the ProcessGroupNCCL watchdog thread: with its event cache off (:func:`nccl_graph_safe_env`)
+        an event the watchdog still queries is never re-recorded inside the capture.  Call it outside
+        any capture; raises if the work does not complete within ``timeout_s``."""
+        import time
+
+        w, self._last = self._last, None
+        if w is None:
+            return False
+        t0 = time.monotonic()
+        while not w.is_completed():
+            if time.monotonic() - t0 > timeout_s:
+                raise RuntimeError(f"GradSync.drain_: a collective did not complete within {timeout_s} s")
+            time.sleep(0.0005)
+        return True
+
+    def forget_(self) -> None:
+        """Drop the newest-work reference (after a capture: captured works must never be queried)."""
+        self._last = None
 
     def broadcast_params(self, models, src: int = 0) -> None:
         if self.world <= 1:

@@ -84,11 +84,11 @@ class GraphedStep:
             raise RuntimeError("graph capture needs the native (device-counter) RNG")
         if trainer.grad_sync is not None and trainer.world > 1:
             # RCCL collectives are graph-capturable (ProcessGroupNCCL records them on the captured
-            # stream); gloo / CPU collectives are not.  Opt-in (HFREP_GRAPH_DP=1) until a multi-GPU
-            # run validates replayed all-reduces against the eager step.
-            if trainer.grad_sync.backend != "nccl" or os.environ.get("HFREP_GRAPH_DP", "0") != "1":
-                raise RuntimeError("graph capture under data parallelism needs RCCL and HFREP_GRAPH_DP=1 "
-                                   "(collectives stay eager otherwise)")
+            # stream; tests/test_gpu_rccl.py replays them bitwise against the eager step); gloo / CPU
+            # collectives are not.  HFREP_GRAPH_DP=0 keeps DP steps eager.
+            if trainer.grad_sync.backend != "nccl" or os.environ.get("HFREP_GRAPH_DP", "1") == "0":
+                raise RuntimeError("graph capture under data parallelism needs RCCL (HFREP_GRAPH_DP=0 "
+                                   "keeps the collectives eager)")
         self.t, self.warmup, self.calls = trainer, warmup, 0
         self.graph = None
 
@@ -100,20 +100,21 @@ class GraphedStep:
         ``hipEventQuery``), and in the default global mode any such query from another thread
         while a stream captures is illegal -- the watchdog then takes the process down (the
         round-2 driver run of tests/test_gpu_rccl.py).  Thread-local mode only forbids unsafe
-        calls on the capturing thread.  Every outstanding bucket is joined and the device drained
-        first, so no eager collective is still in flight when the capture starts."""
+        calls on the capturing thread.  Every outstanding bucket is joined, the device drained and every
+        warmup collective confirmed complete (:meth:`GradSync.drain_`), so no eager collective is still
+        in flight when the capture starts."""
         t = self.t
         if t.grad_sync is not None:
             t.grad_sync.finish_()
         torch.cuda.synchronize()
-        if t.grad_sync is not None and t.grad_sync.world > 1:
-            # let the ProcessGroupNCCL watchdog (100 ms loop) retire the warmup collectives before any
-            # collective is recorded into the capture (see parallel/dp.py:nccl_graph_safe_env)
-            time.sleep(0.3)
+        if t.grad_sync is not None:
+            t.grad_sync.drain_()
         it = t.iteration
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             t.train_step()
+        if t.grad_sync is not None:
+            t.grad_sync.forget_()
         t.iteration = it  # capture recorded the step, it did not run it
 
     def __call__(self):

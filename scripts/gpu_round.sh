@@ -1,9 +1,9 @@
 #!/bin/bash
 # One GPU pass: kernel numerics of the fp32 split kernels, the full GPU suite, the headline bench and a
-# rocprofv3 kernel table of 3 fp32 iterations.  usage: scripts/gpu_r03_round.sh OUTNAME [--no-suite]
+# rocprofv3 kernel table of 3 fp32 iterations.  usage: scripts/gpu_round.sh OUTNAME [--no-suite]
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"
-OUT=gpurun_out/${1:-r03_round}; mkdir -p $OUT
+OUT=gpurun_out/${1:-round}; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "lstmf_wgrad or lstmf_dgrad or narrowf or split_bptt or split_forward" -q --timeout 200 \
   --timeout-method thread > $OUT/tests_split.txt 2>&1 || { tail -n 30 $OUT/tests_split.txt; exit 1; }

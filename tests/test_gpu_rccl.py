@@ -5,7 +5,7 @@ job has 2 ranks, which sends every gradient bucket through ``all_reduce(AVG)`` o
 backend (the async, reverse-pass-overlapped ``start_`` / ``finish_`` path of parallel/dp.py);
 AVG over the one real member is exact, so the trainer must stay bitwise equal to a trainer with
 no sync at all.  The second test captures the same step, collectives included, into a hipGraph
-(``HFREP_GRAPH_DP=1``, train/runner.py GraphedStep).  Both run in a spawned process so the
+(the default for RCCL data parallelism, train/runner.py GraphedStep).  Both run in a spawned process so the
 process group never leaks into other tests.
 """
 import socket
@@ -30,7 +30,6 @@ def _worker(port, graph, key, q):
         from hfrep.train.runner import GraphedStep
 
         os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
-        os.environ["HFREP_GRAPH_DP"] = "1"
         from hfrep.parallel.dp import nccl_graph_safe_env
 
         nccl_graph_safe_env()  # (before the process group: RCCL events are not recycled into captures)

@@ -653,6 +653,33 @@ def test_lstm2_tbwd_bitwise_large_batch(cuda, act):
     assert all(torch.equal(a, c) for a, c in zip(y0, y1))
 
 
+@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("K", [32, 100])
+def test_lstm2_tfwd_bitwise_large_batch(cuda, act, K):
+    """The bf16 tangent forward (hdot and the tangent tape) run three times at B = 32 772 on one primal
+    tape is bitwise equal (act = sigmoid differed run to run in rows 30 / 31 of a few row blocks with
+    lstm_fwd4_kernel<TAN> in r03, profiles/r03_race/README.md)."""
+    from hfrep.ops import functional as Fn
+
+    H, T, B = 100, 24, 32772
+    g = torch.Generator(device=cuda).manual_seed(1)
+    mk = lambda *s_, sc=0.5: (torch.randn(*s_, device=cuda, generator=g) * sc).to(torch.bfloat16)
+    x, xd = mk(B, T, K), mk(B, T, K)
+    W = torch.randn(K, 4 * H, device=cuda, generator=g) * 0.1
+    U = torch.randn(H, 4 * H, device=cuda, generator=g) * 0.1
+    b = torch.randn(4 * H, device=cuda, generator=g) * 0.1
+    _, tape = Fn.lstm_layer_fwd(x, W, b, U, act, True)
+    dH = mk(B, T, H)
+    # (the tangent tape's padded-unit slots are never written: compare what reads it, the tangent reverse)
+    h0, t0 = Fn.lstm_layer_tfwd(xd, W, tape, U, act)
+    z0 = Fn.lstm_layer_tbwd(dH, dH, tape, t0, U, act)
+    for _ in range(2):
+        h1, t1 = Fn.lstm_layer_tfwd(xd, W, tape, U, act)
+        assert torch.equal(h0, h1), "tangent forward hdot not bitwise run to run"
+        z1 = Fn.lstm_layer_tbwd(dH, dH, tape, t1, U, act)
+        assert all(torch.equal(a, c) for a, c in zip(z0, z1)), "tangent tape not bitwise run to run"
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("kind", [0, 1])
 @pytest.mark.parametrize("n,split", [(64, 32), (70 * 24, 35 * 24), (1 << 20, 1 << 19), (1000, 1000)])
@@ -862,14 +889,13 @@ def test_lstmf_dgrad(cuda, M, KO):
     ref = dz.double() @ W.double().t()
     scale = (dz.abs().double() @ W.abs().double().t()).max().item()
     errs = {}
-    for impl in (1, 2, 3):  # exact-fp32 MFMA kernel, three-term bf16 split kernels (partial-sum / LDS-staged)
+    for impl in (1, 3):  # exact-fp32 MFMA kernel, LDS-staged three-term bf16 split kernel
         out = _native.native().lstmf_dgrad(dz.to(cuda), W.to(cuda), impl)
         _close(out, ref, torch.float32, scale=scale)
         again = _native.native().lstmf_dgrad(dz.to(cuda), W.to(cuda), impl)
         assert torch.equal(out, again)
         errs[impl] = (out.double().cpu() - ref).abs().max().item()
     # the split's dropped terms are <= 2^-24 of each product: within 2x the exact kernel's error
-    assert errs[2] <= 2 * errs[1] + 1e-6 * scale, errs
     assert errs[3] <= 2 * errs[1] + 1e-6 * scale, errs
 
 
