@@ -674,6 +674,41 @@ Tensor sample_windows(Tensor data, int64_t batch, int64_t seed, Tensor ctr, at::
   return out;
 }
 
+// ------------------------------------------------------------------------------------ autoencoder
+// The whole fit of the factor autoencoder (Autoencoder_encapsulate.py:72-105) in one launch: Xt (nt, A)
+// and Xv (nv, A) fp32 (MinMax-scaled), order (epochs, nt) int32 batch permutations, We (A, k) / Wd (k, A)
+// fp32 weights and their Nadam slots, the shared step counter / momentum cache.  Returns the per-epoch
+// (train loss, val loss) history (epochs, 2) fp64 and the number of epochs run (int32 scalar tensor).
+bool ae_fit_supported(int64_t A, int64_t k, int64_t batch) { return hfrep::ae_fit_supported((int)A, (int)k, (int)batch); }
+
+std::tuple<Tensor, Tensor> ae_fit(Tensor Xt, Tensor Xv, Tensor order, Tensor We, Tensor Wd, Tensor mWe, Tensor vWe,
+                                  Tensor mWd, Tensor vWd, Tensor step, Tensor m_cache, double lr, double b1, double b2,
+                                  double eps, int64_t batch, int64_t patience, bool bf16) {
+  for (const Tensor* t : {&Xt, &Xv, &We, &Wd, &mWe, &vWe, &mWd, &vWd, &step, &m_cache}) {
+    CHECK_F32(*t);
+    TORCH_CHECK(t->is_contiguous() && t->device() == Xt.device(), "ae_fit: contiguous fp32 tensors on one device");
+  }
+  TORCH_CHECK(order.is_cuda() && order.device() == Xt.device() && order.scalar_type() == at::kInt && order.is_contiguous() &&
+                  order.dim() == 2, "ae_fit: order must be a contiguous (epochs, nt) int32 tensor");
+  TORCH_CHECK(Xt.dim() == 2 && Xv.dim() == 2 && Xv.size(1) == Xt.size(1), "ae_fit: Xt (nt, A), Xv (nv, A)");
+  const int nt = Xt.size(0), nv = Xv.size(0), A = Xt.size(1), k = We.numel() / A, epochs = order.size(0);
+  TORCH_CHECK(order.size(1) == nt && nt > 0 && epochs > 0, "ae_fit: order shape");
+  TORCH_CHECK(We.numel() == (int64_t)A * k && Wd.numel() == We.numel() && mWe.numel() == We.numel() &&
+                  vWe.numel() == We.numel() && mWd.numel() == We.numel() && vWd.numel() == We.numel(),
+              "ae_fit: weight / slot sizes");
+  TORCH_CHECK(step.numel() == 1 && m_cache.numel() == 1, "ae_fit: scalar counters");
+  TORCH_CHECK(hfrep::ae_fit_supported(A, k, (int)batch) && patience >= 1, "ae_fit: A, k <= 32 and batch <= 64");
+  GUARD(Xt);
+  Tensor hist = at::zeros({epochs, 2}, Xt.options().dtype(at::kDouble));
+  Tensor nep = at::zeros({1}, Xt.options().dtype(at::kInt));
+  hfrep::launch_ae_fit(bf16, Xt.data_ptr<float>(), nt, Xv.data_ptr<float>(), nv, order.data_ptr<int>(), epochs, (int)batch,
+                       (int)patience, We.data_ptr<float>(), Wd.data_ptr<float>(), mWe.data_ptr<float>(), vWe.data_ptr<float>(),
+                       mWd.data_ptr<float>(), vWd.data_ptr<float>(), step.data_ptr<float>(), m_cache.data_ptr<float>(),
+                       (float)lr, (float)b1, (float)b2, (float)eps, A, k, hist.data_ptr<double>(), nep.data_ptr<int>(),
+                       cur_stream(Xt));
+  return {hist, nep};
+}
+
 // ------------------------------------------------------------------------------------ optimizers
 void rmsprop_(Tensor p, Tensor g, Tensor ms, double lr, double rho, double eps, double clip, double gscale) {
   CHECK_F32(p); CHECK_F32(g); CHECK_F32(ms);
@@ -761,6 +796,10 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("interpolate(Tensor real, Tensor fake, Tensor alpha) -> Tensor");
   m.def("philox_fill_(Tensor(a!) out, int seed, Tensor(b!) ctr, int dist) -> ()");
   m.def("sample_windows(Tensor data, int batch, int seed, Tensor(a!) ctr, ScalarType out_dtype, Tensor(b!)? dst=None) -> Tensor");
+  m.def("ae_fit_supported(int A, int k, int batch) -> bool", &ae_fit_supported);  // no tensor inputs: catch-all kernel
+  m.def("ae_fit(Tensor Xt, Tensor Xv, Tensor order, Tensor(a!) We, Tensor(b!) Wd, Tensor(c!) mWe, Tensor(d!) vWe, "
+        "Tensor(e!) mWd, Tensor(f!) vWd, Tensor(g!) step, Tensor(h!) m_cache, float lr, float b1, float b2, float eps, "
+        "int batch, int patience, bool bf16) -> (Tensor, Tensor)");
   m.def("rmsprop_(Tensor(a!) p, Tensor g, Tensor(b!) ms, float lr, float rho, float eps, float clip, float gscale) -> ()");
   m.def("adam_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, float lr, float b1, float b2, float eps, float clip, float gscale) -> ()");
   m.def("nadam_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor m_cache, float lr, float b1, float b2, float eps, float gscale) -> ()");
@@ -801,6 +840,7 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("interpolate", &interpolate);
   m.impl("philox_fill_", &philox_fill_);
   m.impl("sample_windows", &sample_windows);
+  m.impl("ae_fit", &ae_fit);
   m.impl("rmsprop_", &rmsprop_);
   m.impl("adam_", &adam_);
   m.impl("nadam_", &nadam_);

@@ -71,6 +71,13 @@ int set_lstmf_bwd_impl(int v);  // 2: the exact-fp32 BPTT kernel, 3: the split-r
 // impl: 0 = default (exact under HFREP_FP32_EXACT=1, else the LDS-staged split for KO > 64), 1 = exact, 3 = three-term bf16 split
 bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl = 0);
 
+// ---- ae.hip (factor autoencoder: the whole Keras fit -- MSE, Nadam, EarlyStopping -- in one launch) ----
+bool ae_fit_supported(int A, int k, int batch);
+void launch_ae_fit(bool bf16, const float* Xt, int nt, const float* Xv, int nv, const int* order, int epochs, int batch,
+                   int patience, float* We, float* Wd, float* mWe, float* vWe, float* mWd, float* vWd, float* step,
+                   float* m_cache, float lr, float b1, float b2, float eps, int A, int k, double* hist, int* nep,
+                   hipStream_t s);
+
 // ---- gemm.hip ----
 // C[M,N] = act(A[M,K] . op(W) + bias);  op(W) = W (K,N) or W^T when w_trans (W stored (N,K)).
 // A and C share the activation dtype `dt`; W and bias are fp32 (converted while staging).

@@ -21,6 +21,7 @@ import torch
 
 from ..data.scaler import MinMaxScaler
 from ..models.autoencoder import FactorAutoencoder
+from ..ops import _native
 from ..train.optim import KerasOptimizer
 from .replication import ex_post_return, normalization, ols, reshape_cab
 
@@ -54,16 +55,32 @@ class AETrainer:
         self.opt = KerasOptimizer.nadam(lr, device=self.device)
 
     def fit(self, x: np.ndarray, epochs: int = 1000, batch_size: int = 48, validation_split: float = 0.25,
-            patience: int = 5, shuffle: bool = True, seed: int = 123, dtype=torch.float32, verbose: int = 0):
+            patience: int = 5, shuffle: bool = True, seed: int = 123, dtype=torch.float32, verbose: int = 0,
+            fused: bool | None = None):
+        """Keras ``fit`` semantics: ``validation_split`` takes the LAST rows, one Nadam tick per batch,
+        EarlyStopping(val_loss, patience) per epoch (weights of the last epoch are kept).
+
+        On the GPU the whole fit is ONE launch of csrc/ae.hip (``fused``, default on a native GPU
+        build): the batch permutations are drawn here up front from the same numpy stream, and the
+        forward, the fused MSE value + gradient, the reverse pass, Nadam, the validation loss and the
+        stopping decision all run inside one workgroup.  ``fused=False`` runs the explicit engine
+        batch by batch (the CPU path)."""
         x = np.asarray(x, dtype=np.float64)
         n = len(x)
         split = int(n * (1.0 - validation_split)) if validation_split else n
+        rs = np.random.RandomState(seed)
+        enc, dec = self.model.parts()
+        A, k = x.shape[1], self.model.latent_dim
+        if fused is None:
+            fused = (self.device.type == "cuda" and _native.use_native_for(enc.flat)
+                     and dtype in (torch.float32, torch.bfloat16)
+                     and bool(_native.native().ae_fit_supported(A, k, batch_size)))
+        if fused:
+            return self._fit_fused(x, split, epochs, batch_size, patience, shuffle, rs, dtype, verbose)
         xt = torch.as_tensor(x[:split], dtype=dtype, device=self.device)
         xv = torch.as_tensor(x[split:], dtype=dtype, device=self.device) if split < n else None
-        rs = np.random.RandomState(seed)
         hist = {"loss": [], "val_loss": []}
         best, wait = np.inf, 0
-        enc, dec = self.model.parts()
         # one host <-> device round trip per epoch: the epoch's batch order goes to the device in
         # one copy, the loss is accumulated there (float64, batch order: the same sum as the
         # host-side one), and the training and validation losses come back together for the
@@ -99,6 +116,30 @@ class AETrainer:
                     wait += 1
                     if wait >= patience:
                         break
+        return hist
+
+    @torch.no_grad()
+    def _fit_fused(self, x, split, epochs, batch_size, patience, shuffle, rs, dtype, verbose):
+        n, A = x.shape
+        enc, dec = self.model.parts()
+        k = self.model.latent_dim
+        orders = np.stack([rs.permutation(split) if shuffle else np.arange(split) for _ in range(epochs)])
+        dev = self.device
+        xt = torch.as_tensor(x[:split], dtype=torch.float32, device=dev)
+        xv = torch.as_tensor(x[split:], dtype=torch.float32, device=dev).reshape(-1, A)
+        order_t = torch.as_tensor(orders.astype(np.int32), device=dev)
+        nw = A * k
+        (mWe, vWe), (mWd, vWd) = self.opt._slots(enc.flat), self.opt._slots(dec.flat)
+        hist_t, nep_t = _native.native().ae_fit(
+            xt, xv, order_t, enc.flat.data[:nw], dec.flat.data[:nw], mWe[:nw], vWe[:nw], mWd[:nw], vWd[:nw],
+            self.opt.iterations, self.opt.m_cache, self.opt.lr, self.opt.b1, self.opt.b2, self.opt.eps, batch_size,
+            patience if split < n else epochs + 1, dtype == torch.bfloat16)
+        ne = int(nep_t.item())
+        h = hist_t[:ne].cpu().numpy()
+        hist = {"loss": h[:, 0].tolist(), "val_loss": h[:, 1].tolist() if split < n else []}
+        if verbose:
+            for ep in range(ne):
+                print(f"epoch {ep + 1}: loss {h[ep, 0]:.6f} val_loss {h[ep, 1]:.6f}")
         return hist
 
 

@@ -1,9 +1,10 @@
 """Factor autoencoder (BASELINE config 2: AE on one MI355X) — the GPU engine vs the CPU fp64 engine.
 
-The AE trains through the explicit engine: native Dense (no bias, LeakyReLU epilogue) kernels,
-the fused Keras-Nadam kernel and the MSE adjoint on the GPU (Autoencoder_encapsulate.py:23-30,
-:79-96).  Same initial weights, same batch order, five epochs: fp32 must track the fp64 CPU run
-tightly, bf16 (bf16 activations, fp32 master weights) within bf16 noise.
+On the GPU the whole fit (forward, fused MSE value + gradient, reverse pass, Keras Nadam, validation
+loss, EarlyStopping) is ONE launch of csrc/ae.hip; ``fused=False`` runs the explicit engine batch by
+batch (native Dense / LeakyReLU / Nadam kernels).  Same initial weights, same batch order, five
+epochs: fp32 must track the fp64 CPU run tightly, bf16 (bf16 activations, fp32 master weights)
+within bf16 noise (Autoencoder_encapsulate.py:23-30, :79-96).
 """
 import numpy as np
 import pytest
@@ -17,7 +18,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("dt,tol", [(torch.float32, 2e-4), (torch.bfloat16, 5e-2)])
 @pytest.mark.parametrize("k", [1, 7, 21])
-def test_ae_trainer_gpu_vs_cpu(cuda, dt, tol, k):
+@pytest.mark.parametrize("fused", [True, False])
+def test_ae_trainer_gpu_vs_cpu(cuda, dt, tol, k, fused):
     rs = np.random.RandomState(k)
     x = rs.rand(168, 22)
     mg = FactorAutoencoder(k, 22, seed=3, device=cuda)
@@ -25,7 +27,7 @@ def test_ae_trainer_gpu_vs_cpu(cuda, dt, tol, k):
     with torch.no_grad():
         for a, b in zip(mg.parts(), mc.parts()):
             b.flat.copy_(a.flat.double().cpu())
-    hg = AETrainer(mg, device=cuda).fit(x, epochs=5, patience=100, seed=9, dtype=dt)
+    hg = AETrainer(mg, device=cuda).fit(x, epochs=5, patience=100, seed=9, dtype=dt, fused=fused)
     hc = AETrainer(mc).fit(x, epochs=5, patience=100, seed=9, dtype=torch.float64)
     np.testing.assert_allclose(hg["loss"], hc["loss"], rtol=tol * 10, atol=1e-7)
     for a, b in zip(mg.parts(), mc.parts()):
@@ -50,3 +52,34 @@ def test_ae_replication_object_on_gpu(cuda, cleaned):
         post = ae.post(etf)
         assert ante.shape == (144, 13) and post.shape == (144, 13)
         assert np.isfinite(post.to_numpy()).all()
+
+
+def test_ae_fused_fit_early_stopping(cuda):
+    """The in-kernel EarlyStopping: the fused fit stops where the Keras rule says, given the history it
+    returns (first epoch whose val_loss has not improved on the best for `patience` epochs), and its
+    weights / optimizer counter equal an eager fp32 run of that many epochs within fp32 noise."""
+    rs = np.random.RandomState(5)
+    x = rs.rand(168, 22)
+    m1 = FactorAutoencoder(3, 22, seed=4, device=cuda)
+    m2 = FactorAutoencoder(3, 22, seed=4, device=cuda)
+    t1 = AETrainer(m1, device=cuda)
+    h1 = t1.fit(x, epochs=1000, patience=3, seed=2, fused=True)
+    ne = len(h1["val_loss"])
+    assert 3 < ne < 1000
+    vl, best, wait, stop = h1["val_loss"], np.inf, 0, None
+    for i, v in enumerate(vl):
+        if v < best:
+            best, wait = v, 0
+        else:
+            wait += 1
+            if wait >= 3:
+                stop = i + 1
+                break
+    assert stop == ne, (stop, ne)
+    t2 = AETrainer(m2, device=cuda)
+    h2 = t2.fit(x, epochs=ne, patience=10 ** 6, seed=2, fused=False)
+    np.testing.assert_allclose(h1["loss"], h2["loss"], rtol=1e-4)
+    assert float(t1.opt.iterations.item()) == float(t2.opt.iterations.item()) == ne * 3
+    for a, b in zip(m1.parts(), m2.parts()):
+        rel = ((a.flat - b.flat).norm() / b.flat.norm()).item()
+        assert rel < 1e-4, rel
