@@ -10,10 +10,11 @@ the whole-job aggregate over all ranks.
 Model: the reference architecture at the north-star shape — generator LSTM(100, sigmoid) -> LN ->
 LSTM(100, sigmoid) -> LeakyReLU -> LN -> Dense(32); critic LSTM(100) -> LSTM(100) -> Flatten ->
 Dense(1); random init; synthetic return windows (no dataset/network on the box); compute dtype
-fp32 (the reference's Keras float32: fp32 storage and accumulation, products on the exact-f32 MFMA
-except the first LSTM layer's weight gradient, which splits each fp32 operand exactly into three
-bf16 terms -- six products, error at the fp32 rounding level, tests/test_kernels_gpu.py
-test_lstmf_wgrad_split_vs_exact) for the headline record, and a bf16 sub-record
+fp32 (the reference's Keras float32: fp32 storage, tapes, gradients, optimizer state and accumulation;
+products on the exact-f32 MFMA or as the fp32-accurate three-term bf16 split -- each fp32 operand =
+h + m + l, six of the nine products, error <= 2x the exact kernel's vs fp64,
+tests/test_kernels_gpu.py test_lstmf_*split*; HFREP_FP32_EXACT=1 for exact-f32 everywhere) for the
+headline record, and a bf16 sub-record
 (bf16 MFMA with fp32 accumulation, fp32 master weights / optimizer) of the same config.
 
 Usage:
@@ -183,8 +184,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             # fp32 = the reference's precision (Keras float32): fp32 activations, tapes, gradients and
-            # optimizer state; products on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32) except the
-            # K <= 36 LSTM weight gradient (exact three-term bf16 split, fp32-rounding-level error)
+            # optimizer state; products on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32) or the
+            # fp32-accurate three-term bf16 split (see the module docstring)
             "dtype": "fp32" if primary == "float32" else "bf16",
             "data": "synthetic",
             "config": {
@@ -198,7 +199,7 @@ def main():
             },
             "losses_finite": res["losses_finite"],
             # the W-dist half of the metric is a training-quality run, not a throughput step
-            "w_dist_parity": "profiles/r02_parity/README.md" if args.model == "mtss_wgan_gp" else None,
+            "w_dist_parity": "profiles/r03_parity/README.md" if args.model == "mtss_wgan_gp" else None,
             "peak_mem_gb_rank0": res["peak_mem_gb_rank0"],
         }
         if sub is not None:

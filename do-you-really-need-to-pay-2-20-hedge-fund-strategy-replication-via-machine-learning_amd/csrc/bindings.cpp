@@ -80,6 +80,9 @@ Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act, optional<Tens
   else if (dt_of(x) == hfrep::DT_F32 && hfrep::narrowf_supported(K, N))
     hfrep::launch_narrowf(x.data_ptr<float>(), W.data_ptr<float>(), N, 1, b.has_value() ? b->data_ptr<float>() : nullptr,
                           y.data_ptr<float>(), M, K, N, (int)act, cur_stream(x));
+  else if (dt_of(x) == hfrep::DT_F32 && hfrep::widef_supported(K, N))
+    hfrep::launch_widef(x.data_ptr<float>(), W.data_ptr<float>(), N, 1, b.has_value() ? b->data_ptr<float>() : nullptr,
+                        y.data_ptr<float>(), M, K, N, (int)act, cur_stream(x));
   else if (dt_of(x) == hfrep::DT_BF16 && hfrep::narrow_supported(K, N))
     hfrep::launch_narrow_fwd(x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
                              y.data_ptr(), M, K, N, (int)act, cur_stream(x));
@@ -104,6 +107,9 @@ Tensor linear_dgrad(Tensor dz, Tensor W) {
   else if (dt_of(dz) == hfrep::DT_F32 && hfrep::narrowf_supported(K, N))  // B[k][n] = W[n][k]
     hfrep::launch_narrowf(dz.data_ptr<float>(), W.data_ptr<float>(), 1, K, nullptr, dx.data_ptr<float>(), M, K, N, 0,
                           cur_stream(dz));
+  else if (dt_of(dz) == hfrep::DT_F32 && hfrep::widef_supported(K, N))  // B[k][n] = W[n][k]
+    hfrep::launch_widef(dz.data_ptr<float>(), W.data_ptr<float>(), 1, K, nullptr, dx.data_ptr<float>(), M, K, N, 0,
+                        cur_stream(dz));
   else if (dt_of(dz) == hfrep::DT_BF16 && N > 64)
     hfrep::launch_linear2(dz.data_ptr(), W.data_ptr<float>(), nullptr, dx.data_ptr(), M, N, K, 1, 0, cur_stream(dz));
   else

@@ -58,7 +58,7 @@ bool launch_lstmf_tbwd(const float* dH, const float* dHd, const float* tape, con
 // (lstmf_wgrad_workspace_floats) and one fixed-order reduce
 bool lstmf_wgrad_supported(int K, int H, int N);
 // impl: 0 = default (exact under HFREP_FP32_EXACT=1, else the pair split for K <= 36 and the quad split for K = 100), 1 = exact-fp32
-// MFMA, 2 = the three-term bf16 split (pair), 3 = the three-term bf16 split (quad)
+// MFMA, 2 = the three-term bf16 split (pair), 3 = the three-term bf16 split (quad), 4 = pair, pipelined
 size_t lstmf_wgrad_workspace_floats(int M, int K, int impl = 0);
 bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
                         float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl = 0);
@@ -113,6 +113,11 @@ void launch_narrow_fwd(const void* x, const float* W, const float* b, void* y, i
                        hipStream_t s);
 // exact-fp32 narrow GEMM y = act(x B + b), B[k][n] = Bp[k sk + n sn]; K in {32, 36, 64, 100, 128}, 4 < N <= 112
 bool narrowf_supported(int K, int N);
+// fp32 y = act(x B + b) for K % 4 == 0, K <= 320, any N > 4 (B staged in LDS per 112-column block):
+// the shapes narrowf cannot hold in registers (conv critic im2col GEMMs and their input gradients)
+bool widef_supported(int K, int N);
+void launch_widef(const float* x, const float* B, int sk, int sn, const float* b, float* y, int M, int K, int N,
+                  int act, hipStream_t s);
 void launch_narrowf(const float* x, const float* B, int sk, int sn, const float* b, float* y, int M, int K, int N,
                     int act, hipStream_t s);
 void launch_skinny_fwd(int dt, const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,

@@ -385,6 +385,115 @@ __global__ void __launch_bounds__(256) narrowf_kernel(const float* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// fp32 GEMM for the shapes narrowf cannot hold in registers: widef_kernel
+// ------------------------------------------------------------------------------------------
+// y = act(x B + b), x (M, K) fp32 row-major with K % 4 == 0 and K <= 320, any N (column blocks of 112 over
+// grid.y).  The conv critic's im2col GEMMs (K = k C = 300 at C = 100) and their input gradients (N = k C)
+// went to hipBLASLt (K14): narrowf keeps its B fragments in registers (K / 4 per column tile), which at
+// K = 300 would be 525 of them.  Here the workgroup's B block (K x 112, zero-padded) is staged once in
+// LDS (<= 145 KiB; row stride 116 floats: the four k-rows of a 16x16x4 B fragment land on distinct bank
+// halves) and every wave walks 16-row chunks of x with the exact-fp32 v_mfma_f32_16x16x4_f32: per chunk
+// the lane's x values are loaded as float4 (k = 16 q + 4 g + 0..3, the same k permutation on both
+// operands as narrowf) one chunk ahead, B fragments are single ds_read_b32 per MFMA.  Exact fp32 (an
+// fmaf chain per output), any activation in the epilogue.
+constexpr int WF_NT = 7, WF_LDB = 16 * WF_NT + 4, WF_KMAX = 320;
+template <int NQ>
+__global__ void __launch_bounds__(256) widef_kernel(const float* __restrict__ x, const float* __restrict__ Bp, int sk,
+                                                    int sn, const float* __restrict__ bias, float* __restrict__ y,
+                                                    int M, int K, int N, int act) {
+  extern __shared__ __attribute__((aligned(16))) float bsm[];  // [16 NQ][WF_LDB]
+  const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int col0 = blockIdx.y * 16 * WF_NT;
+  for (int e = threadIdx.x; e < 16 * NQ * WF_LDB; e += 256) {
+    const int k = e / WF_LDB, c = e - k * WF_LDB, col = col0 + c;
+    bsm[e] = (k < K && c < 16 * WF_NT && col < N) ? Bp[(size_t)k * sk + (size_t)col * sn] : 0.f;
+  }
+  float bv[WF_NT];
+#pragma unroll
+  for (int n = 0; n < WF_NT; ++n) {
+    const int col = col0 + 16 * n + c16;
+    bv[n] = (bias && col < N) ? bias[col] : 0.f;
+  }
+  __syncthreads();
+  const int nch = (M + 15) / 16;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  typedef __amdgpu_buffer_rsrc_t rsrc_t;
+  auto rsrc_of = [&](int c) -> rsrc_t {  // rows of chunk c (past M: zero-size descriptor, loads read 0)
+    const int r0 = c * 16, nr = c < nch ? min(16, M - r0) : 0;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x) + (nr ? (size_t)r0 * K : 0), 0, nr * K * 4, 0x00020000);
+  };
+  f32x4 a4[2][NQ];
+  auto load = [&](int set, int c) {
+    const rsrc_t r = rsrc_of(c);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int k = 16 * q + 4 * g;  // (K % 4 == 0: a float4 is wholly inside the row or past its end)
+      a4[set][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, k < K ? (c16 * K + k) * 4 : 0x7fff0000,
+                                                                                   0, 0));
+    }
+  };
+  const float* bl = bsm + (4 * g) * WF_LDB + c16;  // B[k = 16 q + 4 g + j][16 n + c16]
+  auto body = [&](int set, int c) {
+    f32x4 acc[WF_NT];
+#pragma unroll
+    for (int n = 0; n < WF_NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float av = a4[set][q][j];
+#pragma unroll
+        for (int n = 0; n < WF_NT; ++n)
+          acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bl[(16 * q + j) * WF_LDB + 16 * n], acc[n], 0, 0, 0);
+      }
+    const int r0 = c * 16 + 4 * g;
+#pragma unroll
+    for (int n = 0; n < WF_NT; ++n) {
+      const int col = col0 + 16 * n + c16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (col < N && r0 + i < M) y[(size_t)(r0 + i) * N + col] = act_f(act, acc[n][i] + bv[n]);
+    }
+  };
+  int c = wid;
+  if (c < nch) load(0, c);
+  for (; c < nch; c += 2 * nw) {
+    load(1, c + nw);
+    body(0, c);
+    if (c + nw >= nch) break;
+    load(0, c + 2 * nw);
+    body(1, c + nw);
+  }
+}
+
+bool widef_supported(int K, int N) { return K >= 4 && K <= WF_KMAX && K % 4 == 0 && N > 4; }
+
+void launch_widef(const float* x, const float* B, int sk, int sn, const float* b, float* y, int M, int K, int N,
+                  int act, hipStream_t s) {
+  if (M <= 0) return;
+  const int nq = (K + 15) / 16, nch = (M + 15) / 16, ncb = (N + 16 * WF_NT - 1) / (16 * WF_NT);
+  const size_t smem = (size_t)16 * nq * WF_LDB * 4;
+  const int grid = std::max(1, std::min((nch + 3) / 4, std::max(1, device_cu_count() / ncb)));
+  auto go = [&](auto kern) {
+    static bool attr = false;  // (per instantiation: the lambda's template parameter makes one per NQ)
+    if (!attr) {
+      HFREP_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          160 * 1024));
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid, ncb), dim3(256), smem, s, x, B, sk, sn, b, y, M, K, N, act);
+  };
+  switch (nq) {
+#define HFREP_WIDEF(Q) case Q: go(widef_kernel<Q>); break;
+    HFREP_WIDEF(1) HFREP_WIDEF(2) HFREP_WIDEF(3) HFREP_WIDEF(4) HFREP_WIDEF(5) HFREP_WIDEF(6) HFREP_WIDEF(7)
+    HFREP_WIDEF(8) HFREP_WIDEF(9) HFREP_WIDEF(10) HFREP_WIDEF(11) HFREP_WIDEF(12) HFREP_WIDEF(13) HFREP_WIDEF(14)
+    HFREP_WIDEF(15) HFREP_WIDEF(16) HFREP_WIDEF(17) HFREP_WIDEF(18) HFREP_WIDEF(19)
+    default: go(widef_kernel<20>); break;
+#undef HFREP_WIDEF
+  }
+}
+
 bool narrowf_supported(int K, int N) {
   return N > 4 && N <= 112 && (K == 32 || K == 36 || K == 64 || K == 100 || K == 128);
 }

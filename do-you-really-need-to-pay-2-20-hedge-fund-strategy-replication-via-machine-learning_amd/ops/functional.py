@@ -10,7 +10,6 @@ dtype of the explicit engine); gradients are always fp32.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -33,29 +32,16 @@ def _2d(x: torch.Tensor) -> torch.Tensor:
 # ---------------------------------------------------------------------------------------
 # dense / GEMM family
 # ---------------------------------------------------------------------------------------
-# fp32 GEMMs: K in {32, 36, 64, 100, 128} with 4 < N <= 112 (every Dense of the LSTM and MLP zoo at
-# the bench shapes, forward and input gradient) run on the native exact-fp32 narrow kernel
-# (csrc/skinny.hip narrowf_kernel).  Other fp32 shapes with many rows (the conv critic's im2col
-# GEMMs, K = k C > 128) go to the vendor library (hipBLASLt through torch.mm; exact fp32 on gfx950):
-# at M = 786k it ran those 1.4-2.6x faster than the generic tile kernel of csrc/gemm.hip
-# (profiles/r02_fp32/gemm_fp32_native_vs_hipblaslt.jsonl).  bf16 and small M stay native.
-_BLAS_MIN_ROWS = int(os.environ.get("HFREP_FP32_BLAS_MIN_ROWS", "65536"))
-
-
-def _blas_fp32(a: torch.Tensor, rows: int, K: int, N: int) -> bool:
-    return (a.dtype == torch.float32 and _BLAS_MIN_ROWS > 0 and rows >= _BLAS_MIN_ROWS
-            and not _ops().narrowf_supported(int(K), int(N)))
+# fp32 GEMMs run on native exact-fp32 kernels: K in {32, 36, 64, 100, 128} with 4 < N <= 112 (every Dense
+# of the LSTM and MLP zoo at the bench shapes) on the register-resident narrow kernel, any other K % 4 == 0
+# up to 320 and any N (the conv critic's im2col GEMMs, K = k C) on the LDS-staged wide kernel
+# (csrc/skinny.hip narrowf_kernel / widef_kernel).
 
 
 def linear(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None, act: int,
            out: torch.Tensor | None = None) -> torch.Tensor:
     """act(x @ W + b) on the last axis. Output dtype = x dtype.  ``out``: a contiguous destination
     of the output's shape (e.g. a row slice of a larger buffer); the result is written there."""
-    if _nat(x) and act == 0 and W.shape[1] > 4 and _blas_fp32(x, x.numel() // x.shape[-1], W.shape[0], W.shape[1]):
-        x2 = _2d(x.contiguous())
-        y = torch.addmm(b, x2, W) if b is not None else torch.mm(x2, W)
-        y = y.reshape(*x.shape[:-1], W.shape[1])
-        return y if out is None else out.copy_(y)
     if _nat(x):
         y = _ops().linear(_2d(x.contiguous()), W, b, int(act), out)
         return y.reshape(*x.shape[:-1], W.shape[1])
@@ -75,8 +61,6 @@ def linear_dgrad(dz: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     if (dz.dtype == torch.float32 and W.dtype == torch.float32 and dz.shape[-1] == 400
             and W.shape[0] <= 112 and _nat(dz)):
         return _ops().lstmf_dgrad(_2d(dz.contiguous()), W.contiguous()).reshape(*dz.shape[:-1], W.shape[0])
-    if _nat(dz) and W.shape[1] > 4 and _blas_fp32(dz, dz.numel() // dz.shape[-1], W.shape[1], W.shape[0]):
-        return torch.mm(_2d(dz.contiguous()), W.t()).reshape(*dz.shape[:-1], W.shape[0])
     if _nat(dz):
         return _ops().linear_dgrad(_2d(dz.contiguous()), W).reshape(*dz.shape[:-1], W.shape[0])
     return torch.matmul(dz, W.t().to(dz.dtype))
