@@ -103,8 +103,10 @@ void launch_linear2(const void* A, const float* W, const float* bias, void* C, i
 // ---- wgrad3.hip (bf16 LDS-DMA streaming LSTM wgrad; Hd == 100, K in {32, 100}; false = use wgrad2) ----
 bool lstm_wgrad3_supported(int M, int K, int Hd, int N);
 size_t lstm_wgrad3_workspace_floats(int K, int Hd, int N);
+// stages: LDS ring depth (4 default, 5 A/B)
 bool launch_lstm_wgrad3(const void* X0, const void* H0, const void* D0, const void* X1, const void* H1, const void* D1,
-                        float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s);
+                        float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s,
+                        int stages = 4);
 
 // ---- skinny.hip (bf16 / fp32, N <= 4 output columns, K % 8 == 0: the Flatten -> Dense(1) critic head) ----
 bool skinny_supported(int K, int N);

@@ -5,11 +5,15 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"
 OUT=gpurun_out/${1:-r04_first}; mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "lstmf or narrowf or tfwd_bitwise" -q --timeout 200 \
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "lstmf or narrowf or tfwd_bitwise or linear or wgrad_fused" -q --timeout 200 \
   --timeout-method thread > $OUT/tests_split.txt 2>&1 || { tail -n 30 $OUT/tests_split.txt; exit 1; }
 tail -n 2 $OUT/tests_split.txt
 timeout -k 10 200 python -u scripts/bench_wgrad.py --dtype float32 --batch 262144 --iters 5 > $OUT/bench_wgrad.jsonl 2>&1 || { tail -n 20 $OUT/bench_wgrad.jsonl; exit 1; }
 cat $OUT/bench_wgrad.jsonl
+timeout -k 10 200 python -u scripts/bench_wgrad.py --dtype bfloat16 --batch 262144 --iters 5 > $OUT/bench_wgrad_bf16.jsonl 2>&1 || { tail -n 20 $OUT/bench_wgrad_bf16.jsonl; exit 1; }
+cat $OUT/bench_wgrad_bf16.jsonl
+timeout -k 10 200 python -u scripts/bench_small.py --iters 100 > $OUT/bench_small.jsonl 2>&1 || { tail -n 20 $OUT/bench_small.jsonl; exit 1; }
+cat $OUT/bench_small.jsonl
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/tests_all.txt 2>&1 \
   || { tail -n 30 $OUT/tests_all.txt; exit 1; }
 tail -n 2 $OUT/tests_all.txt

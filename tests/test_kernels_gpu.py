@@ -421,12 +421,13 @@ def test_trainer_gradients_bf16_fused(cuda, key, T, F, B, lrelu):
         assert rel < BF16_GLOBAL and worst < BF16_BLOCK, (rel, worst, name)
 
 
-@pytest.mark.parametrize("impl", [0, 2])
+@pytest.mark.parametrize("impl", [0, 2, 3])
 @pytest.mark.parametrize("B,T,K,tangent", [(70, 24, 32, False), (33, 24, 100, True), (200, 12, 35, True), (5, 3, 100, False),
                                            (1000, 24, 32, True), (2051, 24, 100, True), (4096, 24, 100, False)])
 def test_lstm_wgrad_fused(cuda, B, T, K, tangent, impl):
     """One-launch LSTM weight gradients vs fp64 products: impl 0 = LDS-DMA streaming kernel
-    (wgrad3.hip) where the shape allows it, impl 2 = the tr-read tile kernel (gemm2.hip)."""
+    (wgrad3.hip) where the shape allows it, impl 2 = the tr-read tile kernel (gemm2.hip), impl 3 =
+    wgrad3 with a 5-deep LDS ring."""
     from hfrep.ops import functional as Fn
 
     H, N = 100, 400
