@@ -173,12 +173,11 @@ void lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<
                               M, K, Tn, ws.data_ptr<float>(), cur_stream(x), (int)impl);
     return;
   }
-  // impl: 0 = auto (LDS-DMA streaming v3 where supported), 2 = force v2 (tests / A-B), 3 = v3 with a 5-deep ring
+  // impl: 0 = auto (LDS-DMA streaming v3 where supported), 2 = force v2 (tests / A-B)
   if (impl != 2 && hfrep::lstm_wgrad3_supported(M, K, Hd, N)) {
     Tensor ws = out_empty({(int64_t)hfrep::lstm_wgrad3_workspace_floats(K, Hd, N)}, x.options().dtype(at::kFloat));
     if (hfrep::launch_lstm_wgrad3(x.data_ptr(), hs.data_ptr(), dZ.data_ptr(), X1, H1, D1, gW.data_ptr<float>(),
-                                  gU.data_ptr<float>(), gbp, M, K, Hd, N, Tn, ws.data_ptr<float>(), cur_stream(x),
-                                  impl == 3 ? 5 : 4))
+                                  gU.data_ptr<float>(), gbp, M, K, Hd, N, Tn, ws.data_ptr<float>(), cur_stream(x)))
       return;
   }
   Tensor ws = out_empty({(int64_t)hfrep::lstm_wgrad2_workspace_floats(M, K, Hd, N)}, x.options().dtype(at::kFloat));

@@ -58,7 +58,7 @@ bool launch_lstmf_tbwd(const float* dH, const float* dHd, const float* tape, con
 // (lstmf_wgrad_workspace_floats) and one fixed-order reduce
 bool lstmf_wgrad_supported(int K, int H, int N);
 // impl: 0 = default (exact under HFREP_FP32_EXACT=1, else the pair split for K <= 36 and the quad split for K = 100), 1 = exact-fp32
-// MFMA, 2 = the three-term bf16 split (pair), 3 = the three-term bf16 split (quad), 4 = pair, pipelined
+// MFMA, 2 = the three-term bf16 split (pair), 3 = the three-term bf16 split (quad)
 size_t lstmf_wgrad_workspace_floats(int M, int K, int impl = 0);
 bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
                         float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl = 0);
@@ -103,10 +103,8 @@ void launch_linear2(const void* A, const float* W, const float* bias, void* C, i
 // ---- wgrad3.hip (bf16 LDS-DMA streaming LSTM wgrad; Hd == 100, K in {32, 100}; false = use wgrad2) ----
 bool lstm_wgrad3_supported(int M, int K, int Hd, int N);
 size_t lstm_wgrad3_workspace_floats(int K, int Hd, int N);
-// stages: LDS ring depth (4 default, 5 A/B)
 bool launch_lstm_wgrad3(const void* X0, const void* H0, const void* D0, const void* X1, const void* H1, const void* D1,
-                        float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s,
-                        int stages = 4);
+                        float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s);
 
 // ---- skinny.hip (bf16 / fp32, N <= 4 output columns, K % 8 == 0: the Flatten -> Dense(1) critic head) ----
 bool skinny_supported(int K, int N);

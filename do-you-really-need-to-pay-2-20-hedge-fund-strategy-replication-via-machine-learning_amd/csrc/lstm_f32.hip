@@ -1583,274 +1583,6 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// split weight gradient, column PAIR, pipelined: lstmf_wgrad_p2_kernel
-// ------------------------------------------------------------------------------------------
-// lstmf_wgrad_q4_kernel splits every A row [x | h_{t-1} | 1] (201 values at K = 100) in FOUR workgroups
-// (one per 100-column quarter of D) and adds each tile's six products to its running sum in VALU: ~3.4
-// VALU instructions per MFMA, so VALU issue, not the matrix pipe, set its pace (46 % MFMA busy,
-// profiles/r03_end/pmc_fp32.txt).  Here a workgroup PAIR shares a row range (blocks b, b + 8: one XCD,
-// the A rows both stage come from one L2) and splits the 400 gate columns in 208 + 192 (13 j-tiles
-// each, the second part's last one zero): every A value is split twice instead of four times and every
-// D value once (~1.8 VALU per MFMA).  Both double-buffered stages fit the 160 KiB at a 416-byte plane row
-// (104 dwords = 40 mod 64: the 8 consecutive rows of a tr-read lane group land on 8 distinct 8-bank
-// groups, conflict-free like the 8 mod 64 strides).  8 waves, two per SIMD: SIMD s owns j-tiles
-// 3 s .. 3 s + 2 for every i-tile (one A fragment read feeds three j-tiles) plus a quarter of j-tile 12's
-// i-tiles (43 / 42 / 42 / 42 tiles at K = 100); its two waves split the i-tiles (7 / 6 + the j-tile-12
-// share: 21 / 22 tiles).  Registers (256 per wave): the running sums in VGPRs (the VALU adds), the B
-// fragments and the staging set in VGPRs too (no AGPRs: the compiler then halves the VGPR budget).  Pipelined as q4: chunk c + 1's rows are split
-// into the other LDS buffer in slices between chunk c's i-tiles, each slot reloaded with chunk c + 2
-// right after; each tile's six products go to a fresh accumulator added to the running sum in VALU fp32.
-constexpr int WP_CD = 208, WP_RB = 416;  // D columns of a part (the second: 192 real), plane row bytes
-template <int KX>
-struct WPGeo {
-  static constexpr int KR = KX + FH + 1;
-  static constexpr int NI = (KR + 15) / 16;
-  // staging map: per operand (x, h, D) a thread owns ONE float4 column c of rows r0, r0 + R, r0 + 2 R, ..
-  // (R = 256 / float4s per row): its bases are computed once, slot k = base + k R rows (no per-slot
-  // division to keep or recompute)
-  static constexpr int NCX = KX / 4, NCH = FH / 4, NCD = WP_CD / 4;  // float4 per row
-  static constexpr int RX = 512 / NCX, RH = 512 / NCH, RD = 512 / NCD;  // rows per pass
-  static constexpr int JX = (32 + RX - 1) / RX, JH = (32 + RH - 1) / RH, JD = (32 + RD - 1) / RD;
-  static constexpr int NIA = (NI + 1) / 2;  // i-tiles of waves 0..3 (waves 4..7: the rest + j-tile 12's share)
-  static constexpr int NS = JX + JH + JD;  // float4 staging slots per thread
-  static constexpr int PL = 32 * WP_RB;    // bytes per plane image
-  static constexpr int IMGD = 3 * PL;      // D image offset in a stage
-  static constexpr int BUF = 6 * PL;       // one stage: A and D images, three planes each
-  static_assert(KX % 4 == 0 && 16 * NI <= WP_CD && 2 * BUF <= 160 * 1024, "wgrad p2: K / LDS");
-  // j-tile 12's i-tiles of SIMD s: [q0(s), q0(s + 1))
-  static constexpr int q0(int s) { return s * (NI / 4) + (s < NI % 4 ? s : NI % 4); }
-  static constexpr int MAXT = 3 * NIA > 3 * (NI - NIA) + q0(1) ? 3 * NIA : 3 * (NI - NIA) + q0(1);  // tiles per wave
-};
-
-template <int KX>
-__global__ void __launch_bounds__(512, 1)
-lstmf_wgrad_p2_kernel(const float* __restrict__ X, const float* __restrict__ Hs, const float* __restrict__ D,
-                      const float* __restrict__ Xd, const float* __restrict__ Hds, const float* __restrict__ Dd,
-                      float* __restrict__ slab, int M, int Tn, int rows_per_z, int Z) {
-  using G = WPGeo<KX>;
-  constexpr int NI = G::NI, JX = G::JX, JH = G::JH, NS = G::NS, MAXT = G::MAXT;
-  extern __shared__ __attribute__((aligned(16))) char wsm_[];
-  lds_char* wsm = (lds_char*)wsm_;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // block -> (row range z, column part jh); with Z % 8 == 0 the pair shares an XCD (b, b + 8)
-  int z, jh;
-  if (Z % 8 == 0) {
-    const int slot = blockIdx.x >> 3;
-    jh = slot & 1;
-    z = (slot >> 1) * 8 + (blockIdx.x & 7);
-  } else {
-    jh = blockIdx.x & 1;
-    z = blockIdx.x >> 1;
-  }
-  const int mb = z * rows_per_z, me = min(M, mb + rows_per_z);
-  const int jbase = WP_CD * jh, nd4 = jh ? (FG - WP_CD) / 4 : WP_CD / 4;  // D float4 per row of this part
-
-  for (int i = tid; i < 2 * G::BUF / 16; i += 512) reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(wsm)[i] = u32x4_t{0, 0, 0, 0};
-  __syncthreads();
-
-  f32x4 acc[MAXT];
-#pragma unroll
-  for (int a = 0; a < MAXT; ++a) {
-    acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
-    asm volatile("" : "+v"(acc[a]));  // (running sums in VGPRs: the VALU adds read and write them)
-  }
-
-  // per-buffer lane bases of the transposed reads (opaque: folded into the reads' 16-bit immediates the
-  // buffer / image offsets overflowed them)
-  int tro_a[2], tro_d[2];
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    tro_a[b] = tr_lane_off(lane, WP_RB) + b * G::BUF;
-    tro_d[b] = tr_lane_off(lane, WP_RB) + b * G::BUF + G::IMGD;
-    asm volatile("" : "+v"(tro_a[b]), "+v"(tro_d[b]));
-  }
-  const int step32 = 32 % Tn;
-
-  // per operand (x, h, D) this thread's first row and float4 column, packed (r0 << 8 | c; r0 = 255:
-  // no slot).  They pass through an opaque copy at every chunk: hoisted out of the chunk loop, the
-  // per-slot offset / range selections (two chunk parities x two segments x NS slots) were loop
-  // invariants the compiler kept -- and spilled (371 registers at K = 100)
-  int pk[3];
-  {
-    const int rx0 = tid / G::NCX, rh0 = tid / G::NCH, rd0 = tid / G::NCD, cd0 = tid - rd0 * G::NCD;
-    pk[0] = tid < G::RX * G::NCX ? (rx0 << 8) | (tid - rx0 * G::NCX) : 255 << 8;
-    pk[1] = tid < G::RH * G::NCH ? (rh0 << 8) | (tid - rh0 * G::NCH) : 255 << 8;
-    pk[2] = tid < G::RD * G::NCD && cd0 < nd4 ? (rd0 << 8) | cd0 : 255 << 8;
-  }
-  // slot s -> (row, float4 column, active); rows >= 32 (the last pass) are inactive
-  auto slot_row = [&](int s, int& r, int& c, bool& ok) __attribute__((always_inline)) {
-    const int ty = s < JX ? 0 : s < JX + JH ? 1 : 2, k = s < JX ? s : s < JX + JH ? s - JX : s - JX - JH;
-    const int R = ty == 0 ? G::RX : ty == 1 ? G::RH : G::RD;
-    c = pk[ty] & 255;
-    r = (pk[ty] >> 8) + R * k;
-    ok = r < 32;
-  };
-
-  f32x4 v[NS];
-  for (int seg = 0; seg < (Xd ? 2 : 1); ++seg) {
-    const float* Xs = seg ? Xd : X;
-    const float* Hq = seg ? Hds : Hs;
-    const float* Dq = seg ? Dd : D;
-    const int nr = me > mb ? me - mb : 0;
-    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * KX, nr * KX * 4);
-    // (row mb - 1 based: every voffset >= 0; h_{-1} rows are masked by t)
-    const rsrc_t rh = make_rsrc(Hq + ((ptrdiff_t)mb - 1) * FH, (nr ? nr + 1 : 0) * FH * 4);
-    const rsrc_t rd = make_rsrc(Dq + (size_t)mb * FG + jbase, nr ? ((nr - 1) * FG + 4 * nd4) * 4 : 0);
-    int tm[JH];  // (row mod Tn) of this thread's H slots at the next chunk to load
-#pragma unroll
-    for (int j = 0; j < JH; ++j) tm[j] = (mb + (pk[1] >> 8) + G::RH * j) % Tn;
-    auto load_slot = [&](int s, int m0) __attribute__((always_inline)) {
-      int r, c;
-      bool ok;
-      slot_row(s, r, c, ok);
-      ok = ok && r < me - m0;
-      if (s < JX) {
-        v[s] = ld4s(rx, ok ? (r * KX + 4 * c) * 4 : kOOB, (m0 - mb) * KX * 4);
-      } else if (s < JX + JH) {
-        int& tmj = tm[s - JX];
-        v[s] = ld4s(rh, ok && tmj != 0 ? (r * FH + 4 * c) * 4 : kOOB, (m0 - mb) * FH * 4);
-        tmj += step32;
-        if (tmj >= Tn) tmj -= Tn;
-      } else {
-        v[s] = ld4s(rd, ok ? (r * FG + 4 * c) * 4 : kOOB, (m0 - mb) * FG * 4);
-      }
-    };
-    auto stage = [&](lds_char* base, int s) __attribute__((always_inline)) {
-      int r, c;
-      bool ok;
-      slot_row(s, r, c, ok);
-      if (!ok) return;
-      uint32_t p[3][2];
-      split3(v[s], p);
-      const int lo = s < JX ? r * WP_RB + 8 * c : s < JX + JH ? r * WP_RB + 2 * KX + 8 * c : G::IMGD + r * WP_RB + 8 * c;
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(base + lo + q * G::PL) = u32x2_t{p[q][0], p[q][1]};
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    if (tid < 64) {  // bias column KR - 1: 1 in plane h for the primal segment, 0 for the tangent one
-      const int buf = tid >> 5, r = tid & 31;
-      *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wsm + buf * G::BUF + r * WP_RB + (G::KR - 1) * 2) =
-          seg ? 0 : 0x3f80;
-    }
-    const int nch = nr > 0 ? (nr + 31) / 32 : 0;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) load_slot(s, mb);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) stage(wsm, s);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) load_slot(s, mb + 32);
-    __syncthreads();
-    auto chunk = [&](auto S_, int c) __attribute__((always_inline)) {
-      constexpr int S = decltype(S_)::value;
-      asm volatile("" : "+v"(pk[0]), "+v"(pk[1]), "+v"(pk[2]));
-      const lds_char* A_ = wsm;  // (+ S BUF in tro_a[S], + S BUF + IMGD in tro_d[S])
-      lds_char* nxt = wsm + (S ^ 1) * G::BUF;
-      // one straight-line body per wave (no branch between an MFMA and the VALU read of its result)
-      auto body = [&](auto WK) __attribute__((always_inline)) {
-        constexpr int W = decltype(WK)::value;
-        constexpr int SM = W & 3, H = W >> 2;
-        constexpr int I0 = H ? G::NIA : 0, NIW = H ? NI - G::NIA : G::NIA;  // main i range
-        constexpr int Q0 = G::q0(SM), NQ = H ? G::q0(SM + 1) - G::q0(SM) : 0;  // j-tile 12's share (waves 4..7)
-        // passes over the wave's i-tiles, each with the B fragments of one or two j-tiles in registers (the A
-        // fragments are re-read per pass): K <= 36 (3, 3 + 1 ... ) j-tiles (3 SM, 3 SM + 1) then 3 SM + 2;
-        // K = 100 one j-tile per pass (its 22 running sums leave no room for a second B fragment set)
-        constexpr int NP = NI > 9 ? 3 : 2;           // passes
-        constexpr int NIT = NP * NIW + NQ;           // A-fragment iterations per chunk
-        constexpr int SPI = (NS + NIT - 1) / NIT;    // staging slots per iteration
-        auto tile6 = [&](const bf16x8 (&a3)[3], const bf16x8 (&b3)[3], f32x4& acc_) __attribute__((always_inline)) {
-          f32x4 t = mma32(a3[2], b3[0], f32x4{0.f, 0.f, 0.f, 0.f});  // lh
-          t = mma32(a3[0], b3[2], t);                                 // hl
-          t = mma32(a3[1], b3[1], t);                                 // mm
-          t = mma32(a3[1], b3[0], t);                                 // mh
-          t = mma32(a3[0], b3[1], t);                                 // hm
-          t = mma32(a3[0], b3[0], t);                                 // hh
-          acc_ += t;
-          asm volatile("" : "+v"(acc_));
-        };
-        auto pass = [&](auto P_) __attribute__((always_inline)) {
-          constexpr int P = decltype(P_)::value;
-          constexpr int NJP = NP == 3 ? 1 : (P == 0 ? 2 : 1);   // main j-tiles of this pass
-          constexpr int JP0 = NP == 3 ? P : 2 * P;              // first main j-tile (offset from 3 SM)
-          constexpr bool LAST = P == NP - 1;
-          bf16x8 bfr[NP == 3 ? 1 : 2][3];
-#pragma unroll
-          for (int jj = 0; jj < NJP; ++jj)
-#pragma unroll
-            for (int q = 0; q < 3; ++q) bfr[jj][q] = tr_frag<WP_RB>(A_ + q * G::PL, tro_d[S], 16 * (3 * SM + JP0 + jj));
-          constexpr int NI_P = LAST ? NIW + NQ : NIW;
-#pragma unroll
-          for (int ii = 0; ii < NI_P; ++ii) {
-            __builtin_amdgcn_sched_barrier(0);
-            const bool share = ii >= NIW;  // (compile-time) j-tile 12 at i-tile Q0 + ii - NIW
-            if (share && ii == NIW) {
-#pragma unroll
-              for (int q = 0; q < 3; ++q) bfr[NJP - 1][q] = tr_frag<WP_RB>(A_ + q * G::PL, tro_d[S], 16 * 12);
-            }
-            bf16x8 a3[3];
-#pragma unroll
-            for (int q = 0; q < 3; ++q)
-              a3[q] = tr_frag<WP_RB>(A_ + q * G::PL, tro_a[S], 16 * (share ? Q0 + ii - NIW : I0 + ii));
-            if (!share) {
-#pragma unroll
-              for (int jj = 0; jj < NJP; ++jj) tile6(a3, bfr[jj], acc[3 * ii + JP0 + jj]);
-            } else {
-              tile6(a3, bfr[NJP - 1], acc[3 * NIW + ii - NIW]);
-            }
-            const int it = P * NIW + ii;
-#pragma unroll
-            for (int s = it * SPI; s < (it + 1) * SPI && s < NS; ++s) {
-              stage(nxt, s);
-              load_slot(s, mb + 32 * (c + 2));
-            }
-          }
-        };
-        pass(std::integral_constant<int, 0>{});
-        pass(std::integral_constant<int, 1>{});
-        if constexpr (NP == 3) pass(std::integral_constant<int, 2>{});
-      };
-      switch (w) {
-        case 0: body(std::integral_constant<int, 0>{}); break;
-        case 1: body(std::integral_constant<int, 1>{}); break;
-        case 2: body(std::integral_constant<int, 2>{}); break;
-        case 3: body(std::integral_constant<int, 3>{}); break;
-        case 4: body(std::integral_constant<int, 4>{}); break;
-        case 5: body(std::integral_constant<int, 5>{}); break;
-        case 6: body(std::integral_constant<int, 6>{}); break;
-        default: body(std::integral_constant<int, 7>{}); break;
-      }
-      __syncthreads();
-    };
-    int c = 0;
-    for (; c + 1 < nch; c += 2) {
-      chunk(I0{}, c);
-      chunk(I1{}, c + 1);
-    }
-    if (c < nch) chunk(I0{}, c);
-    __syncthreads();  // (the bias column of both buffers is rewritten for the next segment)
-  }
-  // slab store: acc[3 ii + jj] -> (i-tile I0 + ii, j-tile 3 sm + jj); acc[3 NIW + k] -> (i-tile q0(sm) + k, j-tile 12)
-  float* out = slab + (size_t)z * G::KR * FG;
-  const int g = lane >> 4, c16 = lane & 15, sm = w & 3, hh = w >> 2;
-  const int i0w = hh ? G::NIA : 0, niw = hh ? NI - G::NIA : G::NIA;
-  const int q0w = G::q0(sm), nq = hh ? G::q0(sm + 1) - G::q0(sm) : 0;
-  const int ncol = jh ? FG - WP_CD : WP_CD;
-#pragma unroll
-  for (int a = 0; a < MAXT; ++a) {
-    const bool main = a < 3 * niw, share = !main && a - 3 * niw < nq;
-    const int it = main ? i0w + a / 3 : q0w + (a - 3 * niw), jt = main ? 3 * sm + a % 3 : 12;
-    const int col = 16 * jt + c16;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = 16 * it + 4 * g + r;
-      if ((main || share) && i < G::KR && col < ncol) out[(size_t)i * FG + jbase + col] = acc[a][r];
-    }
-  }
-}
-
 constexpr int DS_KS = 13;  // the 400 gate columns as 13 k-steps of 32 (k = 400..415 zero)
 
 // ==========================================================================================
@@ -2757,42 +2489,24 @@ static int wgrads_z(int M) {
   const int chunks = (M + 31) / 32, half = device_cu_count() / 2;
   return chunks < half ? chunks : half;
 }
-// pair-pipelined kernel: Z row ranges x 2 column parts, one workgroup per CU
-static int wgradp_z(int M) { return wgrads_z(M); }
 // quad kernel: Z row ranges x 4 column quarters, one workgroup per CU
 static int wgradq_z(int M) {
   const int chunks = (M + 31) / 32, q = device_cu_count() / 4;
   return chunks < q ? chunks : q;
 }
 static int wgradf_pick(int impl, int K) {
-  const int v = impl >= 1 && impl <= 4 ? impl : wgradf_version();
+  const int v = impl >= 1 && impl <= 3 ? impl : wgradf_version();
   return v ? v : (K <= 36 ? 2 : 3);
 }
 size_t lstmf_wgrad_workspace_floats(int M, int K, int impl) {
   const int v = wgradf_pick(impl, K);
-  const int z = v == 1 ? wgradf_grid(M) : v == 3 ? wgradq_z(M) : v == 4 ? wgradp_z(M) : wgrads_z(M);
+  const int z = v == 1 ? wgradf_grid(M) : v == 3 ? wgradq_z(M) : wgrads_z(M);
   return (size_t)z * (K + FH + 1) * FG;
 }
 
 bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
                         float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl) {
   if (!lstmf_wgrad_supported(K, FH, FG) || M <= 0) return false;
-  if (wgradf_pick(impl, K) == 4) {
-    const int z0 = wgradp_z(M);
-    const int rpz = ((M + z0 - 1) / z0 + 31) / 32 * 32;
-    const int z = (M + rpz - 1) / rpz;
-    auto go = [&](auto k, size_t sm) {
-      allow_lds(reinterpret_cast<const void*>(k));
-      hipLaunchKernelGGL(k, dim3(2 * z), dim3(512), sm, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpz, z);
-    };
-    switch (K) {
-      case 32: go(lstmf_wgrad_p2_kernel<32>, 2 * WPGeo<32>::BUF); break;
-      case 36: go(lstmf_wgrad_p2_kernel<36>, 2 * WPGeo<36>::BUF); break;
-      default: go(lstmf_wgrad_p2_kernel<100>, 2 * WPGeo<100>::BUF); break;
-    }
-    launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s);
-    return true;
-  }
   if (wgradf_pick(impl, K) == 3) {
     const int z0 = wgradq_z(M);
     const int rpz = ((M + z0 - 1) / z0 + 31) / 32 * 32;

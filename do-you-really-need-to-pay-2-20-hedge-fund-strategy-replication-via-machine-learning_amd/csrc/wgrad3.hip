@@ -33,9 +33,10 @@ namespace {
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
+constexpr int W3_STAGES = 4;
 constexpr int W3_WAVES = 8;
 
-template <int K, int HD, int W3_STAGES = 4>  // W3_STAGES: LDS ring depth
+template <int K, int HD>
 struct W3 {
   static constexpr int N = 4 * HD;
   static constexpr int JT = 208;  // j-tile: 13 x 16 columns; two tiles cover N <= 416
@@ -91,12 +92,12 @@ __device__ __forceinline__ bf16x8 tr2(uint32_t lo, uint32_t hi) {
 
 }  // namespace
 
-template <int K, int HD, int W3_STAGES>
+template <int K, int HD>
 __global__ void __launch_bounds__(512, 1)
 lstm_wgrad3_kernel(const bf16_t* __restrict__ X0, const bf16_t* __restrict__ H0, const bf16_t* __restrict__ D0,
                    const bf16_t* __restrict__ X1, const bf16_t* __restrict__ H1, const bf16_t* __restrict__ D1,
                    float* __restrict__ slab, int M, int Tn, int nseg, int rps) {
-  using G = W3<K, HD, W3_STAGES>;
+  using G = W3<K, HD>;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -255,20 +256,20 @@ lstm_wgrad3_kernel(const bf16_t* __restrict__ X0, const bf16_t* __restrict__ H0,
   }
 }
 
-template <int K, int HD, int S>
+template <int K, int HD>
 static void run_wgrad3(const void* X0, const void* H0, const void* D0, const void* X1, const void* H1, const void* D1,
                        float* gW, float* gU, float* gb, int M, int Tn, int nsplit, float* ws, hipStream_t s) {
-  using G = W3<K, HD, S>;
+  using G = W3<K, HD>;
   int rps = (M + nsplit - 1) / nsplit;
   rps = (rps + 31) / 32 * 32;
   const int nseg = X1 ? 2 : 1;
   static bool attr = false;
   if (!attr) {
-    HFREP_CHECK_HIP(hipFuncSetAttribute((const void*)lstm_wgrad3_kernel<K, HD, S>,
+    HFREP_CHECK_HIP(hipFuncSetAttribute((const void*)lstm_wgrad3_kernel<K, HD>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
     attr = true;
   }
-  hipLaunchKernelGGL((lstm_wgrad3_kernel<K, HD, S>), dim3(nsplit * G::NJT), dim3(512), G::LDS, s, (const bf16_t*)X0,
+  hipLaunchKernelGGL((lstm_wgrad3_kernel<K, HD>), dim3(nsplit * G::NJT), dim3(512), G::LDS, s, (const bf16_t*)X0,
                      (const bf16_t*)H0, (const bf16_t*)D0, (const bf16_t*)X1, (const bf16_t*)H1, (const bf16_t*)D1, ws,
                      M, Tn, nseg, rps);
   launch_lstm_wgrad2_reduce(ws, gW, gU, gb, nsplit, K, HD, G::N, s);
@@ -289,20 +290,14 @@ bool lstm_wgrad3_supported(int M, int K, int Hd, int N) {
 size_t lstm_wgrad3_workspace_floats(int K, int Hd, int N) { return (size_t)wgrad3_splits() * (K + Hd + 1) * N; }
 
 bool launch_lstm_wgrad3(const void* X0, const void* H0, const void* D0, const void* X1, const void* H1, const void* D1,
-                        float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s,
-                        int stages) {
+                        float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s) {
   if (M <= 0) return true;
   if (!lstm_wgrad3_supported(M, K, Hd, N)) return false;
   auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (!(al(X0) && al(H0) && al(D0) && al(X1) && al(H1) && al(D1))) return false;
   const int ns = wgrad3_splits();
-  if (stages == 5) {
-    if (K == 32) run_wgrad3<32, 100, 5>(X0, H0, D0, X1, H1, D1, gW, gU, gb, M, Tn, ns, ws, s);
-    else run_wgrad3<100, 100, 5>(X0, H0, D0, X1, H1, D1, gW, gU, gb, M, Tn, ns, ws, s);
-    return true;
-  }
-  if (K == 32) run_wgrad3<32, 100, 4>(X0, H0, D0, X1, H1, D1, gW, gU, gb, M, Tn, ns, ws, s);
-  else run_wgrad3<100, 100, 4>(X0, H0, D0, X1, H1, D1, gW, gU, gb, M, Tn, ns, ws, s);
+  if (K == 32) run_wgrad3<32, 100>(X0, H0, D0, X1, H1, D1, gW, gU, gb, M, Tn, ns, ws, s);
+  else run_wgrad3<100, 100>(X0, H0, D0, X1, H1, D1, gW, gU, gb, M, Tn, ns, ws, s);
   return true;
 }
 

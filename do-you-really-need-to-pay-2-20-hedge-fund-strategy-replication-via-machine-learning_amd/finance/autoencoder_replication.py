@@ -125,8 +125,9 @@ class AETrainer:
         k = self.model.latent_dim
         orders = np.stack([rs.permutation(split) if shuffle else np.arange(split) for _ in range(epochs)])
         dev = self.device
-        xt = torch.as_tensor(x[:split], dtype=torch.float32, device=dev)
-        xv = torch.as_tensor(x[split:], dtype=torch.float32, device=dev).reshape(-1, A)
+        # row-major copies: the scaler's output can be column-major (MinMaxScaler keeps Fortran order)
+        xt = torch.as_tensor(np.ascontiguousarray(x[:split]), dtype=torch.float32, device=dev).contiguous()
+        xv = torch.as_tensor(np.ascontiguousarray(x[split:]), dtype=torch.float32, device=dev).reshape(-1, A).contiguous()
         order_t = torch.as_tensor(orders.astype(np.int32), device=dev)
         nw = A * k
         (mWe, vWe), (mWd, vWd) = self.opt._slots(enc.flat), self.opt._slots(dec.flat)

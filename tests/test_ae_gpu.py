@@ -27,7 +27,8 @@ def test_ae_trainer_gpu_vs_cpu(cuda, dt, tol, k, fused):
     with torch.no_grad():
         for a, b in zip(mg.parts(), mc.parts()):
             b.flat.copy_(a.flat.double().cpu())
-    hg = AETrainer(mg, device=cuda).fit(x, epochs=5, patience=100, seed=9, dtype=dt, fused=fused)
+    # column-major input, as MinMaxScaler returns it (the fused fit must take any layout)
+    hg = AETrainer(mg, device=cuda).fit(np.asfortranarray(x), epochs=5, patience=100, seed=9, dtype=dt, fused=fused)
     hc = AETrainer(mc).fit(x, epochs=5, patience=100, seed=9, dtype=torch.float64)
     np.testing.assert_allclose(hg["loss"], hc["loss"], rtol=tol * 10, atol=1e-7)
     for a, b in zip(mg.parts(), mc.parts()):

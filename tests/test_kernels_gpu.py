@@ -421,13 +421,12 @@ def test_trainer_gradients_bf16_fused(cuda, key, T, F, B, lrelu):
         assert rel < BF16_GLOBAL and worst < BF16_BLOCK, (rel, worst, name)
 
 
-@pytest.mark.parametrize("impl", [0, 2, 3])
+@pytest.mark.parametrize("impl", [0, 2])
 @pytest.mark.parametrize("B,T,K,tangent", [(70, 24, 32, False), (33, 24, 100, True), (200, 12, 35, True), (5, 3, 100, False),
                                            (1000, 24, 32, True), (2051, 24, 100, True), (4096, 24, 100, False)])
 def test_lstm_wgrad_fused(cuda, B, T, K, tangent, impl):
     """One-launch LSTM weight gradients vs fp64 products: impl 0 = LDS-DMA streaming kernel
-    (wgrad3.hip) where the shape allows it, impl 2 = the tr-read tile kernel (gemm2.hip), impl 3 =
-    wgrad3 with a 5-deep LDS ring."""
+    (wgrad3.hip) where the shape allows it, impl 2 = the tr-read tile kernel (gemm2.hip)."""
     from hfrep.ops import functional as Fn
 
     H, N = 100, 400
@@ -820,7 +819,7 @@ def test_lstmf_wgrad_fused(cuda, B, T, K, tangent):
                                            (41, 5, 36, True), (1000, 24, 100, True), (4500, 24, 32, False),
                                            (20000, 24, 100, True)])
 def test_lstmf_wgrad_split_vs_exact(cuda, B, T, K, tangent):
-    """The three-term bf16 split weight gradients (impl 2 pair, 3 quad, 4 pair pipelined) and the exact-fp32
+    """The three-term bf16 split weight gradients (impl 2 pair, 3 quad) and the exact-fp32
     MFMA kernel (impl 1) vs fp64: all inside the fp32 tolerance and the splits' error within 2x the exact
     kernel's (the dropped split terms are <= 2^-24 of each product); bitwise run-to-run."""
     from hfrep.ops import functional as Fn
@@ -836,7 +835,7 @@ def test_lstmf_wgrad_split_vs_exact(cuda, B, T, K, tangent):
         rW = rW + xd.double().reshape(-1, K).t() @ dzd.double().reshape(-1, N)
         rU = rU + R.shift_prev(hds.double()).reshape(-1, H).t() @ dzd.double().reshape(-1, N)
     errs = {}
-    for impl in (1, 2, 2, 3, 3, 4, 4):
+    for impl in (1, 2, 2, 3, 3):
         gW, gU, gb = torch.zeros(K, N, device=cuda), torch.zeros(H, N, device=cuda), torch.zeros(N, device=cuda)
         Fn.lstm_wgrad_(x, hs, dz, gW, gU, gb, xd, hds, dzd, impl=impl)
         out = torch.cat([gW.reshape(-1), gU.reshape(-1), gb])
@@ -846,11 +845,10 @@ def test_lstmf_wgrad_split_vs_exact(cuda, B, T, K, tangent):
         ref = torch.cat([rW.reshape(-1), rU.reshape(-1), rb])
         errs[impl] = ((out.double() - ref).abs().max().item(), out)
     refmax = max(rW.abs().max().item(), rU.abs().max().item(), rb.abs().max().item())
-    e1, e2, e3, e4 = errs[1][0], errs[2][0], errs[3][0], errs[4][0]
-    print(f"max abs err exact {e1:.3e} split {e2:.3e} quad split {e3:.3e} pair pipelined {e4:.3e} (max |ref| {refmax:.3e})")
+    e1, e2, e3 = errs[1][0], errs[2][0], errs[3][0]
+    print(f"max abs err exact {e1:.3e} split {e2:.3e} quad split {e3:.3e} (max |ref| {refmax:.3e})")
     assert e1 <= 1e-5 * refmax + 1e-5 and e2 <= 2 * e1 + 1e-6 * refmax, (e1, e2, refmax)
     assert e3 <= 2 * e1 + 1e-6 * refmax, (e1, e3, refmax)
-    assert e4 <= 2 * e1 + 1e-6 * refmax, (e1, e4, refmax)
 
 
 @pytest.mark.parametrize("K,tangent", [(100, False), (32, True)])
@@ -873,7 +871,7 @@ def test_lstmf_wgrad_large_m(cuda, K, tangent):
     rb = dz.double().reshape(-1, N).sum(0)
     # random-sign sums of 3 M products: scale by the root-sum-square, not the absolute sum
     tol = 2e-5 * (B * T) ** 0.5 * (2 if tangent else 1)
-    for impl in (1, 2, 3, 4):
+    for impl in (1, 2, 3):
         gW, gU, gb = (torch.zeros(K, N, device=cuda), torch.zeros(H, N, device=cuda), torch.zeros(N, device=cuda))
         Fn.lstm_wgrad_(x, hs, dz, gW, gU, gb, xd, hds, dzd, impl=impl)
         for got, ref in ((gW, rW), (gU, rU), (gb, rb)):
