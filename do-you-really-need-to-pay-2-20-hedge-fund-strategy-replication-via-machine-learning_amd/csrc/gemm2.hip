@@ -144,8 +144,8 @@ lstm_wgrad2_kernel(const bf16_t* __restrict__ X0, const bf16_t* __restrict__ H0,
 
 __global__ void __launch_bounds__(256)
 lstm_wgrad2_reduce_kernel(const float* __restrict__ slab, float* __restrict__ gW, float* __restrict__ gU,
-                          float* __restrict__ gb, int splits, int K, int Hd, int N) {
-  const int Ktot = K + Hd + 1;
+                          float* __restrict__ gb, int splits, int K, int Hd, int N, int Ks) {
+  const int Ktot = Ks + Hd + 1;  // slab rows: Ks >= K input rows (rows K .. Ks - 1 padding, dropped)
   const int64_t total = (int64_t)Ktot * N;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // 4 independent chains: loads stay in flight
@@ -160,7 +160,8 @@ lstm_wgrad2_reduce_kernel(const float* __restrict__ slab, float* __restrict__ gW
     const float s = (s0 + s1) + (s2 + s3);
     const int i = (int)(e / N), j = (int)(e % N);
     if (i < K) gW[(size_t)i * N + j] += s;
-    else if (i < K + Hd) gU[(size_t)(i - K) * N + j] += s;
+    else if (i < Ks) continue;
+    else if (i < Ks + Hd) gU[(size_t)(i - Ks) * N + j] += s;
     else if (gb) gb[j] += s;
   }
 }
@@ -194,10 +195,11 @@ void launch_lstm_wgrad2(const void* X0, const void* H0, const void* D0, const vo
 }
 
 void launch_lstm_wgrad2_reduce(const float* ws, float* gW, float* gU, float* gb, int splits, int K, int Hd, int N,
-                               hipStream_t s) {
-  const int64_t total = (int64_t)(K + Hd + 1) * N;
+                               hipStream_t s, int Ks) {
+  if (Ks < K) Ks = K;
+  const int64_t total = (int64_t)(Ks + Hd + 1) * N;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 1024);
-  hipLaunchKernelGGL(lstm_wgrad2_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, gW, gU, gb, splits, K, Hd, N);
+  hipLaunchKernelGGL(lstm_wgrad2_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, gW, gU, gb, splits, K, Hd, N, Ks);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -94,9 +94,10 @@ void launch_wgrad(int dt, const void* X, const void* D, float* gW, float* gb, in
 size_t lstm_wgrad2_workspace_floats(int M, int K, int Hd, int N);
 void launch_lstm_wgrad2(const void* X0, const void* H0, const void* D0, const void* X1, const void* H1, const void* D1,
                         float* gW, float* gU, float* gb, int M, int K, int Hd, int N, int Tn, float* ws, hipStream_t s);
-// split-slab reduce shared by wgrad2 / wgrad3: rows 0..K-1 -> gW, K..K+Hd-1 -> gU, K+Hd -> gb (if non-null)
+// split-slab reduce shared by wgrad2 / wgrad3 / the fp32 kernels: slab rows 0..K-1 -> gW, Ks..Ks+Hd-1 -> gU,
+// Ks+Hd -> gb (if non-null); Ks (default K) > K: rows K..Ks-1 are image padding (K = 35 in a 36-row image)
 void launch_lstm_wgrad2_reduce(const float* ws, float* gW, float* gU, float* gb, int splits, int K, int Hd, int N,
-                               hipStream_t s);
+                               hipStream_t s, int Ks = 0);
 void launch_linear2(const void* A, const float* W, const float* bias, void* C, int M, int N, int K, int w_trans, int act,
                     hipStream_t s);
 

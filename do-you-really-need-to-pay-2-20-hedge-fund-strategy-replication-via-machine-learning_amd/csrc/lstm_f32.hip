@@ -174,6 +174,21 @@ __device__ __forceinline__ f32x4 ld4(rsrc_t r, int voff) {
 __device__ __forceinline__ f32x4 ld4s(rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
+// one float4 of an X row of XR floats at byte offset voff (+ soff), columns col .. col + 3: one 16-byte
+// load when rows are 16-byte aligned; for XR = 35 (the reference's 35 features, staged as a 36-column
+// image) four dword loads with the columns >= XR reading zero -- no byte past the row is addressed
+template <int XR>
+__device__ __forceinline__ f32x4 ldx4(rsrc_t r, int voff, int soff, int col) {
+  if constexpr (XR % 4 == 0) {
+    return ld4s(r, voff, soff);
+  } else {
+    f32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff != kOOB && col + i < XR ? voff + 4 * i : kOOB, soff, 0));
+    return v;
+  }
+}
 __device__ __forceinline__ void st4(f32x4 v, rsrc_t r, int voff) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), r, voff, 0, 0);
 }
@@ -875,7 +890,7 @@ struct WFGeo {
   static constexpr int JX = (NX4 + 511) / 512, JH = (NH4 + 511) / 512, JD = (ND4 + 511) / 512;
 };
 
-template <int KX>
+template <int KX, int XR = KX>  // XR: X row stride in floats (35: a 36-column image, column 35 zero)
 __global__ void __launch_bounds__(512)
 lstmf_wgrad_kernel(const float* __restrict__ X, const float* __restrict__ Hs, const float* __restrict__ D,
                    const float* __restrict__ Xd, const float* __restrict__ Hds, const float* __restrict__ Dd,
@@ -908,7 +923,7 @@ lstmf_wgrad_kernel(const float* __restrict__ X, const float* __restrict__ Hs, co
     // descriptors based at this workgroup's first row (row mb - 1 for the shifted H): the byte
     // offsets stay 32-bit however large M is (a whole-tensor base overflowed past 1.34 M rows of dZ)
     const int hb = mb > 0 ? mb - 1 : 0, nr = me > mb ? me - mb : 0;
-    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * KX, nr * KX * 4);
+    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * XR, nr * XR * 4);
     const rsrc_t rh = make_rsrc(Hq + (size_t)hb * FH, (nr ? me - hb : 0) * FH * 4);
     const rsrc_t rd = make_rsrc(Dq + (size_t)mb * FG, nr * FG * 4);
     auto load = [&](int m0) {
@@ -916,7 +931,7 @@ lstmf_wgrad_kernel(const float* __restrict__ X, const float* __restrict__ Hs, co
       for (int j = 0; j < WG::JX; ++j) {
         const int e = tid + 512 * j, r = e / (KX / 4), c = e - r * (KX / 4);
         const bool ok = e < WG::NX4 && m0 + r < me;
-        vx[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? ((m0 - mb + r) * KX + 4 * c) * 4 : kOOB, 0, 0));
+        vx[j] = ldx4<XR>(rx, ok ? ((m0 - mb + r) * XR + 4 * c) * 4 : kOOB, 0, 4 * c);
       }
 #pragma unroll
       for (int j = 0; j < WG::JH; ++j) {
@@ -1068,26 +1083,22 @@ struct WSGeo {
   using Img = WImg<16 * NI, WS_CD>;
 };
 
-// three bf16 planes of four fp32 values, packed two per dword
+// three bf16 planes of four fp32 values, packed two per dword.  The residual subtractions run on
+// value pairs (v_pk_add_f32 with a negated operand): 4.5 VALU per value instead of 5.5.  The masks
+// are taken on the u32 PAIR: written as two scalar ands feeding a float2, LLVM (ROCm 7.2) folded
+// the pair into one and + op_sel and subtracted the first value's high part from BOTH lanes.
 __device__ __forceinline__ void split3(const f32x4 v, uint32_t (&p)[3][2]) {
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    uint32_t hb[2], mb[2], lb[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const float a = v[2 * e + k];
-      const uint32_t u = __builtin_bit_cast(uint32_t, a), h = u & 0xffff0000u;
-      const float r1 = a - __builtin_bit_cast(float, h);
-      const uint32_t u1 = __builtin_bit_cast(uint32_t, r1), m = u1 & 0xffff0000u;
-      const float r2 = r1 - __builtin_bit_cast(float, m);
-      hb[k] = h;
-      mb[k] = m;
-      lb[k] = __builtin_bit_cast(uint32_t, r2);
-    }
+    const f2_t a = {v[2 * e], v[2 * e + 1]};
+    const u32x2_t h = __builtin_bit_cast(u32x2_t, a) & 0xffff0000u;
+    const f2_t r1 = a - __builtin_bit_cast(f2_t, h);
+    const u32x2_t m = __builtin_bit_cast(u32x2_t, r1) & 0xffff0000u;
+    const u32x2_t l = __builtin_bit_cast(u32x2_t, r1 - __builtin_bit_cast(f2_t, m));
     // high halves of (x1, x0) -> x0 in the low 16 bits, x1 in the high 16 bits
-    p[0][e] = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
-    p[1][e] = __builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u);
-    p[2][e] = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
+    p[0][e] = __builtin_amdgcn_perm(h.y, h.x, 0x07060302u);
+    p[1][e] = __builtin_amdgcn_perm(m.y, m.x, 0x07060302u);
+    p[2][e] = __builtin_amdgcn_perm(l.y, l.x, 0x07060302u);
   }
 }
 
@@ -1150,7 +1161,7 @@ __device__ __forceinline__ void ws_chunk(f32x4 (&acc)[NA][NB], const lds_char* A
   }
 }
 
-template <int KX>
+template <int KX, int XR = KX>  // XR: X row stride in floats (35: a 36-column image, column 35 zero)
 __global__ void __launch_bounds__(512, 1)
 lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ Hs, const float* __restrict__ D,
                          const float* __restrict__ Xd, const float* __restrict__ Hds, const float* __restrict__ Dd,
@@ -1203,7 +1214,7 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
   for (int j = 0; j < JX; ++j) {
     const int e = tid + 512 * j, r = e / (KX / 4), c4 = e - r * (KX / 4);
     const bool ok = e < 32 * KX / 4;
-    gx[j] = ok ? (r * KX + 4 * c4) * 4 : kOOB;
+    gx[j] = ok ? (r * XR + 4 * c4) * 4 : kOOB;
     lx[j] = ok ? r * GI::ROWA + 8 * c4 : -1;
   }
 #pragma unroll
@@ -1233,7 +1244,7 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
     // t = 0 rows are masked) so every voffset is >= 0 -- the range check is on voffset alone, and a
     // negative voffset with a compensating soffset reads zeros
     const int nr = me > mb ? me - mb : 0;
-    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * KX, nr * KX * 4);
+    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * XR, nr * XR * 4);
     const rsrc_t rh = make_rsrc(Hq + ((ptrdiff_t)mb - 1) * FH, (nr ? nr + 1 : 0) * FH * 4);
     const rsrc_t rd = make_rsrc(Dq + (size_t)mb * FG, nr * FG * 4);
     // t = (row) mod Tn of this thread's H slots at the current chunk (h_{-1} = 0 rows)
@@ -1243,7 +1254,8 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
     auto load = [&](int m0) {  // rows past me: voffset out of range, zeros
       const int lim = me - m0;
 #pragma unroll
-      for (int j = 0; j < JX; ++j) vx[j] = ld4s(rx, (gx[j] >> 2) / KX < lim ? gx[j] : kOOB, (m0 - mb) * KX * 4);
+      for (int j = 0; j < JX; ++j)
+        vx[j] = ldx4<XR>(rx, (gx[j] >> 2) / XR < lim ? gx[j] : kOOB, (m0 - mb) * XR * 4, (gx[j] >> 2) % XR);
 #pragma unroll
       for (int j = 0; j < JH; ++j) vh[j] = ld4s(rh, rhr[j] < lim && tm[j] != 0 ? gh[j] : kOOB, (m0 - mb) * FH * 4);
 #pragma unroll
@@ -2477,7 +2489,7 @@ static int wgradf_grid(int M) {
   const int chunks = (M + WF_R - 1) / WF_R, cus = device_cu_count();
   return chunks < cus ? chunks : cus;
 }
-bool lstmf_wgrad_supported(int K, int H, int N) { return H == FH && N == FG && (K == 32 || K == 36 || K == 100); }
+bool lstmf_wgrad_supported(int K, int H, int N) { return H == FH && N == FG && (K == 32 || K == 35 || K == 36 || K == 100); }
 
 // impl 1 / 2 / 3: the exact-fp32 MFMA kernel / the three-term bf16 split (pair) / the split quad;
 // default (0): exact under HFREP_FP32_EXACT, else the pair split for K <= 36 (12.1 -> 9.8 ms at 12.6 M
@@ -2496,12 +2508,13 @@ static int wgradq_z(int M) {
 }
 static int wgradf_pick(int impl, int K) {
   const int v = impl >= 1 && impl <= 3 ? impl : wgradf_version();
+  if (K == 35 && v == 3) return 2;  // the quad kernel reads 16-byte X rows only
   return v ? v : (K <= 36 ? 2 : 3);
 }
 size_t lstmf_wgrad_workspace_floats(int M, int K, int impl) {
   const int v = wgradf_pick(impl, K);
   const int z = v == 1 ? wgradf_grid(M) : v == 3 ? wgradq_z(M) : wgrads_z(M);
-  return (size_t)z * (K + FH + 1) * FG;
+  return (size_t)z * ((K == 35 ? 36 : K) + FH + 1) * FG;
 }
 
 bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
@@ -2533,10 +2546,11 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
     };
     switch (K) {
       case 32: go(lstmf_wgrad_split_kernel<32>, 2 * WSGeo<32>::Img::BUF); break;
+      case 35: go(lstmf_wgrad_split_kernel<36, 35>, 2 * WSGeo<36>::Img::BUF); break;
       case 36: go(lstmf_wgrad_split_kernel<36>, 2 * WSGeo<36>::Img::BUF); break;
       default: go(lstmf_wgrad_split_kernel<100>, 2 * WSGeo<100>::Img::BUF); break;
     }
-    launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s);
+    launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s, K == 35 ? 36 : K);
     return true;
   }
   const int grid = wgradf_grid(M);
@@ -2544,10 +2558,11 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
   const int z = (M + rpw - 1) / rpw;
   switch (K) {
     case 32: hipLaunchKernelGGL(lstmf_wgrad_kernel<32>, dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
+    case 35: hipLaunchKernelGGL((lstmf_wgrad_kernel<36, 35>), dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
     case 36: hipLaunchKernelGGL(lstmf_wgrad_kernel<36>, dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
     default: hipLaunchKernelGGL(lstmf_wgrad_kernel<100>, dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
   }
-  launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s);
+  launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s, K == 35 ? 36 : K);
   return true;
 }
 

@@ -372,23 +372,13 @@ def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None, impl: int = 
     """All weight gradients of one LSTM layer: gW += X^T dZ (+ Xd^T dZd), gU += H_{t-1}^T dZ (+ ...),
     gb += sum(dZ).  bf16 GPU: ONE fused launch (csrc/wgrad3.hip LDS-DMA streaming kernel where the
     shape is supported, csrc/gemm2.hip otherwise; ``impl=2`` forces the latter); fp32 GPU at the
-    model widths: ONE fused launch of csrc/lstm_f32.hip -- lstmf_wgrad_split_kernel (fp32 operands
-    split exactly into three bf16 terms, six products on the bf16 matrix pipe; default for K <= 36,
-    ``impl=2``) or the exact-fp32 MFMA kernel lstmf_wgrad_kernel (default for K = 100, ``impl=1``);
-    otherwise per-product calls."""
+    model widths (K in {32, 35, 36, 100}; 35-wide rows are read in place): ONE fused launch of
+    csrc/lstm_f32.hip -- the fp32-accurate three-term bf16 split (every fp32 operand h + m + l, six
+    products on the bf16 matrix pipe): lstmf_wgrad_split_kernel for K <= 36 (``impl=2``),
+    lstmf_wgrad_q4_kernel for K = 100 (``impl=3``); the exact-fp32 MFMA kernel lstmf_wgrad_kernel
+    under HFREP_FP32_EXACT=1 (``impl=1``); otherwise per-product calls."""
     f32 = (dZ.dtype == torch.float32 and x.shape[-1] in (32, 35, 36, 100) and hs.shape[-1] == 100
            and dZ.shape[-1] == 400)
-    if f32 and x.shape[-1] == 35 and _nat(dZ):
-        # the reference's 35-feature windows (GAN/MTSS_WGAN_GP.py:101): one zero column makes the rows
-        # 16-byte aligned for the fused kernel (instead of four per-product launches that each re-read dZ)
-        pad = torch.nn.functional.pad
-        gW36 = torch.zeros(36, gW.shape[-1], dtype=gW.dtype, device=gW.device)
-        _ops().lstm_wgrad_(pad(x, (0, 1)).contiguous(), hs.contiguous(), dZ.contiguous(), gW36, gU, gb,
-                           None if xd is None else pad(xd, (0, 1)).contiguous(),
-                           None if hds is None else hds.contiguous(), None if dZd is None else dZd.contiguous(),
-                           int(impl))
-        gW.add_(gW36[:35].reshape(gW.shape))
-        return
     if (dZ.dtype == torch.bfloat16 or f32) and _nat(dZ):
         _ops().lstm_wgrad_(x.contiguous(), hs.contiguous(), dZ.contiguous(), gW, gU, gb,
                            None if xd is None else xd.contiguous(), None if hds is None else hds.contiguous(),

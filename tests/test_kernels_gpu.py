@@ -817,11 +817,12 @@ def test_lstmf_wgrad_fused(cuda, B, T, K, tangent):
 
 @pytest.mark.parametrize("B,T,K,tangent", [(1, 5, 100, False), (70, 24, 32, False), (33, 12, 100, True),
                                            (41, 5, 36, True), (1000, 24, 100, True), (4500, 24, 32, False),
-                                           (20000, 24, 100, True)])
+                                           (20000, 24, 100, True), (41, 5, 35, True), (3001, 24, 35, False)])
 def test_lstmf_wgrad_split_vs_exact(cuda, B, T, K, tangent):
     """The three-term bf16 split weight gradients (impl 2 pair, 3 quad) and the exact-fp32
     MFMA kernel (impl 1) vs fp64: all inside the fp32 tolerance and the splits' error within 2x the exact
-    kernel's (the dropped split terms are <= 2^-24 of each product); bitwise run-to-run."""
+    kernel's (the dropped split terms are <= 2^-24 of each product); bitwise run-to-run.  K = 35: the
+    reference's 35-feature rows read in place (dword loads, a 36-column image; impl 3 falls back to 2)."""
     from hfrep.ops import functional as Fn
 
     H, N = 100, 400
