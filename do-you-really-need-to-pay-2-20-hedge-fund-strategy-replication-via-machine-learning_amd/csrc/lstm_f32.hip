@@ -1083,18 +1083,22 @@ struct WSGeo {
   using Img = WImg<16 * NI, WS_CD>;
 };
 
-// three bf16 planes of four fp32 values, packed two per dword.  The residual subtractions run on
-// value pairs (v_pk_add_f32 with a negated operand): 4.5 VALU per value instead of 5.5.  The masks
-// are taken on the u32 PAIR: written as two scalar ands feeding a float2, LLVM (ROCm 7.2) folded
-// the pair into one and + op_sel and subtracted the first value's high part from BOTH lanes.
+// three bf16 planes of four fp32 values, packed two per dword (4 VALU per value + 1.5 perms).  Scalar
+// on purpose: the pair form (v_pk_add_f32 for the residuals, 4.5 instructions per value) was slower
+// beside the MFMAs -- BPTT 7.96 -> 8.34 ms, K = 100 quad weight gradient 14.6 -> 15.4 ms at B = 262 144
+// (profiles/r04_ab: gfx950 issues a packed f32 op at more than the cost of two scalar ones)
 __device__ __forceinline__ void split3(const f32x4 v, uint32_t (&p)[3][2]) {
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    const f2_t a = {v[2 * e], v[2 * e + 1]};
-    const u32x2_t h = __builtin_bit_cast(u32x2_t, a) & 0xffff0000u;
-    const f2_t r1 = a - __builtin_bit_cast(f2_t, h);
-    const u32x2_t m = __builtin_bit_cast(u32x2_t, r1) & 0xffff0000u;
-    const u32x2_t l = __builtin_bit_cast(u32x2_t, r1 - __builtin_bit_cast(f2_t, m));
+    u32x2_t h, m, l;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float a = v[2 * e + k];
+      h[k] = __builtin_bit_cast(uint32_t, a) & 0xffff0000u;
+      const float r1 = a - __builtin_bit_cast(float, h[k]);
+      m[k] = __builtin_bit_cast(uint32_t, r1) & 0xffff0000u;
+      l[k] = __builtin_bit_cast(uint32_t, r1 - __builtin_bit_cast(float, m[k]));
+    }
     // high halves of (x1, x0) -> x0 in the low 16 bits, x1 in the high 16 bits
     p[0][e] = __builtin_amdgcn_perm(h.y, h.x, 0x07060302u);
     p[1][e] = __builtin_amdgcn_perm(m.y, m.x, 0x07060302u);
