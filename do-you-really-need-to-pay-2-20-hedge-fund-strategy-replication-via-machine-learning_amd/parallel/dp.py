@@ -75,6 +75,10 @@ class GradSync:
     def __init__(self, group, world: int, buckets: int = 2):
         self.group, self.world, self.buckets = group, world, buckets
         self.backend = dist.get_backend(group) if group is not None else None
+        # the group the gradient buckets go through: ``group``, or after :meth:`use_graph_group_` a
+        # second communicator over the same ranks that only ever runs inside hipGraph captures
+        self.bucket_group = group
+        self._graph_group = None
         self._pending = []
         # the newest async work: RCCL runs a group's collectives on one stream in issue order, so its
         # completion implies every earlier one's (graph capture waits for it, drain_)
@@ -84,7 +88,7 @@ class GradSync:
         if self.world <= 1:
             return
         if self.backend == "nccl":
-            dist.all_reduce(flat_grad, op=dist.ReduceOp.AVG, group=self.group)
+            dist.all_reduce(flat_grad, op=dist.ReduceOp.AVG, group=self.bucket_group)
         else:
             dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.group)
             flat_grad.div_(self.world)
@@ -101,7 +105,7 @@ class GradSync:
         if self.world <= 1:
             return
         if self.backend == "nccl":
-            w = dist.all_reduce(grad_slice, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+            w = dist.all_reduce(grad_slice, op=dist.ReduceOp.AVG, group=self.bucket_group, async_op=True)
             self._pending.append(w)
             self._last = w
         else:
@@ -136,6 +140,27 @@ class GradSync:
             if time.monotonic() - t0 > timeout_s:
                 raise RuntimeError(f"GradSync.drain_: a collective did not complete within {timeout_s} s")
             time.sleep(0.0005)
+        return True
+
+    def use_graph_group_(self) -> bool:
+        """Route the bucket all-reduces through a communicator reserved for hipGraph captures.
+
+        ProcessGroupNCCL's watchdog thread keeps querying the end events of a group's eager collectives
+        until it retires them, and HIP refuses ``hipEventQuery`` on an event of a stream that is being
+        captured (hipErrorCapturedEvent, which the watchdog turns into an abort) -- the captured
+        collectives pull the group's RCCL stream into the capture.  Whether the watchdog has retired
+        the warmup works before the capture starts is timing (round 3 slept 0.3 s; round 4's
+        completion poll alone failed on the GPU).  A second group over the same ranks, connected
+        eagerly and used ONLY inside captures, has no eager work for its watchdog to query, and the
+        first group's stream never joins a capture: no timing assumption left.  Collective call (every
+        rank, same point); nccl only.  Returns whether the switch happened."""
+        if self.backend != "nccl" or self.world <= 1 or self.group is None:
+            return False
+        if self._graph_group is None:
+            ranks = dist.get_process_group_ranks(self.group)
+            dev = torch.device("cuda", torch.cuda.current_device())
+            self._graph_group = dist.new_group(ranks=ranks, backend="nccl", device_id=dev)
+        self.bucket_group = self._graph_group
         return True
 
     def forget_(self) -> None:

@@ -101,14 +101,17 @@ class GraphedStep:
         while a stream captures is illegal -- the watchdog then takes the process down (the
         round-2 driver run of tests/test_gpu_rccl.py).  Thread-local mode only forbids unsafe
         calls on the capturing thread.  Every outstanding bucket is joined, the device drained and every
-        warmup collective confirmed complete (:meth:`GradSync.drain_`), so no eager collective is still
-        in flight when the capture starts."""
+        warmup collective confirmed complete (:meth:`GradSync.drain_`), and the captured bucket
+        all-reduces go through a communicator that never runs eager work
+        (:meth:`GradSync.use_graph_group_`): the watchdog has no event of a capturing stream to query."""
         t = self.t
         if t.grad_sync is not None:
             t.grad_sync.finish_()
         torch.cuda.synchronize()
         if t.grad_sync is not None:
             t.grad_sync.drain_()
+            t.grad_sync.use_graph_group_()
+            torch.cuda.synchronize()
         it = t.iteration
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
