@@ -1086,23 +1086,28 @@ struct WSGeo {
 // three bf16 planes of four fp32 values, packed two per dword (4 VALU per value + 1.5 perms).  Scalar
 // on purpose: the pair form (v_pk_add_f32 for the residuals, 4.5 instructions per value) was slower
 // beside the MFMAs -- BPTT 7.96 -> 8.34 ms, K = 100 quad weight gradient 14.6 -> 15.4 ms at B = 262 144
-// (profiles/r04_ab: gfx950 issues a packed f32 op at more than the cost of two scalar ones)
+// (profiles/r04_ab: gfx950 issues a packed f32 op at more than the cost of two scalar ones).  Plain
+// scalars, no ext_vector elements: clang (ROCm 7.2) compiles __builtin_bit_cast(T, vec[i]) / (T, vec.y)
+// as a cast of ELEMENT 0 (profiles/r04_ab/README.md; tests/test_isa_hazards.py lints the sources).
 __device__ __forceinline__ void split3(const f32x4 v, uint32_t (&p)[3][2]) {
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    u32x2_t h, m, l;
+    uint32_t hb[2], mb[2], lb[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const float a = v[2 * e + k];
-      h[k] = __builtin_bit_cast(uint32_t, a) & 0xffff0000u;
-      const float r1 = a - __builtin_bit_cast(float, h[k]);
-      m[k] = __builtin_bit_cast(uint32_t, r1) & 0xffff0000u;
-      l[k] = __builtin_bit_cast(uint32_t, r1 - __builtin_bit_cast(float, m[k]));
+      const uint32_t u = __builtin_bit_cast(uint32_t, a), h = u & 0xffff0000u;
+      const float r1 = a - __builtin_bit_cast(float, h);
+      const uint32_t u1 = __builtin_bit_cast(uint32_t, r1), m = u1 & 0xffff0000u;
+      const float r2 = r1 - __builtin_bit_cast(float, m);
+      hb[k] = h;
+      mb[k] = m;
+      lb[k] = __builtin_bit_cast(uint32_t, r2);
     }
     // high halves of (x1, x0) -> x0 in the low 16 bits, x1 in the high 16 bits
-    p[0][e] = __builtin_amdgcn_perm(h.y, h.x, 0x07060302u);
-    p[1][e] = __builtin_amdgcn_perm(m.y, m.x, 0x07060302u);
-    p[2][e] = __builtin_amdgcn_perm(l.y, l.x, 0x07060302u);
+    p[0][e] = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
+    p[1][e] = __builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u);
+    p[2][e] = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
   }
 }
 

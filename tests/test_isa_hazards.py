@@ -74,3 +74,20 @@ def test_no_cross_opcode_mfma_srcc_hazard(asm_files):
     _, hits = isa_mfma_srcc.scan(asm_files)
     assert not hits, "\n".join(f"{os.path.basename(p)}:{ln} {(fn or '?')[:60]}: {a} -> {b} ({ws} < {need})"
                                for p, ln, fn, a, b, ws, need in hits)
+
+
+def test_no_bit_cast_of_vector_elements():
+    """Source lint: clang (ROCm 7.2) compiles ``__builtin_bit_cast(T, v[i])`` / ``(T, v.y)`` on an
+    ext_vector element as a cast of element 0 (a round-4 split helper written that way gave the fp32
+    trainer a 38x gradient error while its instruction count looked right; profiles/r04_ab/README.md).
+    Kernel sources copy an element into a scalar before bit-casting it."""
+    import re
+
+    pat = re.compile(r"__builtin_bit_cast\(\s*[\w:]+\s*,\s*\w+\s*(\[|\.[xyzw]\b)")
+    bad = []
+    for f in sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h")) +
+                    glob.glob(os.path.join(CSRC, "*.cpp"))):
+        for n, line in enumerate(open(f), 1):
+            if pat.search(line.split("//")[0]):
+                bad.append(f"{os.path.basename(f)}:{n}: {line.strip()}")
+    assert not bad, "bit_cast of a vector element:\n" + "\n".join(bad)
