@@ -1,0 +1,13 @@
+#!/bin/bash
+# fp32 LDS-DMA streaming weight gradient (impl 4): numerics vs fp64 / the exact kernel, then timing of
+# every fp32 weight-gradient kernel at the critic's 12.6 M rows
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"
+OUT=gpurun_out/${1:-wdma}; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "lstmf_wgrad" -q --timeout 200 --timeout-method thread \
+  > $OUT/tests.txt 2>&1 || { tail -n 40 $OUT/tests.txt; exit 1; }
+tail -n 2 $OUT/tests.txt
+timeout -k 10 300 python -u scripts/bench_wgrad.py --dtype float32 --batch 262144 --iters 5 > $OUT/bench_wgrad.jsonl 2>&1 \
+  || { tail -n 20 $OUT/bench_wgrad.jsonl; exit 1; }
+grep -v amdgpu.ids $OUT/bench_wgrad.jsonl
