@@ -1636,7 +1636,8 @@ struct FDGeo {
   static constexpr int XI = (XB + 1023) / 1024, HI = (HB + 1023) / 1024, NI = XI + HI;
   static constexpr int NPA = (NI + FD_W - 1) / FD_W;         // A DMA instructions per wave and chunk
   static constexpr int NPD = (FD_NDI + FD_W - 1) / FD_W;     // D DMA instructions per wave and chunk
-  static constexpr int STAGE = NI * 1024, OFF_H = XI * 1024;
+  // stage: X image, 1 KiB never written (H_{t-1} row -1 of a range starting at row 0 reads zeros), H image
+  static constexpr int STAGE = (NI + 1) * 1024, OFF_H = (XI + 1) * 1024;
   static constexpr int DOFF = 2 * STAGE, RAWD = DOFF + 2 * FD_DBUF, TRASH = RAWD + FD_NDI * 1024;
   static constexpr int LDS = TRASH + 1024;
   static_assert(32 * FD_JT / 4 == 64 * FD_NDI, "D chunk = whole DMA instructions");
@@ -1660,11 +1661,10 @@ __device__ __forceinline__ void fd_wait_vm() {
 // A fragment of one i-block from the raw ring: rows 4 G + j (j < 4) and 16 + 4 G + j - 4 of this
 // lane's column (the k order of tr_frag), P = row pitch in bytes (compile-time: the reads' offsets are
 // immediates), then masked / made (bias, zero) and split into the three planes
-// (vlo / vhi: this lane's valid-row bits for rows 4 G + j / 16 + 4 G + j; xm: all ones for X lanes;
-// isH selects the row mask)
-template <int P>
-__device__ __forceinline__ void fd_afrag(const lds_char* a0, bool isH, uint32_t xm, uint32_t vlo, uint32_t vhi,
-                                         uint32_t orv, bf16x8 (&af)[3]) {
+// (MADE: the last i-block, whose lanes include the bias column (value orv) and zero columns: value =
+// (raw & xm) | orv; the t = 0 rows of H_{t-1} are zeroed in LDS before the chunk's barrier)
+template <int P, bool MADE>
+__device__ __forceinline__ void fd_afrag(const lds_char* a0, uint32_t xm, uint32_t orv, bf16x8 (&af)[3]) {
   float r[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) r[j] = *reinterpret_cast<const __attribute__((address_space(3))) float*>(a0 + (j < 4 ? j : 12 + j) * P);
@@ -1672,9 +1672,7 @@ __device__ __forceinline__ void fd_afrag(const lds_char* a0, bool isH, uint32_t 
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float rj = r[j];
-    const uint32_t b = __builtin_bit_cast(uint32_t, rj);
-    const uint32_t hm = (uint32_t)__builtin_amdgcn_sbfe((int)(j < 4 ? vlo : vhi), j & 3, 1);
-    v[j >> 2][j & 3] = __builtin_bit_cast(float, (b & (isH ? hm : xm)) | orv);
+    v[j >> 2][j & 3] = MADE ? __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, rj) & xm) | orv) : rj;
   }
   uint32_t p0[3][2], p1[3][2];
   split3(v[0], p0);
@@ -1782,7 +1780,7 @@ lstmf_wgrad_dma_kernel(const float* __restrict__ X0, const float* __restrict__ H
   const int g = lane >> 4, c16 = lane & 15;
   constexpr int NB = IPS + 1;
   int aoff[NB];       // LDS byte offset in a stage of row 4 g, this lane's column (0 for bias / zero lanes)
-  bool aH[NB];        // H_{t-1} column (t = 0 rows masked)
+  bool aH[NB];        // H_{t-1} column
   uint32_t aX[NB];    // X column: all ones mask; bias / zero: 0
   bool aB[NB];        // bias column
 #pragma unroll
@@ -1823,31 +1821,42 @@ lstmf_wgrad_dma_kernel(const float* __restrict__ X0, const float* __restrict__ H
 #pragma unroll
       for (int k = 0; k < NPD; ++k) asm volatile("" : "+v"(drc[k]));
       asm volatile("" : "+v"(tro_d));
-      fd_wait_vm<0>();                        // this wave's DMA of chunk c has landed
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      issue(c + 1, S ^ 1);
       int sg, m0, xl, hl;
       chunk_rows(c, sg, m0, xl, hl);
       if (c == nchs) t0 = __builtin_amdgcn_readfirstlane(mb % Tn);  // second segment
-      // rows of this chunk with t = 0 (H_{t-1} belongs to the previous window): bit rr of zm
+      // rows of this chunk with t = 0 (their H_{t-1} belongs to the previous window): bit rr of zm
       uint32_t zm = 0;
       for (int rr = t0 == 0 ? 0 : Tn - t0; rr < 32; rr += Tn) zm |= 1u << rr;
       t0 += step32;
       if (t0 >= Tn) t0 -= Tn;
-      const uint32_t vm = ~zm;
-      const uint32_t vlo = vm >> (4 * g), vhi = vm >> (16 + 4 * g);  // this lane's rows
+      fd_wait_vm<0>();  // this wave's DMA of chunk c has landed: zero the t = 0 rows among its H bytes
+      {
+        const int hoff = m0 - 1 - hl;  // H image row of chunk row rr: rr + hoff
+#pragma unroll
+        for (int k = 0; k < NPA; ++k) {
+          const int n = w + FD_W * k;
+          if (n < G::XI || n >= G::NI) continue;  // (wave-uniform)
+          const int bo = (n - G::XI) * 1024 + lane * 16, rr = bo / (FH * 4) - hoff;
+          if (bo < G::HB && rr >= 0 && rr < 32 && ((zm >> rr) & 1u))
+            *reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(sm + S * G::STAGE + G::OFF_H + bo) = u32x4_t{0, 0, 0, 0};
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      issue(c + 1, S ^ 1);
       const uint32_t bval = sg ? 0u : 0x3f800000u;
       const int stb = S * G::STAGE;
       const int xs = (m0 - xl) * K * 4, hs = (m0 - 1 - hl) * FH * 4;  // row shifts of the images
       const lds_char* dpl = sm + G::DOFF + S * FD_DBUF;
-      auto block = [&](int r, bf16x8 (&af)[3]) {
+      auto block = [&](auto R_, bf16x8 (&af)[3]) {
+        constexpr int r = decltype(R_)::value;
+        constexpr bool MADE = r == IPS;  // the last i-block
         const lds_char* a0 = sm + stb + aoff[r] + (aH[r] ? hs : aX[r] ? xs : 0);
-        const uint32_t orv = aB[r] ? bval : 0u;
+        const uint32_t xm = aH[r] ? 0xffffffffu : aX[r], orv = aB[r] ? bval : 0u;
         if constexpr (K == 100) {
-          fd_afrag<K * 4>(a0, aH[r], aX[r], vlo, vhi, orv, af);  // X and H rows share the 400-byte pitch
+          fd_afrag<K * 4, MADE>(a0, xm, orv, af);  // X and H rows share the 400-byte pitch
         } else {
-          if (aH[r] || !aX[r]) fd_afrag<FH * 4>(a0, aH[r], aX[r], vlo, vhi, orv, af);  // (wave-uniform for K = 32)
-          else fd_afrag<K * 4>(a0, aH[r], aX[r], vlo, vhi, orv, af);
+          if (aH[r] || !aX[r]) fd_afrag<FH * 4, MADE>(a0, xm, orv, af);  // (wave-uniform for K = 32)
+          else fd_afrag<K * 4, MADE>(a0, xm, orv, af);
         }
       };
       auto bload = [&](bf16x8 (&bf)[3], int jb) {
@@ -1862,6 +1871,7 @@ lstmf_wgrad_dma_kernel(const float* __restrict__ X0, const float* __restrict__ H
         constexpr int NJ = decltype(NJ_)::value, ACC0 = decltype(ACC0_)::value;
         bf16x8 bf[2][3];
         bload(bf[0], jf);
+        f32x4 tp;  // the previous tile's products: added after this tile's MFMAs are issued
 #pragma unroll
         for (int jj = 0; jj < NJ; ++jj) {
           __builtin_amdgcn_sched_barrier(0);
@@ -1873,8 +1883,10 @@ lstmf_wgrad_dma_kernel(const float* __restrict__ X0, const float* __restrict__ H
           t = mma32(a3[1], b3[0], t);                                 // mh
           t = mma32(a3[0], b3[1], t);                                 // hm
           t = mma32(a3[0], b3[0], t);                                 // hh
-          acc[ACC0 + jj] += t;
+          if (jj > 0) acc[ACC0 + jj - 1] += tp;
+          tp = t;
         }
+        acc[ACC0 + NJ - 1] += tp;
         __builtin_amdgcn_sched_barrier(0);
       };
       // base i-blocks: IPS x NJB tiles; this wave's raw D of chunk c + 1 is split into the other
@@ -1882,7 +1894,7 @@ lstmf_wgrad_dma_kernel(const float* __restrict__ X0, const float* __restrict__ H
       auto rr = [&](auto R_) {
         constexpr int r = decltype(R_)::value;
         bf16x8 af[3];
-        block(r, af);
+        block(R_, af);
         tiles(af, JB0, std::integral_constant<int, NJB>{}, std::integral_constant<int, NJB * r>{});
         if (r == IPS - 1) {
           fd_wait_vm<NPA>();  // this wave's D DMA of chunk c + 1 (issued before its A DMA) has landed
@@ -1894,7 +1906,7 @@ lstmf_wgrad_dma_kernel(const float* __restrict__ X0, const float* __restrict__ H
       if constexpr (IPS > 2) rr(std::integral_constant<int, 2>{});
       if constexpr (HALF == 1) {  // the last i-block: this SIMD's quarter of its j-blocks (3 or 4: the
         bf16x8 af[3];             // fourth tile of SIMDs 1-3 is computed and dropped, as SIMD 0's is kept)
-        block(IPS, af);
+        block(std::integral_constant<int, IPS>{}, af);
         tiles(af, FD_JL[s], std::integral_constant<int, 4>{}, std::integral_constant<int, 6 * IPS>{});
       }
     };
