@@ -1624,6 +1624,9 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
 //  * one raw s_barrier per chunk; the next chunk's DMA is issued right after it.
 // Products and accumulation as the split kernels: six bf16 products per tile into a fresh
 // accumulator, added to the running sum in VALU fp32.
+#ifndef HFREP_WDMA_IL  // A/B: the next block's A fragments built between the current block's tiles
+#define HFREP_WDMA_IL 0
+#endif
 constexpr int FD_W = 8, FD_JT = 208, FD_NDI = 26;  // waves, columns per workgroup, D DMA instructions
 constexpr int FD_ROWD = 416, FD_PLD = 32 * FD_ROWD, FD_DBUF = 3 * FD_PLD;  // D planes: 104-dword rows
 template <int K>
@@ -1663,11 +1666,37 @@ __device__ __forceinline__ void fd_wait_vm() {
 // immediates), then masked / made (bias, zero) and split into the three planes
 // (MADE: the last i-block, whose lanes include the bias column (value orv) and zero columns: value =
 // (raw & xm) | orv; the t = 0 rows of H_{t-1} are zeroed in LDS before the chunk's barrier)
+template <int P>
+__device__ __forceinline__ void fd_areads(const lds_char* a0, float (&r)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = *reinterpret_cast<const __attribute__((address_space(3))) float*>(a0 + (j < 4 ? j : 12 + j) * P);
+}
+// rows h (0: j < 4, 1: j >= 4) of the fragment: four values split into dwords 2 h, 2 h + 1 of the planes
+template <bool MADE>
+__device__ __forceinline__ void fd_asplit(const float (&r)[8], int h, uint32_t xm, uint32_t orv, uint32_t (&pk)[3][4]) {
+  f32x4 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float rj = r[4 * h + j];
+    v[j] = MADE ? __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, rj) & xm) | orv) : rj;
+  }
+  uint32_t p[3][2];
+  split3(v, p);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    pk[q][2 * h] = p[q][0];
+    pk[q][2 * h + 1] = p[q][1];
+  }
+}
+// (row pitch P per lane at run time: K = 32, whose X and H blocks differ in pitch)
+__device__ __forceinline__ void fd_areads_rt(const lds_char* a0, int P, float (&r)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = *reinterpret_cast<const __attribute__((address_space(3))) float*>(a0 + (j < 4 ? j : 12 + j) * P);
+}
 template <int P, bool MADE>
 __device__ __forceinline__ void fd_afrag(const lds_char* a0, uint32_t xm, uint32_t orv, bf16x8 (&af)[3]) {
   float r[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = *reinterpret_cast<const __attribute__((address_space(3))) float*>(a0 + (j < 4 ? j : 12 + j) * P);
+  fd_areads<P>(a0, r);
   f32x4 v[2];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -1889,6 +1918,80 @@ lstmf_wgrad_dma_kernel(const float* __restrict__ X0, const float* __restrict__ H
         acc[ACC0 + NJ - 1] += tp;
         __builtin_amdgcn_sched_barrier(0);
       };
+#if HFREP_WDMA_IL
+      // the next i-block's A fragments are built between this block's tiles: reads after tile 0, the
+      // split of its two row halves after tiles 2 and 3 (the VALU issues beside the MFMAs)
+      auto a_reads = [&](auto R_, float (&rv)[8]) {
+        constexpr int r = decltype(R_)::value;
+        const lds_char* a0 = sm + stb + aoff[r] + (aH[r] ? hs : aX[r] ? xs : 0);
+        if constexpr (K == 100) fd_areads<K * 4>(a0, rv);
+        else fd_areads_rt(a0, aX[r] ? K * 4 : FH * 4, rv);
+      };
+      auto a_split = [&](auto R_, const float (&rv)[8], int h, uint32_t (&pk)[3][4]) {
+        constexpr int r = decltype(R_)::value;
+        const uint32_t xm = aH[r] ? 0xffffffffu : aX[r], orv = aB[r] ? bval : 0u;
+        fd_asplit<r == IPS>(rv, h, xm, orv, pk);
+      };
+      // NJ tiles of block R (fragments a3) and, if NXT, the pieces of block R + 1 into an
+      auto tiles2 = [&](const bf16x8 (&a3)[3], int jf, auto NJ_, auto ACC0_, auto R_, auto NXT_, bf16x8 (&an)[3]) {
+        constexpr int NJ = decltype(NJ_)::value, ACC0 = decltype(ACC0_)::value, R = decltype(R_)::value;
+        constexpr bool NXT = decltype(NXT_)::value;
+        static_assert(!NXT || NJ >= 4, "next-block pieces need four tiles");
+        bf16x8 bf[2][3];
+        bload(bf[0], jf);
+        f32x4 tp;
+        float rv[8];
+        uint32_t pk[3][4];
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (jj + 1 < NJ) bload(bf[(jj + 1) & 1], jf + jj + 1);
+          const bf16x8(&b3)[3] = bf[jj & 1];
+          f32x4 t = mma32(a3[2], b3[0], f32x4{0.f, 0.f, 0.f, 0.f});  // lh
+          t = mma32(a3[0], b3[2], t);                                 // hl
+          t = mma32(a3[1], b3[1], t);                                 // mm
+          t = mma32(a3[1], b3[0], t);                                 // mh
+          t = mma32(a3[0], b3[1], t);                                 // hm
+          t = mma32(a3[0], b3[0], t);                                 // hh
+          if constexpr (NXT) {
+            if (jj == 0) a_reads(std::integral_constant<int, R + 1>{}, rv);
+            if (jj == 2) a_split(std::integral_constant<int, R + 1>{}, rv, 0, pk);
+            if (jj == 3) {
+              a_split(std::integral_constant<int, R + 1>{}, rv, 1, pk);
+#pragma unroll
+              for (int q = 0; q < 3; ++q) an[q] = __builtin_bit_cast(bf16x8, make_uint4(pk[q][0], pk[q][1], pk[q][2], pk[q][3]));
+            }
+          }
+          if (jj > 0) acc[ACC0 + jj - 1] += tp;
+          tp = t;
+        }
+        acc[ACC0 + NJ - 1] += tp;
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      constexpr int NBLK = IPS + HALF;  // i-blocks of this wave
+      bf16x8 af[2][3];
+      block(std::integral_constant<int, 0>{}, af[0]);
+      auto rr = [&](auto R_) {
+        constexpr int r = decltype(R_)::value;
+        constexpr bool NXT = r + 1 < NBLK;
+        if constexpr (r < IPS)
+          tiles2(af[r & 1], JB0, std::integral_constant<int, NJB>{}, std::integral_constant<int, NJB * r>{}, R_,
+                 std::integral_constant<bool, NXT>{}, af[(r + 1) & 1]);
+        else  // the last i-block (half 1): this SIMD's quarter of its j-blocks (the 4th of SIMDs 1-3 dropped)
+          tiles2(af[r & 1], FD_JL[s], std::integral_constant<int, 4>{}, std::integral_constant<int, 6 * IPS>{}, R_,
+                 std::integral_constant<bool, false>{}, af[(r + 1) & 1]);
+        if (r == IPS - 1) {
+          fd_wait_vm<NPA>();  // this wave's D DMA of chunk c + 1 (issued before its A DMA) has landed
+          stage_d(c + 1, S ^ 1);
+        }
+      };
+      rr(std::integral_constant<int, 0>{});
+      rr(std::integral_constant<int, 1>{});
+      if constexpr (NBLK > 2) rr(std::integral_constant<int, 2>{});
+      if constexpr (NBLK > 3) rr(std::integral_constant<int, 3>{});
+      static_assert(NBLK <= 4, "i-blocks per wave");
+    };
+#else
       // base i-blocks: IPS x NJB tiles; this wave's raw D of chunk c + 1 is split into the other
       // planes buffer after the first one (its DMA was issued at the top of this chunk)
       auto rr = [&](auto R_) {
@@ -1910,6 +2013,7 @@ lstmf_wgrad_dma_kernel(const float* __restrict__ X0, const float* __restrict__ H
         tiles(af, FD_JL[s], std::integral_constant<int, 4>{}, std::integral_constant<int, 6 * IPS>{});
       }
     };
+#endif
     for (int c = 0; c < nch; ++c) chunk(c);
     fd_wait_vm<0>();
 

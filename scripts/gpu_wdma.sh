@@ -11,3 +11,11 @@ tail -n 2 $OUT/tests.txt
 timeout -k 10 300 python -u scripts/bench_wgrad.py --dtype float32 --batch 262144 --iters 5 > $OUT/bench_wgrad.jsonl 2>&1 \
   || { tail -n 20 $OUT/bench_wgrad.jsonl; exit 1; }
 grep -v amdgpu.ids $OUT/bench_wgrad.jsonl
+if [ -f variants/wdma_il/_hfrep_native.so ]; then
+  HFREP_NATIVE_LIB="$R/variants/wdma_il/_hfrep_native.so" timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "lstmf_wgrad_split_vs_exact" -q \
+    --timeout 200 --timeout-method thread > $OUT/tests_il.txt 2>&1 || { tail -n 40 $OUT/tests_il.txt; exit 1; }
+  tail -n 1 $OUT/tests_il.txt
+  HFREP_NATIVE_LIB="$R/variants/wdma_il/_hfrep_native.so" timeout -k 10 300 python -u scripts/bench_wgrad.py --dtype float32 --batch 262144 --iters 5 \
+    > $OUT/bench_wgrad_il.jsonl 2>&1 || { tail -n 20 $OUT/bench_wgrad_il.jsonl; exit 1; }
+  grep '"f32_dma"' $OUT/bench_wgrad_il.jsonl
+fi
