@@ -2530,6 +2530,10 @@ constexpr int DS4_PL = 16 * DS4_RS * 2;       // bytes per plane image (16 rows)
 constexpr int DS4_BUF = 3 * DS4_PL;           // one buffer: three planes
 constexpr int DS4_SLOTS = (16 * 100 + 255) / 256;  // float4 staging slots per thread per chunk (7)
 constexpr int DS4_K0 = DS_KS - DS4_SLOTS;     // first k-step followed by a staging slot
+#ifndef HFREP_DS4_SETS  // A/B: register sets of the dZ prefetch (2: one chunk ahead, 3: two chunks ahead)
+#define HFREP_DS4_SETS 2
+#endif
+constexpr int DS4_NS = HFREP_DS4_SETS;
 
 template <int NT2>
 __global__ void __launch_bounds__(256, 1)
@@ -2566,7 +2570,7 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
       }
     }
   }
-  f32x4 v[2][DS4_SLOTS];
+  f32x4 v[DS4_NS][DS4_SLOTS];
   auto load = [&](auto S_, int c) {  // chunk c's rows (past M: zero-size descriptor, zeros)
     constexpr int S = decltype(S_)::value;
     const int r0 = c * 16, nr = c < nch ? min(16, M - r0) : 0;
@@ -2597,21 +2601,23 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   const int cs = gridDim.x;
-  // prologue: the first chunk staged into buffer 0, the second in flight in set 1
+  // prologue: this workgroup's chunk i (i = 0, 1, ...) lives in register set i % DS4_NS; chunk 0 staged
+  // into buffer 0, chunks 1 .. DS4_NS - 1 in flight
   load(I0{}, blockIdx.x);
 #pragma unroll
   for (int j = 0; j < DS4_SLOTS; ++j) stage(I0{}, dsm, j);
   load(I1{}, blockIdx.x + cs);
+  if constexpr (DS4_NS > 2) load(std::integral_constant<int, 2>{}, blockIdx.x + 2 * cs);
   __syncthreads();
   const int ao = (c16 * DS4_RS + 8 * g) * 2;  // this lane's A fragment: row c16, k = 8 g .. + 7 of a k-step
   // chunk cc (buffer S): chunk cc + 2 cs loaded into set S, the MFMAs on buffer S, chunk cc + cs (set
   // S ^ 1) split into buffer S ^ 1 in slices after the last DS4_SLOTS k-steps (unconditional: past
   // the end it stages zeros)
-  auto chunk = [&](auto S_, int cc) {
-    constexpr int S = decltype(S_)::value;
-    load(S_, cc + 2 * cs);
-    const lds_char* A_ = dsm + S * DS4_BUF;
-    lds_char* nxt = dsm + (S ^ 1) * DS4_BUF;
+  auto chunk = [&](auto S_, int cc, int P) {  // S: register set of chunk cc, P: its LDS buffer
+    constexpr int S = decltype(S_)::value, SN = (S + 1) % DS4_NS;  // SN: set of chunk cc + cs
+    load(S_, cc + DS4_NS * cs);
+    const lds_char* A_ = dsm + P * DS4_BUF;
+    lds_char* nxt = dsm + (P ^ 1) * DS4_BUF;
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     // A fragments one k-step ahead (two sets): the LDS latency hides under the previous k-step's MFMAs
     bf16x8 af[2][3];
@@ -2636,7 +2642,7 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
         acc[e] = mma32(a[0], bw[e][ks][0], acc[e]);  // hh
       }
       if (ks >= DS4_K0) {
-        stage(std::integral_constant<int, S ^ 1>{}, nxt, ks - DS4_K0);  // (compile-time)
+        stage(std::integral_constant<int, SN>{}, nxt, ks - DS4_K0);  // (compile-time)
         // in-order issue: the split's VALU only overlaps the matrix pipe when it sits BETWEEN the
         // MFMAs in program order (12 MFMAs x 16 cycles vs ~24 VALU x 4 cycles per slot)
 #pragma unroll
@@ -2659,11 +2665,23 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
     __syncthreads();
   };
   int c = blockIdx.x;
-  for (; c + cs < nch; c += 2 * cs) {
-    chunk(I0{}, c);
-    chunk(I1{}, c + cs);
+  if constexpr (DS4_NS == 2) {
+    for (; c + cs < nch; c += 2 * cs) {
+      chunk(I0{}, c, 0);
+      chunk(I1{}, c + cs, 1);
+    }
+    if (c < nch) chunk(I0{}, c, 0);
+  } else {
+    int p = 0;  // LDS buffer of chunk c
+    for (; c + 2 * cs < nch; c += 3 * cs) {
+      chunk(I0{}, c, p);
+      chunk(I1{}, c + cs, p ^ 1);
+      chunk(std::integral_constant<int, 2>{}, c + 2 * cs, p);
+      p ^= 1;
+    }
+    if (c < nch) chunk(I0{}, c, p);
+    if (c + cs < nch) chunk(I1{}, c + cs, p ^ 1);
   }
-  if (c < nch) chunk(I0{}, c);
 }
 
 // ==========================================================================================

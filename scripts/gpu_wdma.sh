@@ -19,3 +19,15 @@ if [ -f variants/wdma_il/_hfrep_native.so ]; then
     > $OUT/bench_wgrad_il.jsonl 2>&1 || { tail -n 20 $OUT/bench_wgrad_il.jsonl; exit 1; }
   grep '"f32_dma"' $OUT/bench_wgrad_il.jsonl
 fi
+if [ -f variants/ds4_3/_hfrep_native.so ]; then
+  for tag in base ds4_3; do
+    if [ $tag = base ]; then unset HFREP_NATIVE_LIB; else export HFREP_NATIVE_LIB="$R/variants/ds4_3/_hfrep_native.so"; fi
+    timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "test_lstmf_dgrad" -q --timeout 200 --timeout-method thread \
+      > $OUT/tests_dgrad_$tag.txt 2>&1 || { tail -n 40 $OUT/tests_dgrad_$tag.txt; exit 1; }
+    tail -n 1 $OUT/tests_dgrad_$tag.txt
+    timeout -k 10 200 python -u scripts/bench_lstm.py --dtype float32 --batch 262144 --K 100 --iters 10 --only dgrad \
+      > $OUT/dgrad_$tag.jsonl 2>&1 || { tail -n 20 $OUT/dgrad_$tag.jsonl; exit 1; }
+    grep '"op"' $OUT/dgrad_$tag.jsonl
+  done
+  unset HFREP_NATIVE_LIB
+fi
