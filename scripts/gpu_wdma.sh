@@ -31,3 +31,5 @@ if [ -f variants/ds4_3/_hfrep_native.so ]; then
   done
   unset HFREP_NATIVE_LIB
 fi
+timeout -k 10 400 python -u scripts/ae_bf16_diag.py --latents 1,4,8 --seeds 1,2 > $OUT/ae_bf16_diag.jsonl 2>&1 || { tail -n 20 $OUT/ae_bf16_diag.jsonl; exit 1; }
+grep '"k"' $OUT/ae_bf16_diag.jsonl
