@@ -58,7 +58,7 @@ bool launch_lstmf_tbwd(const float* dH, const float* dHd, const float* tape, con
 // (lstmf_wgrad_workspace_floats) and one fixed-order reduce
 bool lstmf_wgrad_supported(int K, int H, int N);
 // impl: 0 = default (exact under HFREP_FP32_EXACT=1, else the pair split for K <= 36 and the quad split for K = 100), 1 = exact-fp32
-// MFMA, 2 = the three-term bf16 split (pair), 3 = the three-term bf16 split (quad), 4 = the split with LDS-DMA streaming (K = 32 / 100, M >= 64; else as 0)
+// MFMA, 2 = the three-term bf16 split (pair), 3 = the three-term bf16 split (quad)
 size_t lstmf_wgrad_workspace_floats(int M, int K, int impl = 0);
 bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
                         float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl = 0);

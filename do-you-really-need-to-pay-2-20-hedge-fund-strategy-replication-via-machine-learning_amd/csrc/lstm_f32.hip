@@ -1604,443 +1604,6 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// split weight gradient, LDS-DMA streaming: lstmf_wgrad_dma_kernel (K = 32 / 100)
-// ------------------------------------------------------------------------------------------
-// The split / quad kernels stage each fp32 chunk through registers one chunk ahead of its use.  Their
-// r04 PMC counters (profiles/r04_wgrad) at B = 65 536: 31 / 38 % MFMA busy, a third of the wave cycles
-// in waits, HBM at 2.0-2.3 TB/s of exactly the unique bytes (the redundant A reads of the pair / quad
-// hit L2) -- latency-bound, not bandwidth-, VALU- or MFMA-bound.  Here, per workgroup PAIR (blocks b,
-// b + 8 on one XCD: the two 208-column halves of C for one row range, as wgrad3.hip), every byte
-// arrives by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction, no registers in flight):
-//  * the A rows [X | H_{t-1}] into a 2-stage raw fp32 ring; every wave builds its own A fragments from
-//    it (8 ds_read_b32 of its column, the t = 0 rows of H_{t-1} masked, the bias column made in
-//    registers, the three-term split);
-//  * the chunk's 208 D columns into a raw region where each wave's DMA instructions carry exactly the
-//    float4s its own threads split into the double-buffered bf16 planes (the B operands, read with
-//    ds_read_b64_tr_b16) -- so a wave's vmcnt is all the staging needs, no extra barrier;
-//  * SIMD s owns base i-blocks IPS s .. IPS s + IPS - 1 (its two waves: j-blocks 0-6 / 7-12) and a
-//    quarter of the last i-block's j-blocks (second wave): 21 / 22 tiles per wave at K = 100;
-//  * one raw s_barrier per chunk; the next chunk's DMA is issued right after it.
-// Products and accumulation as the split kernels: six bf16 products per tile into a fresh
-// accumulator, added to the running sum in VALU fp32.
-#ifndef HFREP_WDMA_IL  // A/B: the next block's A fragments built between the current block's tiles
-#define HFREP_WDMA_IL 0
-#endif
-constexpr int FD_W = 8, FD_JT = 208, FD_NDI = 26;  // waves, columns per workgroup, D DMA instructions
-constexpr int FD_ROWD = 416, FD_PLD = 32 * FD_ROWD, FD_DBUF = 3 * FD_PLD;  // D planes: 104-dword rows
-template <int K>
-struct FDGeo {
-  static constexpr int KTOT = K + FH + 1, NIB = (KTOT + 15) / 16;
-  static constexpr int IPS = (NIB - 1) / 4;  // base i-blocks per SIMD
-  static_assert(4 * IPS + 1 == NIB && (IPS == 2 || IPS == 3), "i-block map: four SIMDs x IPS base blocks + the last");
-  static_assert(K == 32 || K == 100, "X / H i-blocks: block aligned (K = 32) or equal row pitch (K = 100)");
-  static constexpr int XB = 32 * K * 4, HB = 32 * FH * 4;
-  static constexpr int XI = (XB + 1023) / 1024, HI = (HB + 1023) / 1024, NI = XI + HI;
-  static constexpr int NPA = (NI + FD_W - 1) / FD_W;         // A DMA instructions per wave and chunk
-  static constexpr int NPD = (FD_NDI + FD_W - 1) / FD_W;     // D DMA instructions per wave and chunk
-  // stage: X image, 1 KiB never written (H_{t-1} row -1 of a range starting at row 0 reads zeros), H image
-  static constexpr int STAGE = (NI + 1) * 1024, OFF_H = (XI + 1) * 1024;
-  static constexpr int DOFF = 2 * STAGE, RAWD = DOFF + 2 * FD_DBUF, TRASH = RAWD + FD_NDI * 1024;
-  static constexpr int LDS = TRASH + 1024;
-  static_assert(32 * FD_JT / 4 == 64 * FD_NDI, "D chunk = whole DMA instructions");
-  static_assert(LDS <= 160 * 1024, "wgrad dma LDS");
-};
-constexpr int FD_JL[5] = {0, 4, 7, 10, 13};  // last i-block: j-blocks [JL s, JL s+1) on SIMD s
-
-// 16 bytes per lane from sbase + voff into LDS lds_dst + 16 lane (M0 = lds_dst)
-__device__ __forceinline__ void fd_dma16(const void* sbase, uint32_t voff, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(sbase), "s"(lds_dst)
-               : "memory");
-}
-template <int N>
-__device__ __forceinline__ void fd_wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// A fragment of one i-block from the raw ring: rows 4 G + j (j < 4) and 16 + 4 G + j - 4 of this
-// lane's column (the k order of tr_frag), P = row pitch in bytes (compile-time: the reads' offsets are
-// immediates), then masked / made (bias, zero) and split into the three planes
-// (MADE: the last i-block, whose lanes include the bias column (value orv) and zero columns: value =
-// (raw & xm) | orv; the t = 0 rows of H_{t-1} are zeroed in LDS before the chunk's barrier)
-template <int P>
-__device__ __forceinline__ void fd_areads(const lds_char* a0, float (&r)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = *reinterpret_cast<const __attribute__((address_space(3))) float*>(a0 + (j < 4 ? j : 12 + j) * P);
-}
-// rows h (0: j < 4, 1: j >= 4) of the fragment: four values split into dwords 2 h, 2 h + 1 of the planes
-template <bool MADE>
-__device__ __forceinline__ void fd_asplit(const float (&r)[8], int h, uint32_t xm, uint32_t orv, uint32_t (&pk)[3][4]) {
-  f32x4 v;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float rj = r[4 * h + j];
-    v[j] = MADE ? __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, rj) & xm) | orv) : rj;
-  }
-  uint32_t p[3][2];
-  split3(v, p);
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    pk[q][2 * h] = p[q][0];
-    pk[q][2 * h + 1] = p[q][1];
-  }
-}
-// (row pitch P per lane at run time: K = 32, whose X and H blocks differ in pitch)
-__device__ __forceinline__ void fd_areads_rt(const lds_char* a0, int P, float (&r)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = *reinterpret_cast<const __attribute__((address_space(3))) float*>(a0 + (j < 4 ? j : 12 + j) * P);
-}
-template <int P, bool MADE>
-__device__ __forceinline__ void fd_afrag(const lds_char* a0, uint32_t xm, uint32_t orv, bf16x8 (&af)[3]) {
-  float r[8];
-  fd_areads<P>(a0, r);
-  f32x4 v[2];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float rj = r[j];
-    v[j >> 2][j & 3] = MADE ? __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, rj) & xm) | orv) : rj;
-  }
-  uint32_t p0[3][2], p1[3][2];
-  split3(v[0], p0);
-  split3(v[1], p1);
-#pragma unroll
-  for (int q = 0; q < 3; ++q) af[q] = __builtin_bit_cast(bf16x8, make_uint4(p0[q][0], p0[q][1], p1[q][0], p1[q][1]));
-}
-
-template <int K>
-__global__ void __launch_bounds__(512, 1)
-lstmf_wgrad_dma_kernel(const float* __restrict__ X0, const float* __restrict__ H0, const float* __restrict__ D0,
-                       const float* __restrict__ X1, const float* __restrict__ H1, const float* __restrict__ D1,
-                       float* __restrict__ slab, int M, int Tn, int nseg, int rps) {
-  using G = FDGeo<K>;
-  constexpr int IPS = G::IPS, NPA = G::NPA, NPD = G::NPD;
-  extern __shared__ __attribute__((aligned(1024))) unsigned char fd_smem[];
-  lds_char* sm = (lds_char*)fd_smem;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)sm;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int s = w & 3, half = w >> 2;
-  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-  const int z = (slot >> 1) * 8 + xcd, tj = slot & 1;
-  const int jbase = tj * FD_JT;
-  const int mb = z * rps, me = min(M, mb + rps);
-  const int nchs = me > mb ? (me - mb + 31) / 32 : 0, nch = nchs * nseg;
-
-  // zero the whole LDS once: reads past a stage's images (clamped last chunk) must see finite data
-  for (int i = tid; i < G::LDS / 16; i += 512)
-    reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(sm)[i] = u32x4_t{0, 0, 0, 0};
-  __syncthreads();
-
-  // chunk c -> segment sg, first row m0, image base rows xl (X) and hl (H_{t-1}, row m0 - 1 first)
-  auto chunk_rows = [&](int c, int& sg, int& m0, int& xl, int& hl) {
-    sg = c >= nchs;
-    m0 = mb + (c - sg * nchs) * 32;
-    xl = min(m0, M - 32);
-    hl = max(min(m0 - 1, M - 32), 0);
-  };
-  // D float4 n * 64 + lane of the chunk (DMA instruction n = w + 8 k): row r, column group c4
-  int drc[NPD];  // (r << 8) | c4, or -1 past the chunk
-#pragma unroll
-  for (int k = 0; k < NPD; ++k) {
-    const int n = w + FD_W * k, e = n * 64 + lane, r = e / 52, c4 = e - 52 * r;
-    drc[k] = n < FD_NDI ? (r << 8) | c4 : -1;
-  }
-  // the chunk's DMA: D first (this wave's own float4s), then the A images into stage st
-  auto issue = [&](int c, int st) {
-    if (c >= nch) {  // ring tail: per-wave counts stay uniform
-#pragma unroll
-      for (int k = 0; k < NPD + NPA; ++k)
-        if (lane == 0) fd_dma16(X0, 0u, lds0 + G::TRASH);
-      return;
-    }
-    int sg, m0, xl, hl;
-    chunk_rows(c, sg, m0, xl, hl);
-    const char* db = reinterpret_cast<const char*>((sg ? D1 : D0) + (size_t)m0 * FG + jbase);
-    const int rmax = M - 1 - m0;  // rows past the tensor: re-read a row that exists (masked when staged)
-#pragma unroll
-    for (int k = 0; k < NPD; ++k) {
-      const int n = w + FD_W * k;
-      const int r = min(drc[k] >> 8, rmax), c4 = min(drc[k] & 255, (FG - jbase) / 4 - 1);
-      if (n < FD_NDI) fd_dma16(db, (uint32_t)((r * FG + 4 * c4) * 4), lds0 + G::RAWD + n * 1024);
-      else if (lane == 0) fd_dma16(X0, 0u, lds0 + G::TRASH);
-    }
-    const char* xb = reinterpret_cast<const char*>(sg ? X1 : X0) + (size_t)xl * K * 4;
-    const char* hb = reinterpret_cast<const char*>(sg ? H1 : H0) + (size_t)hl * FH * 4;
-#pragma unroll
-    for (int k = 0; k < NPA; ++k) {
-      const int n = w + FD_W * k;
-      if (n < G::XI) {
-        const uint32_t vo = n * 1024 + lane * 16;
-        if (vo < (uint32_t)G::XB) fd_dma16(xb, vo, lds0 + st * G::STAGE + n * 1024);
-      } else if (n < G::NI) {
-        const uint32_t vo = (n - G::XI) * 1024 + lane * 16;
-        if (vo < (uint32_t)G::HB) fd_dma16(hb, vo, lds0 + st * G::STAGE + G::OFF_H + (n - G::XI) * 1024);
-      } else if (lane == 0) {
-        fd_dma16(X0, 0u, lds0 + G::TRASH);
-      }
-    }
-  };
-  // this wave's raw D float4s of chunk c -> planes buffer buf (rows past the range / columns past N: 0)
-  auto stage_d = [&](int c, int buf) {
-    int sg, m0, xl, hl;
-    chunk_rows(c < nch ? c : 0, sg, m0, xl, hl);
-    const int rlim = c < nch ? me - m0 : 0;
-#pragma unroll
-    for (int k = 0; k < NPD; ++k) {
-      const int n = w + FD_W * k;
-      if (n >= FD_NDI) continue;  // (wave-uniform)
-      const int r = drc[k] >> 8, c4 = drc[k] & 255;
-      f32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(sm + G::RAWD + n * 1024 + lane * 16);
-      const bool ok = r < rlim && jbase + 4 * c4 < FG;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = ok ? v[e] : 0.f;
-      uint32_t p[3][2];
-      split3(v, p);
-      lds_char* d = sm + G::DOFF + buf * FD_DBUF + r * FD_ROWD + 8 * c4;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(d + q * FD_PLD) = u32x2_t{p[q][0], p[q][1]};
-    }
-  };
-
-  // ---- A fragment geometry of this lane: the wave's IPS base i-blocks (+ the last block, half 1)
-  const int g = lane >> 4, c16 = lane & 15;
-  constexpr int NB = IPS + 1;
-  int aoff[NB];       // LDS byte offset in a stage of row 4 g, this lane's column (0 for bias / zero lanes)
-  bool aH[NB];        // H_{t-1} column
-  uint32_t aX[NB];    // X column: all ones mask; bias / zero: 0
-  bool aB[NB];        // bias column
-#pragma unroll
-  for (int r = 0; r < NB; ++r) {
-    const int ib = r < IPS ? IPS * s + r : G::NIB - 1;
-    const int i = 16 * ib + c16;
-    aH[r] = i >= K && i < K + FH;
-    aX[r] = i < K ? 0xffffffffu : 0u;
-    aB[r] = i == K + FH;
-    aoff[r] = i < K ? 4 * g * K * 4 + i * 4 : aH[r] ? G::OFF_H + 4 * g * FH * 4 + (i - K) * 4 : 0;
-  }
-  const int step32 = 32 % Tn;
-  int tro_d = tr_lane_off(lane, FD_ROWD);
-
-  // ---- prologue: chunk 0 landed and its D planes staged
-  issue(0, 0);
-  fd_wait_vm<0>();
-  stage_d(0, 0);
-
-  // the chunk loop and the slab store, one instantiation per wave half (compile-time j-blocks and
-  // accumulator count: 7 IPS tiles for half 0, 6 IPS + <= 4 for half 1)
-  auto body = [&](auto HALF_) {
-    constexpr int HALF = decltype(HALF_)::value;
-    constexpr int NJB = HALF ? 6 : 7, JB0 = HALF ? 7 : 0;
-    constexpr int NT = HALF ? 6 * IPS + 4 : 7 * IPS;
-    f32x4 acc[NT];
-#pragma unroll
-    for (int a = 0; a < NT; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
-    int t0 = __builtin_amdgcn_readfirstlane(mb % Tn);  // (row m0) mod Tn
-    // one loop body (a compile-time buffer parity unrolled by two kept both parities' address bases
-    // live and spilled at K = 100)
-    auto chunk = [&](int c) {
-      const int S = c & 1;  // A stage and planes buffer of chunk c
-      // per-lane bases opaque at every chunk: the compiler otherwise hoisted every address derived from
-      // them out of the loop (one register each) and spilled
-#pragma unroll
-      for (int r = 0; r < NB; ++r) asm volatile("" : "+v"(aoff[r]));
-#pragma unroll
-      for (int k = 0; k < NPD; ++k) asm volatile("" : "+v"(drc[k]));
-      asm volatile("" : "+v"(tro_d));
-      int sg, m0, xl, hl;
-      chunk_rows(c, sg, m0, xl, hl);
-      if (c == nchs) t0 = __builtin_amdgcn_readfirstlane(mb % Tn);  // second segment
-      // rows of this chunk with t = 0 (their H_{t-1} belongs to the previous window): bit rr of zm
-      uint32_t zm = 0;
-      for (int rr = t0 == 0 ? 0 : Tn - t0; rr < 32; rr += Tn) zm |= 1u << rr;
-      t0 += step32;
-      if (t0 >= Tn) t0 -= Tn;
-      fd_wait_vm<0>();  // this wave's DMA of chunk c has landed: zero the t = 0 rows among its H bytes
-      {
-        const int hoff = m0 - 1 - hl;  // H image row of chunk row rr: rr + hoff
-#pragma unroll
-        for (int k = 0; k < NPA; ++k) {
-          const int n = w + FD_W * k;
-          if (n < G::XI || n >= G::NI) continue;  // (wave-uniform)
-          const int bo = (n - G::XI) * 1024 + lane * 16, rr = bo / (FH * 4) - hoff;
-          if (bo < G::HB && rr >= 0 && rr < 32 && ((zm >> rr) & 1u))
-            *reinterpret_cast<__attribute__((address_space(3))) u32x4_t*>(sm + S * G::STAGE + G::OFF_H + bo) = u32x4_t{0, 0, 0, 0};
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      issue(c + 1, S ^ 1);
-      const uint32_t bval = sg ? 0u : 0x3f800000u;
-      const int stb = S * G::STAGE;
-      const int xs = (m0 - xl) * K * 4, hs = (m0 - 1 - hl) * FH * 4;  // row shifts of the images
-      const lds_char* dpl = sm + G::DOFF + S * FD_DBUF;
-      auto block = [&](auto R_, bf16x8 (&af)[3]) {
-        constexpr int r = decltype(R_)::value;
-        constexpr bool MADE = r == IPS;  // the last i-block
-        const lds_char* a0 = sm + stb + aoff[r] + (aH[r] ? hs : aX[r] ? xs : 0);
-        const uint32_t xm = aH[r] ? 0xffffffffu : aX[r], orv = aB[r] ? bval : 0u;
-        if constexpr (K == 100) {
-          fd_afrag<K * 4, MADE>(a0, xm, orv, af);  // X and H rows share the 400-byte pitch
-        } else {
-          if (aH[r] || !aX[r]) fd_afrag<FH * 4, MADE>(a0, xm, orv, af);  // (wave-uniform for K = 32)
-          else fd_afrag<K * 4, MADE>(a0, xm, orv, af);
-        }
-      };
-      auto bload = [&](bf16x8 (&bf)[3], int jb) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) bf[q] = tr_frag<FD_ROWD>(dpl + q * FD_PLD, tro_d, 16 * jb);
-      };
-      // NJ tiles of one i-block: the B fragments one tile ahead, one tile per scheduling region (the
-      // scheduler otherwise hoisted every tile's transposed reads to the top and ran out of registers).
-      // Straight-line: no runtime trip count (a loop exit between an MFMA and the VALU read of its
-      // result got 1 wait state of the 7 needed, tests/test_isa_hazards.py)
-      auto tiles = [&](const bf16x8 (&a3)[3], int jf, auto NJ_, auto ACC0_) {
-        constexpr int NJ = decltype(NJ_)::value, ACC0 = decltype(ACC0_)::value;
-        bf16x8 bf[2][3];
-        bload(bf[0], jf);
-        f32x4 tp;  // the previous tile's products: added after this tile's MFMAs are issued
-#pragma unroll
-        for (int jj = 0; jj < NJ; ++jj) {
-          __builtin_amdgcn_sched_barrier(0);
-          if (jj + 1 < NJ) bload(bf[(jj + 1) & 1], jf + jj + 1);
-          const bf16x8(&b3)[3] = bf[jj & 1];
-          f32x4 t = mma32(a3[2], b3[0], f32x4{0.f, 0.f, 0.f, 0.f});  // lh
-          t = mma32(a3[0], b3[2], t);                                 // hl
-          t = mma32(a3[1], b3[1], t);                                 // mm
-          t = mma32(a3[1], b3[0], t);                                 // mh
-          t = mma32(a3[0], b3[1], t);                                 // hm
-          t = mma32(a3[0], b3[0], t);                                 // hh
-          if (jj > 0) acc[ACC0 + jj - 1] += tp;
-          tp = t;
-        }
-        acc[ACC0 + NJ - 1] += tp;
-        __builtin_amdgcn_sched_barrier(0);
-      };
-#if HFREP_WDMA_IL
-      // the next i-block's A fragments are built between this block's tiles: reads after tile 0, the
-      // split of its two row halves after tiles 2 and 3 (the VALU issues beside the MFMAs)
-      auto a_reads = [&](auto R_, float (&rv)[8]) {
-        constexpr int r = decltype(R_)::value;
-        const lds_char* a0 = sm + stb + aoff[r] + (aH[r] ? hs : aX[r] ? xs : 0);
-        if constexpr (K == 100) fd_areads<K * 4>(a0, rv);
-        else fd_areads_rt(a0, aX[r] ? K * 4 : FH * 4, rv);
-      };
-      auto a_split = [&](auto R_, const float (&rv)[8], int h, uint32_t (&pk)[3][4]) {
-        constexpr int r = decltype(R_)::value;
-        const uint32_t xm = aH[r] ? 0xffffffffu : aX[r], orv = aB[r] ? bval : 0u;
-        fd_asplit<r == IPS>(rv, h, xm, orv, pk);
-      };
-      // NJ tiles of block R (fragments a3) and, if NXT, the pieces of block R + 1 into an
-      auto tiles2 = [&](const bf16x8 (&a3)[3], int jf, auto NJ_, auto ACC0_, auto R_, auto NXT_, bf16x8 (&an)[3]) {
-        constexpr int NJ = decltype(NJ_)::value, ACC0 = decltype(ACC0_)::value, R = decltype(R_)::value;
-        constexpr bool NXT = decltype(NXT_)::value;
-        static_assert(!NXT || NJ >= 4, "next-block pieces need four tiles");
-        bf16x8 bf[2][3];
-        bload(bf[0], jf);
-        f32x4 tp;
-        float rv[8];
-        uint32_t pk[3][4];
-#pragma unroll
-        for (int jj = 0; jj < NJ; ++jj) {
-          __builtin_amdgcn_sched_barrier(0);
-          if (jj + 1 < NJ) bload(bf[(jj + 1) & 1], jf + jj + 1);
-          const bf16x8(&b3)[3] = bf[jj & 1];
-          f32x4 t = mma32(a3[2], b3[0], f32x4{0.f, 0.f, 0.f, 0.f});  // lh
-          t = mma32(a3[0], b3[2], t);                                 // hl
-          t = mma32(a3[1], b3[1], t);                                 // mm
-          t = mma32(a3[1], b3[0], t);                                 // mh
-          t = mma32(a3[0], b3[1], t);                                 // hm
-          t = mma32(a3[0], b3[0], t);                                 // hh
-          if constexpr (NXT) {
-            if (jj == 0) a_reads(std::integral_constant<int, R + 1>{}, rv);
-            if (jj == 2) a_split(std::integral_constant<int, R + 1>{}, rv, 0, pk);
-            if (jj == 3) {
-              a_split(std::integral_constant<int, R + 1>{}, rv, 1, pk);
-#pragma unroll
-              for (int q = 0; q < 3; ++q) an[q] = __builtin_bit_cast(bf16x8, make_uint4(pk[q][0], pk[q][1], pk[q][2], pk[q][3]));
-            }
-          }
-          if (jj > 0) acc[ACC0 + jj - 1] += tp;
-          tp = t;
-        }
-        acc[ACC0 + NJ - 1] += tp;
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      constexpr int NBLK = IPS + HALF;  // i-blocks of this wave
-      bf16x8 af[2][3];
-      block(std::integral_constant<int, 0>{}, af[0]);
-      auto rr = [&](auto R_) {
-        constexpr int r = decltype(R_)::value;
-        constexpr bool NXT = r + 1 < NBLK;
-        if constexpr (r < IPS)
-          tiles2(af[r & 1], JB0, std::integral_constant<int, NJB>{}, std::integral_constant<int, NJB * r>{}, R_,
-                 std::integral_constant<bool, NXT>{}, af[(r + 1) & 1]);
-        else  // the last i-block (half 1): this SIMD's quarter of its j-blocks (the 4th of SIMDs 1-3 dropped)
-          tiles2(af[r & 1], FD_JL[s], std::integral_constant<int, 4>{}, std::integral_constant<int, 6 * IPS>{}, R_,
-                 std::integral_constant<bool, false>{}, af[(r + 1) & 1]);
-        if (r == IPS - 1) {
-          fd_wait_vm<NPA>();  // this wave's D DMA of chunk c + 1 (issued before its A DMA) has landed
-          stage_d(c + 1, S ^ 1);
-        }
-      };
-      rr(std::integral_constant<int, 0>{});
-      rr(std::integral_constant<int, 1>{});
-      if constexpr (NBLK > 2) rr(std::integral_constant<int, 2>{});
-      if constexpr (NBLK > 3) rr(std::integral_constant<int, 3>{});
-      static_assert(NBLK <= 4, "i-blocks per wave");
-    };
-#else
-      // base i-blocks: IPS x NJB tiles; this wave's raw D of chunk c + 1 is split into the other
-      // planes buffer after the first one (its DMA was issued at the top of this chunk)
-      auto rr = [&](auto R_) {
-        constexpr int r = decltype(R_)::value;
-        bf16x8 af[3];
-        block(R_, af);
-        tiles(af, JB0, std::integral_constant<int, NJB>{}, std::integral_constant<int, NJB * r>{});
-        if (r == IPS - 1) {
-          fd_wait_vm<NPA>();  // this wave's D DMA of chunk c + 1 (issued before its A DMA) has landed
-          stage_d(c + 1, S ^ 1);
-        }
-      };
-      rr(std::integral_constant<int, 0>{});
-      rr(std::integral_constant<int, 1>{});
-      if constexpr (IPS > 2) rr(std::integral_constant<int, 2>{});
-      if constexpr (HALF == 1) {  // the last i-block: this SIMD's quarter of its j-blocks (3 or 4: the
-        bf16x8 af[3];             // fourth tile of SIMDs 1-3 is computed and dropped, as SIMD 0's is kept)
-        block(std::integral_constant<int, IPS>{}, af);
-        tiles(af, FD_JL[s], std::integral_constant<int, 4>{}, std::integral_constant<int, 6 * IPS>{});
-      }
-    };
-#endif
-    for (int c = 0; c < nch; ++c) chunk(c);
-    fd_wait_vm<0>();
-
-    // slab store: C[16 ib + 4 g + q][jbase + 16 jb + c16]
-    float* out = slab + (size_t)z * G::KTOT * FG;
-#pragma unroll
-    for (int r = 0; r < IPS + HALF; ++r) {
-      const int ib = r < IPS ? IPS * s + r : G::NIB - 1;
-      const int nj = r < IPS ? NJB : FD_JL[s + 1] - FD_JL[s];
-#pragma unroll
-      for (int jj = 0; jj < NJB; ++jj) {
-        if (jj >= nj) break;
-        const int jb = r < IPS ? JB0 + jj : FD_JL[s] + jj;
-        const int col = jbase + 16 * jb + c16;
-        const f32x4 v = acc[r < IPS ? NJB * r + jj : 6 * IPS + (jj < 4 ? jj : 3)];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = 16 * ib + 4 * g + q;
-          if (i < G::KTOT && col < FG) out[(size_t)i * FG + col] = v[q];
-        }
-      }
-    }
-  };
-  if (half) body(std::integral_constant<int, 1>{});
-  else body(std::integral_constant<int, 0>{});
-}
-
 constexpr int DS_KS = 13;  // the 400 gate columns as 13 k-steps of 32 (k = 400..415 zero)
 
 // ==========================================================================================
@@ -2530,10 +2093,9 @@ constexpr int DS4_PL = 16 * DS4_RS * 2;       // bytes per plane image (16 rows)
 constexpr int DS4_BUF = 3 * DS4_PL;           // one buffer: three planes
 constexpr int DS4_SLOTS = (16 * 100 + 255) / 256;  // float4 staging slots per thread per chunk (7)
 constexpr int DS4_K0 = DS_KS - DS4_SLOTS;     // first k-step followed by a staging slot
-#ifndef HFREP_DS4_SETS  // A/B: register sets of the dZ prefetch (2: one chunk ahead, 3: two chunks ahead)
-#define HFREP_DS4_SETS 2
-#endif
-constexpr int DS4_NS = HFREP_DS4_SETS;
+// register sets of the dZ prefetch: 2 = one chunk ahead (three sets, two chunks ahead, measured
+// 3.59 vs 3.54 ms at 6.3 M rows: profiles/r04_wgrad/wdma2)
+constexpr int DS4_NS = 2;
 
 template <int NT2>
 __global__ void __launch_bounds__(256, 1)
@@ -2607,7 +2169,6 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
 #pragma unroll
   for (int j = 0; j < DS4_SLOTS; ++j) stage(I0{}, dsm, j);
   load(I1{}, blockIdx.x + cs);
-  if constexpr (DS4_NS > 2) load(std::integral_constant<int, 2>{}, blockIdx.x + 2 * cs);
   __syncthreads();
   const int ao = (c16 * DS4_RS + 8 * g) * 2;  // this lane's A fragment: row c16, k = 8 g .. + 7 of a k-step
   // chunk cc (buffer S): chunk cc + 2 cs loaded into set S, the MFMAs on buffer S, chunk cc + cs (set
@@ -2665,23 +2226,11 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
     __syncthreads();
   };
   int c = blockIdx.x;
-  if constexpr (DS4_NS == 2) {
-    for (; c + cs < nch; c += 2 * cs) {
-      chunk(I0{}, c, 0);
-      chunk(I1{}, c + cs, 1);
-    }
-    if (c < nch) chunk(I0{}, c, 0);
-  } else {
-    int p = 0;  // LDS buffer of chunk c
-    for (; c + 2 * cs < nch; c += 3 * cs) {
-      chunk(I0{}, c, p);
-      chunk(I1{}, c + cs, p ^ 1);
-      chunk(std::integral_constant<int, 2>{}, c + 2 * cs, p);
-      p ^= 1;
-    }
-    if (c < nch) chunk(I0{}, c, p);
-    if (c + cs < nch) chunk(I1{}, c + cs, p ^ 1);
+  for (; c + cs < nch; c += 2 * cs) {
+    chunk(I0{}, c, 0);
+    chunk(I1{}, c + cs, 1);
   }
+  if (c < nch) chunk(I0{}, c, 0);
 }
 
 // ==========================================================================================
@@ -2970,40 +2519,21 @@ static int wgradq_z(int M) {
   const int chunks = (M + 31) / 32, q = device_cu_count() / 4;
   return chunks < q ? chunks : q;
 }
-// LDS-DMA streaming kernel: Z row ranges (a multiple of 8: the pair of a range shares an XCD) x 2
-// column halves, one workgroup per CU, at least two chunks per range
-static int wgradd_z(int M) {
-  const int half = device_cu_count() / 2, zmax = max(8, (M / 64) / 8 * 8);
-  return min(max(8, half / 8 * 8), zmax);
-}
 static int wgradf_pick(int impl, int K, int M) {
-  int v = impl >= 1 && impl <= 4 ? impl : wgradf_version();
-  if (K == 35 && v == 3) v = 2;                          // the quad kernel reads 16-byte X rows only
-  if (v == 4 && !((K == 32 || K == 100) && M >= 64)) v = 0;
+  (void)M;
+  int v = impl >= 1 && impl <= 3 ? impl : wgradf_version();
+  if (K == 35 && v == 3) v = 2;  // the quad kernel reads 16-byte X rows only
   return v ? v : (K <= 36 ? 2 : 3);
 }
 size_t lstmf_wgrad_workspace_floats(int M, int K, int impl) {
   const int v = wgradf_pick(impl, K, M);
-  const int z = v == 1 ? wgradf_grid(M) : v == 3 ? wgradq_z(M) : v == 4 ? wgradd_z(M) : wgrads_z(M);
+  const int z = v == 1 ? wgradf_grid(M) : v == 3 ? wgradq_z(M) : wgrads_z(M);
   return (size_t)z * ((K == 35 ? 36 : K) + FH + 1) * FG;
 }
 
 bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
                         float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl) {
   if (!lstmf_wgrad_supported(K, FH, FG) || M <= 0) return false;
-  if (wgradf_pick(impl, K, M) == 4) {
-    const int z = wgradd_z(M);
-    const int rps = ((M + z - 1) / z + 31) / 32 * 32;
-    const int nseg = Xd ? 2 : 1;
-    auto go = [&](auto k, size_t sm) {
-      allow_lds(reinterpret_cast<const void*>(k));
-      hipLaunchKernelGGL(k, dim3(2 * z), dim3(512), sm, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, nseg, rps);
-    };
-    if (K == 32) go(lstmf_wgrad_dma_kernel<32>, FDGeo<32>::LDS);
-    else go(lstmf_wgrad_dma_kernel<100>, FDGeo<100>::LDS);
-    launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s);
-    return true;
-  }
   if (wgradf_pick(impl, K, M) == 3) {
     const int z0 = wgradq_z(M);
     const int rpz = ((M + z0 - 1) / z0 + 31) / 32 * 32;

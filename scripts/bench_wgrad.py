@@ -25,7 +25,7 @@ def main():
     dt = getattr(torch, a.dtype)
     # bf16: impl 2 = tile kernel (gemm2), 0 = LDS-DMA streaming (wgrad3); fp32: 1 = exact MFMA, 2 = bf16 split
     impls, names = (((2, 0), {2: "wgrad2", 0: "wgrad3"}) if dt == torch.bfloat16 else
-                    ((1, 2, 3, 4), {1: "f32_exact", 2: "f32_split", 3: "f32_split_quad", 4: "f32_dma"}))
+                    ((1, 2, 3), {1: "f32_exact", 2: "f32_split", 3: "f32_split_quad"}))
     dev = torch.device("cuda:0")
     H, N = 100, 400
     for K, rows_mult, tangent in [(32, 2, False), (100, 2, False), (32, 1, True), (100, 1, True)]:

@@ -819,7 +819,7 @@ def test_lstmf_wgrad_fused(cuda, B, T, K, tangent):
                                            (41, 5, 36, True), (1000, 24, 100, True), (4500, 24, 32, False),
                                            (20000, 24, 100, True), (41, 5, 35, True), (3001, 24, 35, False)])
 def test_lstmf_wgrad_split_vs_exact(cuda, B, T, K, tangent):
-    """The three-term bf16 split weight gradients (impl 2 pair, 3 quad, 4 LDS-DMA streaming) and the exact-fp32
+    """The three-term bf16 split weight gradients (impl 2 pair, 3 quad) and the exact-fp32
     MFMA kernel (impl 1) vs fp64: all inside the fp32 tolerance and the splits' error within 2x the exact
     kernel's (the dropped split terms are <= 2^-24 of each product); bitwise run-to-run.  K = 35: the
     reference's 35-feature rows read in place (dword loads, a 36-column image; impl 3 falls back to 2)."""
@@ -836,7 +836,7 @@ def test_lstmf_wgrad_split_vs_exact(cuda, B, T, K, tangent):
         rW = rW + xd.double().reshape(-1, K).t() @ dzd.double().reshape(-1, N)
         rU = rU + R.shift_prev(hds.double()).reshape(-1, H).t() @ dzd.double().reshape(-1, N)
     errs = {}
-    for impl in (1, 2, 2, 3, 3, 4, 4):
+    for impl in (1, 2, 2, 3, 3):
         gW, gU, gb = torch.zeros(K, N, device=cuda), torch.zeros(H, N, device=cuda), torch.zeros(N, device=cuda)
         Fn.lstm_wgrad_(x, hs, dz, gW, gU, gb, xd, hds, dzd, impl=impl)
         out = torch.cat([gW.reshape(-1), gU.reshape(-1), gb])
@@ -846,11 +846,10 @@ def test_lstmf_wgrad_split_vs_exact(cuda, B, T, K, tangent):
         ref = torch.cat([rW.reshape(-1), rU.reshape(-1), rb])
         errs[impl] = ((out.double() - ref).abs().max().item(), out)
     refmax = max(rW.abs().max().item(), rU.abs().max().item(), rb.abs().max().item())
-    e1, e2, e3, e4 = errs[1][0], errs[2][0], errs[3][0], errs[4][0]
-    print(f"max abs err exact {e1:.3e} split {e2:.3e} quad {e3:.3e} dma {e4:.3e} (max |ref| {refmax:.3e})")
+    e1, e2, e3 = errs[1][0], errs[2][0], errs[3][0]
+    print(f"max abs err exact {e1:.3e} split {e2:.3e} quad {e3:.3e} (max |ref| {refmax:.3e})")
     assert e1 <= 1e-5 * refmax + 1e-5 and e2 <= 2 * e1 + 1e-6 * refmax, (e1, e2, refmax)
     assert e3 <= 2 * e1 + 1e-6 * refmax, (e1, e3, refmax)
-    assert e4 <= 2 * e1 + 1e-6 * refmax, (e1, e4, refmax)
 
 
 @pytest.mark.parametrize("K,tangent", [(100, False), (32, True)])
@@ -873,7 +872,7 @@ def test_lstmf_wgrad_large_m(cuda, K, tangent):
     rb = dz.double().reshape(-1, N).sum(0)
     # random-sign sums of 3 M products: scale by the root-sum-square, not the absolute sum
     tol = 2e-5 * (B * T) ** 0.5 * (2 if tangent else 1)
-    for impl in (1, 2, 3, 4):
+    for impl in (1, 2, 3):
         gW, gU, gb = (torch.zeros(K, N, device=cuda), torch.zeros(H, N, device=cuda), torch.zeros(N, device=cuda))
         Fn.lstm_wgrad_(x, hs, dz, gW, gU, gb, xd, hds, dzd, impl=impl)
         for got, ref in ((gW, rW), (gU, rU), (gb, rb)):
