@@ -109,7 +109,7 @@ bool launch_lstm_wgrad3(const void* X0, const void* H0, const void* D0, const vo
 
 // ---- skinny.hip (bf16 / fp32, N <= 4 output columns, K % 8 == 0: the Flatten -> Dense(1) critic head) ----
 bool skinny_supported(int K, int N);
-bool narrow_supported(int K, int N);  // 4 < N <= 64, K <= 128 (bf16 forward only)
+bool narrow_supported(int K, int N);  // 4 < N <= 64, K <= 128 even (bf16 forward only)
 void launch_narrow_fwd(const void* x, const float* W, const float* b, void* y, int M, int K, int N, int act,
                        hipStream_t s);
 // exact-fp32 narrow GEMM y = act(x B + b), B[k][n] = Bp[k sk + n sn]; K in {32, 36, 64, 100, 128}, 4 < N <= 112

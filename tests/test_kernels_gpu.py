@@ -35,7 +35,7 @@ def _ops():
 @pytest.mark.parametrize("M,K,N,act", [(1000, 32, 400, 0), (777, 100, 400, 0), (300, 35, 100, 1), (64, 2400, 1, 0),
                                        (257, 100, 35, 3), (40, 100, 100, 2), (70001, 100, 32, 0), (333, 36, 36, 1),
                                        (129, 22, 7, 3), (70001, 300, 100, 3), (1000, 96, 100, 3), (33, 300, 100, 0),
-                                       (517, 200, 250, 1)])
+                                       (517, 200, 250, 1), (77, 1, 22, 3), (130, 3, 22, 3), (65, 5, 22, 0), (99, 4, 22, 3)])
 def test_linear(cuda, dt, M, K, N, act):
     g = torch.Generator().manual_seed(0)
     x = torch.randn(M, K, generator=g) * 0.5
