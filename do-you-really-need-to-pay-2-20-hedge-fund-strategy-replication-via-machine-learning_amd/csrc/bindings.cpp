@@ -757,6 +757,53 @@ void clip_(Tensor p, double c) {
   hfrep::launch_clip(p.data_ptr<float>(), p.numel(), (float)c, cur_stream(p));
 }
 
+// ------------------------------------------------------------------------------------ p2p all-reduce
+// The buffer is a uint8 tensor over the hipExtMallocWithFlags allocation (freed by its deleter);
+// its data_ptr is the allocation base, which is what an IPC handle names.
+Tensor p2p_buffer(int64_t cap, int64_t device) {
+  TORCH_CHECK(cap > 0, "p2p_buffer: cap must be positive");
+  bool fine = false;
+  void* p = hfrep::p2p_alloc(cap, (int)device, &fine);
+  auto opts = at::TensorOptions().dtype(at::kByte).device(at::Device(at::kCUDA, (int)device));
+  return torch::from_blob(p, {(int64_t)hfrep::p2p_buffer_bytes(cap)}, [](void* q) { hfrep::p2p_free(q); }, opts);
+}
+
+std::vector<int64_t> p2p_handle(Tensor buf) {
+  TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kByte, "p2p_handle: a p2p_buffer tensor");
+  uint8_t h[64];
+  hfrep::p2p_ipc_handle(buf.data_ptr(), h);
+  return std::vector<int64_t>(h, h + 64);
+}
+
+int64_t p2p_open(std::vector<int64_t> handle, int64_t device) {
+  TORCH_CHECK(handle.size() == 64, "p2p_open: a 64-byte IPC handle");
+  uint8_t h[64];
+  for (int i = 0; i < 64; ++i) h[i] = (uint8_t)handle[i];
+  return (int64_t)reinterpret_cast<intptr_t>(hfrep::p2p_ipc_open(h, (int)device));
+}
+
+void p2p_close(int64_t ptr) { hfrep::p2p_ipc_close(reinterpret_cast<void*>((intptr_t)ptr)); }
+
+void p2p_allreduce_(Tensor x, Tensor buf, std::vector<int64_t> peers, int64_t rank, int64_t cap, double scale) {
+  CHECK_F32(x);
+  TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kByte && buf.device() == x.device(),
+              "p2p_allreduce_: buf must be this device's p2p_buffer");
+  const int world = (int)peers.size();
+  TORCH_CHECK(world >= 1 && world <= hfrep::kP2PMaxRanks && rank >= 0 && rank < world, "p2p_allreduce_: 1 <= world <= 8");
+  TORCH_CHECK(x.numel() <= cap && buf.numel() >= (int64_t)hfrep::p2p_buffer_bytes(cap), "p2p_allreduce_: x exceeds cap");
+  TORCH_CHECK(peers[rank] == (int64_t)reinterpret_cast<intptr_t>(buf.data_ptr()), "p2p_allreduce_: peers[rank] must be buf");
+  hfrep::P2PPeers pp{};
+  for (int r = 0; r < world; ++r) pp.base[r] = reinterpret_cast<char*>((intptr_t)peers[r]);
+  GUARD(x);
+  hfrep::launch_p2p_allreduce(x.data_ptr<float>(), x.numel(), pp, (int)rank, world, cap, (float)scale, cur_stream(x));
+}
+
+int64_t p2p_error(Tensor buf) {
+  TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kByte, "p2p_error: a p2p_buffer tensor");
+  GUARD(buf);
+  return hfrep::p2p_take_error(buf.data_ptr());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(hfrep, m) {
@@ -811,10 +858,19 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("nadam_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor m_cache, float lr, float b1, float b2, float eps, float gscale) -> ()");
   m.def("step_advance_(Tensor(a!) step, Tensor(b!)? m_cache, float b1) -> ()");
   m.def("clip_(Tensor(a!) p, float c) -> ()");
+  m.def("p2p_buffer(int cap, int device) -> Tensor", &p2p_buffer);  // no tensor inputs: catch-all kernel
+  m.def("p2p_handle(Tensor buf) -> int[]");
+  m.def("p2p_open(int[] handle, int device) -> int", &p2p_open);
+  m.def("p2p_close(int ptr) -> ()", &p2p_close);
+  m.def("p2p_allreduce_(Tensor(a!) x, Tensor buf, int[] peers, int rank, int cap, float scale) -> ()");
+  m.def("p2p_error(Tensor buf) -> int");
 }
 
 TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("linear", &linear);
+  m.impl("p2p_handle", &p2p_handle);
+  m.impl("p2p_allreduce_", &p2p_allreduce_);
+  m.impl("p2p_error", &p2p_error);
   m.impl("linear_dgrad", &linear_dgrad);
   m.impl("linear_wgrad_", &linear_wgrad_);
   m.impl("lstm_wgrad_", &lstm_wgrad_);

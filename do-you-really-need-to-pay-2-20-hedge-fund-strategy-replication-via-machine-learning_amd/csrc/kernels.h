@@ -175,4 +175,20 @@ void launch_nadam(float* p, const float* g, float* m, float* v, int64_t n, const
 void launch_step_advance(float* step, float* m_cache, float b1, hipStream_t s);
 void launch_clip(float* p, int64_t n, float c, hipStream_t s);
 
+// ---- p2p.hip: one-shot all-reduce over IPC-mapped peer buffers (layout in p2p.hip) ----
+constexpr int kP2PMaxRanks = 8, kP2PMaxBlocks = 256;
+constexpr int kP2PCtr = 0, kP2PDone = 128, kP2PErr = 256, kP2PFlags = 4096, kP2PData = 16384;
+struct P2PPeers { char* base[kP2PMaxRanks]; };  // every rank's buffer as mapped in this process
+size_t p2p_buffer_bytes(int64_t cap);
+void* p2p_alloc(int64_t cap, int device, bool* fine_grained);  // zeroed; throws std::runtime_error
+void p2p_free(void* p);
+void p2p_ipc_handle(void* p, uint8_t out[64]);
+void* p2p_ipc_open(const uint8_t h[64], int device);
+void p2p_ipc_close(void* p);
+int p2p_take_error(void* own);  // reads and clears the error word (synchronous)
+int p2p_blocks(int64_t n);
+// x[0 .. n) = scale * sum over ranks (rank order) of every rank's x; n <= cap, same n on every rank
+void launch_p2p_allreduce(float* x, int64_t n, const P2PPeers& peers, int rank, int world, int64_t cap, float scale,
+                          hipStream_t s);
+
 }  // namespace hfrep

@@ -83,11 +83,31 @@ class GradSync:
         # the newest async work: RCCL runs a group's collectives on one stream in issue order, so its
         # completion implies every earlier one's (graph capture waits for it, drain_)
         self._last = None
+        # HFREP_DP_P2P=1: buckets of <= HFREP_DP_P2P_CAP floats go through the one-shot IPC all-reduce
+        # (parallel/p2p.py, csrc/p2p.hip) on a side stream instead of RCCL; built at the first bucket
+        self.use_p2p = (os.environ.get("HFREP_DP_P2P", "0") == "1" and self.backend == "nccl" and world > 1)
+        self.p2p_cap = int(os.environ.get("HFREP_DP_P2P_CAP", str(1 << 21)))
+        self.p2p = None
+        self._p2p_stream = None
+
+    def _p2p_for(self, t: torch.Tensor):
+        """The one-shot all-reduce for bucket ``t`` (None: RCCL).  The first call is collective."""
+        if not self.use_p2p or t.numel() > self.p2p_cap or not t.is_cuda or t.dtype != torch.float32:
+            return None
+        if self.p2p is None:
+            from .p2p import P2PAllReduce
+
+            self.p2p = P2PAllReduce(self.group, cap=self.p2p_cap, device=t.device)
+            self._p2p_stream = torch.cuda.Stream(device=t.device)
+        return self.p2p
 
     def all_reduce_(self, flat_grad: torch.Tensor) -> None:
         if self.world <= 1:
             return
-        if self.backend == "nccl":
+        p2p = self._p2p_for(flat_grad)
+        if p2p is not None:
+            p2p.all_reduce_(flat_grad, average=True)
+        elif self.backend == "nccl":
             dist.all_reduce(flat_grad, op=dist.ReduceOp.AVG, group=self.bucket_group)
         else:
             dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.group)
@@ -104,7 +124,15 @@ class GradSync:
         """
         if self.world <= 1:
             return
-        if self.backend == "nccl":
+        p2p = self._p2p_for(grad_slice)
+        if p2p is not None:
+            # the side stream joins the compute stream here and is joined back in finish_
+            s = self._p2p_stream
+            s.wait_stream(torch.cuda.current_stream(grad_slice.device))
+            with torch.cuda.stream(s):
+                p2p.all_reduce_(grad_slice, average=True)
+            self._pending.append(("p2p", s))
+        elif self.backend == "nccl":
             w = dist.all_reduce(grad_slice, op=dist.ReduceOp.AVG, group=self.bucket_group, async_op=True)
             self._pending.append(w)
             self._last = w
@@ -115,7 +143,9 @@ class GradSync:
     def finish_(self) -> int:
         n = len(self._pending)
         for w in self._pending:
-            if isinstance(w, tuple):
+            if isinstance(w, tuple) and w[0] == "p2p":
+                torch.cuda.current_stream(w[1].device).wait_stream(w[1])
+            elif isinstance(w, tuple):
                 w[0].wait()
                 w[1].div_(self.world)
             else:

@@ -293,3 +293,21 @@ def test_nccl_graph_safe_env_defaults(monkeypatch):
     monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "1")
     nccl_graph_safe_env()
     assert os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] == "1"
+
+
+def test_gradsync_p2p_selection(monkeypatch):
+    """HFREP_DP_P2P=1 routes fp32 GPU buckets of <= HFREP_DP_P2P_CAP floats to the one-shot IPC
+    all-reduce (parallel/p2p.py) -- only for RCCL groups of > 1 rank; everything else stays on the
+    process group's collective (the kernel itself: tests/test_p2p_gpu.py)."""
+    from hfrep.parallel.dp import GradSync
+
+    monkeypatch.setenv("HFREP_DP_P2P", "1")
+    monkeypatch.setenv("HFREP_DP_P2P_CAP", "1000")
+    gs = GradSync(None, 2)
+    assert not gs.use_p2p  # no nccl group
+    gs.use_p2p = True
+    assert gs.p2p_cap == 1000
+    assert gs._p2p_for(torch.zeros(10)) is None  # CPU tensor
+    assert gs._p2p_for(torch.zeros(2000)) is None  # over the cap
+    monkeypatch.delenv("HFREP_DP_P2P")
+    assert not GradSync(None, 2).use_p2p

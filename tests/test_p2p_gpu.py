@@ -1,0 +1,137 @@
+"""The one-shot IPC all-reduce (``csrc/p2p.hip``, ``parallel/p2p.py``) with 2 and 8 real processes.
+
+RCCL refuses two ranks on one GPU (``profiles/r04_main/rccl_shared_gpu_probe.txt``), but HIP IPC does
+not: 2 (and 8, the node's rank count) spawned processes all bind cuda:0, exchange their buffers' IPC
+handles over a gloo group, and run the same kernel that would read the peers' buffers over xGMI on a
+node.  Checks: every size (1 element to the capacity, vector and scalar tails) equals the fp32
+rank-order sum bit for bit on every rank, the average variant, a hipGraph-captured call replayed with new inputs (device-side
+epochs), GradSync's bucketed start_ / finish_ through the side stream, and a clean error word.
+"""
+import socket
+import traceback
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 3, 4, 1000, 4097, 65538, 1 << 20]
+
+
+def _inputs(n, tag, world):
+    import torch
+
+    out = []
+    for r in range(world):
+        g = torch.Generator().manual_seed(1000003 * n + 7919 * tag + r)
+        out.append(torch.randn(n, generator=g))
+    return out
+
+
+def _expect(xs, scale=None):
+    s = xs[0] * 0
+    for x in xs:
+        s = s + x  # fp32, rank order: the kernel's summation
+    return s if scale is None else s * scale
+
+
+def _worker(rank, world, port, q):
+    try:
+        import os
+
+        import torch
+        import torch.distributed as dist
+
+        import hfrep  # noqa: F401
+        from hfrep.parallel.dp import GradSync
+        from hfrep.parallel.p2p import P2PAllReduce
+
+        os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        ar = P2PAllReduce(dist.group.WORLD, cap=1 << 20, device=dev)
+        res = {"rank": rank, "bad": []}
+        tag = 0
+        for n in SIZES:
+            for avg in (False, True):
+                tag += 1
+                xs = _inputs(n, tag, world)
+                x = xs[rank].to(dev)
+                dist.barrier()
+                ar.all_reduce_(x, average=avg)
+                torch.cuda.synchronize()
+                if not torch.equal(x.cpu(), _expect(xs, torch.tensor(1.0 / world) if avg else None)):
+                    res["bad"].append(("eager", n, avg))
+        # hipGraph: capture once, replay with new inputs
+        n = 70001
+        xst = torch.zeros(n, device=dev)
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            dist.barrier()
+            ar.all_reduce_(xst)  # eager warmup on the capture stream
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            ar.all_reduce_(xst)
+        for rep in range(3):
+            tag += 1
+            xs = _inputs(n, tag, world)
+            xst.copy_(xs[rank].to(dev))
+            torch.cuda.synchronize()
+            dist.barrier()
+            g.replay()
+            torch.cuda.synchronize()
+            if not torch.equal(xst.cpu(), _expect(xs)):
+                res["bad"].append(("graph", rep))
+        # GradSync's bucketed path (start_ on the side stream, finish_ joins it)
+        gs = GradSync(dist.group.WORLD, world, buckets=2)
+        gs.use_p2p = True  # (the env switch is for nccl groups; the handles here go over gloo)
+        tag += 1
+        xs = _inputs(50000, tag, world)
+        flat = xs[rank].to(dev)
+        dist.barrier()
+        gs.start_(flat[:20000])
+        gs.start_(flat[20000:])
+        gs.finish_()
+        torch.cuda.synchronize()
+        want = torch.cat([_expect([x[:20000] for x in xs], torch.tensor(1.0 / world)),
+                          _expect([x[20000:] for x in xs], torch.tensor(1.0 / world))])
+        if not torch.equal(flat.cpu(), want):
+            res["bad"].append(("gradsync",))
+        ar.check()
+        res["epochs"] = int(ar.buf[:4].view(torch.int32).item())
+        dist.barrier()
+        ar.close()
+        gs.p2p.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put(res)
+    except Exception:
+        q.put(traceback.format_exc())
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_p2p_allreduce_processes(cuda, world):
+    import torch.multiprocessing as mp
+
+    from _spawn import gather
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = gather(procs, q, world, timeout=240)
+    for p in procs:
+        p.join(timeout=30)
+    for r in res:
+        assert not isinstance(r, str), r
+        assert r["bad"] == [], r
+        # 14 eager + 1 warmup + 3 replays
+        assert r["epochs"] == 2 * len(SIZES) + 1 + 3, r
