@@ -1435,10 +1435,14 @@ static int lstm_dbg() {
 
 // act (0 linear, 1 sigmoid, 2 tanh) and the input width K are template parameters: the cell
 // activation switch and the x-tile index arithmetic would otherwise sit in the hottest loop.
+// (the tangent forward is never instantiated for act = sigmoid: that instantiation was not bitwise
+// reproducible at B = 32772 and launch_lstm2_tfwd routes act = 1 to lstm_tfwd2)
 #define HFREP_FWD4_ACT(KXV, TP, TN, ...)                                                          \
   switch (act) {                                                                                 \
     case 0: launch(lstm_fwd4_kernel<100, 0, KXV, TP, TN>, __VA_ARGS__); break;                   \
-    case 1: launch(lstm_fwd4_kernel<100, 1, KXV, TP, TN>, __VA_ARGS__); break;                   \
+    case 1:                                                                                      \
+      if constexpr (!TN) launch(lstm_fwd4_kernel<100, 1, KXV, TP, false>, __VA_ARGS__);          \
+      break;                                                                                     \
     default: launch(lstm_fwd4_kernel<100, 2, KXV, TP, TN>, __VA_ARGS__); break;                  \
   }
 #define HFREP_FWD4_K(TP, TN, ...)                                                                \
