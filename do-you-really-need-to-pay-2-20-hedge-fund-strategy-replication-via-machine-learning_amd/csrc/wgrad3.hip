@@ -92,17 +92,20 @@ __device__ __forceinline__ bf16x8 tr2(uint32_t lo, uint32_t hi) {
 
 }  // namespace
 
-template <int K, int HD>
-__global__ void __launch_bounds__(512, 1)
-lstm_wgrad3_kernel(const bf16_t* __restrict__ X0, const bf16_t* __restrict__ H0, const bf16_t* __restrict__ D0,
-                   const bf16_t* __restrict__ X1, const bf16_t* __restrict__ H1, const bf16_t* __restrict__ D1,
-                   float* __restrict__ slab, int M, int Tn, int nseg, int rps) {
+// One wave's whole loop, with the wave index W a compile-time constant: the DMA plan (which image
+// each of the wave's NPW instructions fills), the i-blocks / j-blocks it owns and their operand kinds
+// fold into straight-line code.  With W a run-time value the loop carried ~150 scalar instructions
+// and ~50 branches per 32-row chunk and wave (pointer selects per DMA slot, wave-kind tests;
+// profiles/r04_wgrad3/README.md), which -- not the bytes -- set the chunk time.
+template <int K, int HD, int W>
+__device__ __forceinline__ void wgrad3_wave(const bf16_t* __restrict__ X0, const bf16_t* __restrict__ H0,
+                                            const bf16_t* __restrict__ D0, const bf16_t* __restrict__ X1,
+                                            const bf16_t* __restrict__ H1, const bf16_t* __restrict__ D1,
+                                            float* __restrict__ slab, int M, int Tn, int nseg, int rps,
+                                            unsigned char* smem, uint32_t lds0, int lane) {
   using G = W3<K, HD>;
-  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ig = w & 3, jh = w >> 2;  // i-group, j-half of this wave
+  constexpr int w = W;
+  constexpr int ig = w & 3, jh = w >> 2;  // i-group, j-half of this wave
   // blocks b and b+8 share an XCD: they take the two j-tiles of one split
   const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
   const int z = (slot >> 1) * 8 + xcd, tj = slot & 1;
@@ -110,9 +113,6 @@ lstm_wgrad3_kernel(const bf16_t* __restrict__ X0, const bf16_t* __restrict__ H0,
   const int mb = z * rps, me = min(M, mb + rps);
   const int nchs = me > mb ? (me - mb + 31) / 32 : 0;  // chunks per segment
   const int nch = nchs * nseg;
-
-  if (tid < 16) reinterpret_cast<uint16_t*>(smem + G::PADS)[tid] = (tid == 8) ? (uint16_t)0x3f80 : (uint16_t)0;
-  __syncthreads();  // nothing in flight yet: the only full barrier of the kernel
 
   // ---- per-lane DMA geometry of this wave's NPW instructions (chunk independent)
   uint32_t voff[G::NPW], vdst[G::NPW];
@@ -254,6 +254,32 @@ lstm_wgrad3_kernel(const bf16_t* __restrict__ X0, const bf16_t* __restrict__ H0,
       }
     }
   }
+}
+
+template <int K, int HD>
+__global__ void __launch_bounds__(512, 1)
+lstm_wgrad3_kernel(const bf16_t* __restrict__ X0, const bf16_t* __restrict__ H0, const bf16_t* __restrict__ D0,
+                   const bf16_t* __restrict__ X1, const bf16_t* __restrict__ H1, const bf16_t* __restrict__ D1,
+                   float* __restrict__ slab, int M, int Tn, int nseg, int rps) {
+  using G = W3<K, HD>;
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid < 16) reinterpret_cast<uint16_t*>(smem + G::PADS)[tid] = (tid == 8) ? (uint16_t)0x3f80 : (uint16_t)0;
+  __syncthreads();  // nothing in flight yet: the only full barrier of the kernel
+#define HFREP_W3_WAVE(WV) wgrad3_wave<K, HD, WV>(X0, H0, D0, X1, H1, D1, slab, M, Tn, nseg, rps, smem, lds0, lane)
+  switch (w) {
+    case 0: HFREP_W3_WAVE(0); break;
+    case 1: HFREP_W3_WAVE(1); break;
+    case 2: HFREP_W3_WAVE(2); break;
+    case 3: HFREP_W3_WAVE(3); break;
+    case 4: HFREP_W3_WAVE(4); break;
+    case 5: HFREP_W3_WAVE(5); break;
+    case 6: HFREP_W3_WAVE(6); break;
+    default: HFREP_W3_WAVE(7); break;
+  }
+#undef HFREP_W3_WAVE
 }
 
 template <int K, int HD>
