@@ -6,12 +6,15 @@
 // The op reads ~1 GB per call at the flagship shape and does ~130 GFLOP: it is an HBM-streaming
 // problem, so the design is organised around bytes in flight, not MFMA tiling:
 //
-//  * one workgroup per CU (4 waves, one per SIMD), each owning ALL Ktot rows x one 208-column
-//    j-tile of C (two j-tiles cover N = 400) in registers (4 i-blocks x 13 j-blocks of 16x16
-//    accumulators per wave); a split of M rows is walked in 32-row chunks, one MFMA k-step each;
+//  * one workgroup per CU (8 waves, two per SIMD) owning ALL of C in registers: wave w holds i-group
+//    w & 3 (i-blocks w & 3 + 4 k) x j-half w >> 2 (13 / 12 of the 25 j-blocks of 16x16 accumulators,
+//    208 registers at K = 100); a split of M rows is walked in 32-row chunks, one MFMA k-step each.
+//    Round 4 replaced two 208-column j-tiles on paired workgroups (the second X / H read an L2 hit):
+//    LDS-DMA is bound per CU (~24 GB/s), so every X / H byte DMA'd twice cost time even from L2 --
+//    full width moves 26 % (K = 100) / 22 % (K = 32) fewer bytes per CU and row (2.90 vs 3.40 ms and
+//    2.43 vs 2.89 ms per call at the bench shape, profiles/r04_wgrad3);
 //  * every chunk lands in LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction):
-//    X rows m0..m0+31, H rows m0-1..m0+30 and the D j-tile are contiguous or row-strided HBM
-//    ranges, copied raw (no transposes, no register staging) into a 4-deep ring, so three chunks
+//    X rows m0..m0+31, H rows m0-1..m0+30 and the D rows are contiguous HBM ranges, copied raw (no transposes, no register staging) into a 4-deep ring, so three chunks
 //    (~80 KB per CU) are in flight while the fourth is consumed.  Waits are counted
 //    (s_waitcnt vmcnt(2 chunks)) and the barrier is a raw s_barrier, so the DMA is never drained
 //    inside the loop;
@@ -19,8 +22,7 @@
 //    reduction index m must sit inside each lane's fragment), with per-lane addresses: the
 //    h_{t-1} shift, the m % T == 0 zero rows, the all-ones bias row and the tail mask are pointer
 //    selects onto a 16-byte zero / ones pad in LDS, never data movement;
-//  * XCD-aware block map: the two j-tiles of a split are blocks b and b+8, i.e. the same XCD, so
-//    the second read of the A chunk is an L2 hit.
+//  * the loop body is instantiated per wave index (wgrad3_wave<K, HD, W>).
 // The fp32 partials go to per-split slabs reduced by lstm_wgrad2_reduce_kernel (deterministic).
 #include "common.h"
 #include "mfma.h"
@@ -39,7 +41,7 @@ constexpr int W3_WAVES = 8;
 template <int K, int HD>
 struct W3 {
   static constexpr int N = 4 * HD;
-  static constexpr int JT = 208;  // j-tile: 13 x 16 columns; two tiles cover N <= 416
+  static constexpr int JT = N;  // one full-width j-tile: each X / H / D chunk is DMA'd once
   static constexpr int NJB = JT / 16;
   static constexpr int NJT = (N + JT - 1) / JT;
   static constexpr int JBW = (NJB + 1) / 2;            // j-blocks per wave (waves 0-3: first half)
@@ -61,7 +63,7 @@ struct W3 {
   static_assert(K % 4 == 0 && HD % 4 == 0, "4-column groups must not straddle X/H");
   static_assert((32 * JT * 2) % 1024 == 0, "D image is whole DMA instructions");
   static_assert((W3_STAGES - 2) * NPW <= 63, "vmcnt range");
-  static_assert(NJT == 2, "tile map assumes two j-tiles");
+  static_assert(NJT == 1 && JT % 16 == 0, "one full-width tile of whole 16-column blocks");
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
@@ -106,10 +108,7 @@ __device__ __forceinline__ void wgrad3_wave(const bf16_t* __restrict__ X0, const
   using G = W3<K, HD>;
   constexpr int w = W;
   constexpr int ig = w & 3, jh = w >> 2;  // i-group, j-half of this wave
-  // blocks b and b+8 share an XCD: they take the two j-tiles of one split
-  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-  const int z = (slot >> 1) * 8 + xcd, tj = slot & 1;
-  const int j0 = tj * G::JT;
+  const int z = blockIdx.x, j0 = 0;  // split z: rows z * rps ..
   const int mb = z * rps, me = min(M, mb + rps);
   const int nchs = me > mb ? (me - mb + 31) / 32 : 0;  // chunks per segment
   const int nch = nchs * nseg;
@@ -302,9 +301,8 @@ static void run_wgrad3(const void* X0, const void* H0, const void* D0, const voi
 }
 
 static int wgrad3_splits() {
-  // one workgroup per CU, two j-tiles per split; the XCD map needs a multiple of 8 splits
-  const int cus = device_cu_count();
-  return std::max(8, (cus / 2) / 8 * 8);
+  // one workgroup (one split of M) per CU
+  return std::max(8, device_cu_count());
 }
 
 bool lstm_wgrad3_supported(int M, int K, int Hd, int N) {
