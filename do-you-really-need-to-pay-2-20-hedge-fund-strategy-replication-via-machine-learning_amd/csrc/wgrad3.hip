@@ -129,7 +129,7 @@ __device__ __forceinline__ void wgrad3_wave(const bf16_t* __restrict__ X0, const
       const int nd = n - G::XI - G::HI, piece = nd * 64 + lane;
       const int r = piece / (G::JT / 8), cc = piece - r * (G::JT / 8);
       vreg[k] = 2; voff[k] = (uint32_t)(r * G::N * 2 + cc * 16); vdst[k] = G::OFF_D + nd * 1024;
-      von[k] = j0 + cc * 8 < G::N;
+      von[k] = true;  // (one full-width tile: every D piece is a real column)
     } else {
       vreg[k] = 3; voff[k] = 0; vdst[k] = G::TRASH; von[k] = lane == 0;
     }
