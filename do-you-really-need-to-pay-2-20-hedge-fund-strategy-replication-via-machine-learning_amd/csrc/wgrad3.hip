@@ -300,9 +300,14 @@ static void run_wgrad3(const void* X0, const void* H0, const void* D0, const voi
   launch_lstm_wgrad2_reduce(ws, gW, gU, gb, nsplit, K, HD, G::N, s);
 }
 
-static int wgrad3_splits() {
-  // one workgroup (one split of M) per CU
-  return std::max(8, device_cu_count());
+// one workgroup (one split of M) per CU at most; small M (the reference preset: B = 32, T = 48) takes
+// fewer splits of >= 1024 rows, since every split writes (and the reduce reads) a whole 201 x 400
+// fp32 slab (0.32 MB) however few rows it had
+static int wgrad3_splits(int64_t M = -1) {
+  const int cus = std::max(8, device_cu_count());
+  if (M < 0) return cus;  // (workspace sizing: the maximum)
+  const int64_t want = (M + 1023) / 1024;
+  return (int)std::max<int64_t>(8, std::min<int64_t>(cus, want));
 }
 
 bool lstm_wgrad3_supported(int M, int K, int Hd, int N) {
@@ -319,7 +324,7 @@ bool launch_lstm_wgrad3(const void* X0, const void* H0, const void* D0, const vo
   if (!lstm_wgrad3_supported(M, K, Hd, N)) return false;
   auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (!(al(X0) && al(H0) && al(D0) && al(X1) && al(H1) && al(D1))) return false;
-  const int ns = wgrad3_splits();
+  const int ns = wgrad3_splits(M);
   if (K == 32) run_wgrad3<32, 100>(X0, H0, D0, X1, H1, D1, gW, gU, gb, M, Tn, ns, ws, s);
   else run_wgrad3<100, 100>(X0, H0, D0, X1, H1, D1, gW, gU, gb, M, Tn, ns, ws, s);
   return true;
