@@ -2,7 +2,7 @@
 
     python scripts/dp_overlap_summary.py OUT/.../kernel_trace.csv [--last-steps 1]
 
-For every RCCL kernel (name contains "nccl" / "rccl") of the traced window: its queue, start / end
+For every collective kernel (name contains "nccl" / "rccl", or the one-shot p2p_allreduce) of the traced window: its queue, start / end
 relative to the first traced kernel, and the compute kernels on OTHER queues that ran during it (the
 reduction overlapping the reverse pass).  The window is the last ``--last-steps`` training iterations,
 found by the optimizer launches (rmsprop_kernel: 6 per iteration).
@@ -42,7 +42,7 @@ def main():
         ks = [k for k in ks if k[0] >= start]
     base = ks[0][0]
     short = lambda n: re.sub(r"\(.*", "", n).replace("void ", "")[:70]
-    coll = [k for k in ks if re.search(r"nccl|rccl", k[3], re.I)]
+    coll = [k for k in ks if re.search(r"nccl|rccl|p2p_allreduce", k[3], re.I)]
     comp = [k for k in ks if k not in coll]
     print(f"# {len(ks)} kernels in the last {a.last_steps} iteration(s), {len(coll)} RCCL kernels; "
           f"queues: RCCL {sorted({k[2] for k in coll})}, compute {sorted({k[2] for k in comp})}")
