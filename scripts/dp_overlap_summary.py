@@ -41,7 +41,7 @@ def main():
         start = opt[-per_it * a.last_steps - 1][1]
         ks = [k for k in ks if k[0] >= start]
     base = ks[0][0]
-    short = lambda n: re.sub(r"\(.*", "", n).replace("void ", "")[:70]
+    short = lambda n: re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", "")).replace("void ", "")[:70]
     coll = [k for k in ks if re.search(r"nccl|rccl|p2p_allreduce", k[3], re.I)]
     comp = [k for k in ks if k not in coll]
     print(f"# {len(ks)} kernels in the last {a.last_steps} iteration(s), {len(coll)} RCCL kernels; "
