@@ -123,6 +123,7 @@ def _measure(args, dtype, rank, world, pg, dev):
         "elapsed_s": elapsed,
         "elapsed_local_s": local,
     }
+    tr.close()
     del tr, ds
     if cuda:
         torch.cuda.empty_cache()

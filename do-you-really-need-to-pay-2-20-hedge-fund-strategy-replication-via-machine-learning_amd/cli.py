@@ -122,12 +122,19 @@ def _run_segment(tr, s, a):
     stop = min(a.stop_at, s["epochs"]) if a.stop_at else s["epochs"]
     if stop < s["epochs"] and not a.ckpt_dir:
         raise SystemExit("--stop-at before the last iteration needs --ckpt-dir")
+    graph = a.graph
+    if graph and tr.world > 1 and os.environ.get("HFREP_GRAPH_DP", "0") != "1":
+        # captured collectives under DP are opt-in (train/runner.py GraphedStep): step eagerly
+        if tr.rank == 0:
+            print("[hfrep] --graph under data parallelism needs HFREP_GRAPH_DP=1; running eager", file=sys.stderr)
+        graph = False
     opts = RunOptions(epochs=stop, log_every=s["log_every"], log_path=a.log, echo=not a.quiet,
                       ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume, nan_guard=not a.no_nan_guard,
-                      graph=a.graph)
+                      graph=graph)
     recs = run(tr, opts)
     if tr.iteration < s["epochs"]:
         checkpoint_now(tr, opts)
+    tr.close()
     return recs, tr.iteration >= s["epochs"]
 
 

@@ -784,7 +784,8 @@ int64_t p2p_open(std::vector<int64_t> handle, int64_t device) {
 
 void p2p_close(int64_t ptr) { hfrep::p2p_ipc_close(reinterpret_cast<void*>((intptr_t)ptr)); }
 
-void p2p_allreduce_(Tensor x, Tensor buf, std::vector<int64_t> peers, int64_t rank, int64_t cap, double scale) {
+void p2p_allreduce_(Tensor x, Tensor buf, std::vector<int64_t> peers, int64_t rank, int64_t cap, double scale,
+                    double timeout_s) {
   CHECK_F32(x);
   TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kByte && buf.device() == x.device(),
               "p2p_allreduce_: buf must be this device's p2p_buffer");
@@ -794,14 +795,25 @@ void p2p_allreduce_(Tensor x, Tensor buf, std::vector<int64_t> peers, int64_t ra
   TORCH_CHECK(peers[rank] == (int64_t)reinterpret_cast<intptr_t>(buf.data_ptr()), "p2p_allreduce_: peers[rank] must be buf");
   hfrep::P2PPeers pp{};
   for (int r = 0; r < world; ++r) pp.base[r] = reinterpret_cast<char*>((intptr_t)peers[r]);
+  TORCH_CHECK(timeout_s > 0, "p2p_allreduce_: timeout_s must be positive");
   GUARD(x);
-  hfrep::launch_p2p_allreduce(x.data_ptr<float>(), x.numel(), pp, (int)rank, world, cap, (float)scale, cur_stream(x));
+  // the tick rate is per device and fixed: query it once per (device, timeout)
+  static thread_local int s_dev = -1;
+  static thread_local double s_sec = -1;
+  static thread_local uint64_t s_ticks = 0;
+  if (s_dev != x.get_device() || s_sec != timeout_s) {
+    s_ticks = hfrep::p2p_timeout_ticks(timeout_s, x.get_device());
+    s_dev = x.get_device();
+    s_sec = timeout_s;
+  }
+  hfrep::launch_p2p_allreduce(x.data_ptr<float>(), x.numel(), pp, (int)rank, world, cap, (float)scale, s_ticks,
+                              cur_stream(x));
 }
 
 int64_t p2p_error(Tensor buf) {
   TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kByte, "p2p_error: a p2p_buffer tensor");
   GUARD(buf);
-  return hfrep::p2p_take_error(buf.data_ptr());
+  return hfrep::p2p_read_error(buf.data_ptr());
 }
 
 }  // namespace
@@ -862,7 +874,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("p2p_handle(Tensor buf) -> int[]");
   m.def("p2p_open(int[] handle, int device) -> int", &p2p_open);
   m.def("p2p_close(int ptr) -> ()", &p2p_close);
-  m.def("p2p_allreduce_(Tensor(a!) x, Tensor buf, int[] peers, int rank, int cap, float scale) -> ()");
+  m.def("p2p_allreduce_(Tensor(a!) x, Tensor buf, int[] peers, int rank, int cap, float scale, float timeout_s) -> ()");
   m.def("p2p_error(Tensor buf) -> int");
 }
 

@@ -185,10 +185,11 @@ void p2p_free(void* p);
 void p2p_ipc_handle(void* p, uint8_t out[64]);
 void* p2p_ipc_open(const uint8_t h[64], int device);
 void p2p_ipc_close(void* p);
-int p2p_take_error(void* own);  // reads and clears the error word (synchronous)
+int p2p_read_error(void* own);  // the sticky error word: 0, or 1 + the rank that gave up first (synchronous)
+uint64_t p2p_timeout_ticks(double seconds, int device);  // seconds -> wall-clock (s_memrealtime) ticks
 int p2p_blocks(int64_t n);
 // x[0 .. n) = scale * sum over ranks (rank order) of every rank's x; n <= cap, same n on every rank
 void launch_p2p_allreduce(float* x, int64_t n, const P2PPeers& peers, int rank, int world, int64_t cap, float scale,
-                          hipStream_t s);
+                          uint64_t timeout_ticks, hipStream_t s);
 
 }  // namespace hfrep

@@ -19,8 +19,15 @@
 // epoch e + 2, and its block b reaches that stage after its epoch e + 1 kernel saw all our epoch
 // e + 1 flags, i.e. after our epoch e kernel -- and its reads of that slot -- completed.  The epoch
 // lives in device memory (the last block of a call advances it), so the launch is hipGraph-safe.
-// A wait that exceeds kP2PSpinMax polls sets the error word and skips the sum: the host raises
-// (`p2p_error`), a missing peer never hangs the GPU.
+// Failure is loud and sticky.  A wait is bounded by TIME (the constant-rate wall clock, `timeout_ticks`
+// from HFREP_P2P_TIMEOUT_S): a block that gives up writes the error word of EVERY rank's buffer (the
+// "poison"), and every waiting block of every rank polls its own error word, so the whole world
+// leaves its waits within microseconds of the first give-up.  A block that did not complete the
+// exchange writes NaN over its chunk of x (the runner's NaN guard then stops every rank at the next
+// log record), the epoch counter is not advanced, and every later call on a poisoned buffer writes
+// NaN at once without touching flags or peers.  The host reads the word asynchronously
+// (P2PAllReduce.poll / GradSync.check_errors) and raises; there is no recovery -- the slot-parity
+// argument above needs every rank in step, so a poisoned communicator is rebuilt, not reused.
 #include "common.h"
 #include "kernels.h"
 
@@ -32,16 +39,31 @@ namespace hfrep {
 
 namespace {
 
-constexpr int kP2PSpinMax = 1 << 22;  // polls of ~0.1-0.2 us: a missing peer gives up after ~1 s
+__device__ inline void nan_fill(float* __restrict__ x, int64_t n, int64_t i0, int64_t i1, bool vec) {
+  const float q = __builtin_nanf("");
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    if (vec) {
+      reinterpret_cast<float4*>(x)[i] = make_float4(q, q, q, q);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (4 * i + k < n) x[4 * i + k] = q;
+    }
+  }
+}
 
 __global__ void __launch_bounds__(256) p2p_allreduce_kernel(float* __restrict__ x, int64_t n, P2PPeers peers,
-                                                            int rank, int world, int64_t cap, float scale) {
+                                                            int rank, int world, int64_t cap, float scale,
+                                                            uint64_t timeout_ticks) {
   char* own = peers.base[rank];
   int* ctr = reinterpret_cast<int*>(own + kP2PCtr);
   int* done = reinterpret_cast<int*>(own + kP2PDone);
   int* err = reinterpret_cast<int*>(own + kP2PErr);
-  __shared__ int s_epoch;
-  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __shared__ int s_epoch, s_dead;
+  if (threadIdx.x == 0) {
+    s_epoch = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    s_dead = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   __syncthreads();
   const int e = s_epoch;
   const int64_t slot = (int64_t)(e & 1) * cap;
@@ -49,6 +71,10 @@ __global__ void __launch_bounds__(256) p2p_allreduce_kernel(float* __restrict__ 
   const int64_t n4 = (n + 3) >> 2, per = (n4 + gridDim.x - 1) / gridDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * per, i1 = i0 + per < n4 ? i0 + per : n4;
   const bool vec = (n & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  if (s_dead) {  // poisoned by an earlier give-up (ours or a peer's): NaN, no flags, no waits
+    nan_fill(x, n, i0, i1, vec);
+    return;
+  }
 
   // 1. stage
   float* mine = reinterpret_cast<float*>(own + kP2PData) + slot;
@@ -68,15 +94,22 @@ __global__ void __launch_bounds__(256) p2p_allreduce_kernel(float* __restrict__ 
     int* fl = reinterpret_cast<int*>(peers.base[threadIdx.x] + kP2PFlags) + rank * kP2PMaxBlocks + blockIdx.x;
     __hip_atomic_store(fl, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  // 3. wait for every rank's chunk b (bounded)
+  // 3. wait for every rank's chunk b, bounded by time; leave early when any rank has given up
   int ok = 1;
   if ((int)threadIdx.x < world) {
     const int* fl = reinterpret_cast<const int*>(own + kP2PFlags) + threadIdx.x * kP2PMaxBlocks + blockIdx.x;
-    int polls = 0;
+    const uint64_t t0 = (uint64_t)wall_clock64();
     while (__hip_atomic_load(fl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-      if (++polls > kP2PSpinMax) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
         ok = 0;
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      if ((uint64_t)wall_clock64() - t0 > timeout_ticks) {
+        ok = 0;
+        // poison every rank (own included): their waiting blocks see it at their next poll
+        for (int r = 0; r < world; ++r)
+          __hip_atomic_store(reinterpret_cast<int*>(peers.base[r] + kP2PErr), 1 + rank, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -84,7 +117,7 @@ __global__ void __launch_bounds__(256) p2p_allreduce_kernel(float* __restrict__ 
   }
   ok = __syncthreads_and(ok);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: peers' chunks after their flags
-  // 4. reduce in rank order
+  // 4. reduce in rank order (or NaN: this chunk's exchange did not complete)
   if (ok) {
     for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
       if (vec) {
@@ -106,15 +139,18 @@ __global__ void __launch_bounds__(256) p2p_allreduce_kernel(float* __restrict__ 
         }
       }
     }
+  } else {
+    nan_fill(x, n, i0, i1, vec);
   }
   // epoch bookkeeping: the last block of the call advances the counter (the next call, later in
-  // stream order, reads it)
+  // stream order, reads it) -- unless the call failed: a poisoned buffer keeps its epoch
   __syncthreads();
   if (threadIdx.x == 0) {
     const int prev = __hip_atomic_fetch_add(done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == (int)gridDim.x - 1) {
       __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctr, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0)
+        __hip_atomic_store(ctr, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -133,11 +169,10 @@ void* p2p_alloc(int64_t cap, int device, bool* fine_grained) {
   ck(hipSetDevice(device), "hipSetDevice");
   void* p = nullptr;
   const size_t bytes = p2p_buffer_bytes(cap);
-  *fine_grained = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) == hipSuccess;
-  if (!*fine_grained) {
-    (void)hipGetLastError();
-    ck(hipMalloc(&p, bytes), "hipMalloc");
-  }
+  // fine-grained or nothing: the system-scope flag / data protocol above relies on it (coarse-grained
+  // memory may serve a peer stale lines)
+  ck(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained), "hipExtMallocWithFlags(fine-grained)");
+  *fine_grained = true;
   ck(hipMemset(p, 0, bytes), "hipMemset");
   ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
   ck(hipSetDevice(prev), "hipSetDevice");
@@ -167,14 +202,18 @@ void* p2p_ipc_open(const uint8_t h[64], int device) {
 
 void p2p_ipc_close(void* p) { (void)hipIpcCloseMemHandle(p); }
 
-int p2p_take_error(void* own) {
+int p2p_read_error(void* own) {
   int e = 0;
   ck(hipMemcpy(&e, static_cast<char*>(own) + kP2PErr, sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy");
-  if (e) {
-    const int zero = 0;
-    ck(hipMemcpy(static_cast<char*>(own) + kP2PErr, &zero, sizeof(int), hipMemcpyHostToDevice), "hipMemcpy");
-  }
   return e;
+}
+
+uint64_t p2p_timeout_ticks(double seconds, int device) {
+  int khz = 0;
+  ck(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device), "hipDeviceGetAttribute(WallClockRate)");
+  if (khz <= 0) khz = 100000;  // gfx9's constant 100 MHz counter
+  const double t = seconds * (double)khz * 1e3;
+  return t <= 0 ? 1 : t >= 1.8e19 ? ~0ull : (uint64_t)t;
 }
 
 int p2p_blocks(int64_t n) {
@@ -183,9 +222,10 @@ int p2p_blocks(int64_t n) {
 }
 
 void launch_p2p_allreduce(float* x, int64_t n, const P2PPeers& peers, int rank, int world, int64_t cap, float scale,
-                          hipStream_t s) {
+                          uint64_t timeout_ticks, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(p2p_allreduce_kernel, dim3(p2p_blocks(n)), dim3(256), 0, s, x, n, peers, rank, world, cap, scale);
+  hipLaunchKernelGGL(p2p_allreduce_kernel, dim3(p2p_blocks(n)), dim3(256), 0, s, x, n, peers, rank, world, cap, scale,
+                     timeout_ticks);
 }
 
 }  // namespace hfrep

@@ -478,21 +478,24 @@ void launch_widef(const float* x, const float* B, int sk, int sn, const float* b
   const int nq = (K + 15) / 16, nch = (M + 15) / 16, ncb = (N + 16 * WF_NT - 1) / (16 * WF_NT);
   const size_t smem = (size_t)16 * nq * WF_LDB * 4;
   const int grid = std::max(1, std::min((nch + 3) / 4, std::max(1, device_cu_count() / ncb)));
-  auto go = [&](auto kern) {
-    static bool attr = false;  // (per instantiation: the lambda's template parameter makes one per NQ)
-    if (!attr) {
+  // every NQ instantiation needs its own MaxDynamicSharedMemorySize attribute (NQ >= 9 is > 64 KiB of
+  // LDS): a flag per NQ, set at that instantiation's first launch
+  static bool attr[21] = {};
+  auto go = [&](auto kern, int q) {
+    if (!attr[q]) {
       HFREP_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                           160 * 1024));
-      attr = true;
+      attr[q] = true;
     }
     hipLaunchKernelGGL(kern, dim3(grid, ncb), dim3(256), smem, s, x, B, sk, sn, b, y, M, K, N, act);
+    HFREP_CHECK_HIP(hipGetLastError());
   };
   switch (nq) {
-#define HFREP_WIDEF(Q) case Q: go(widef_kernel<Q>); break;
+#define HFREP_WIDEF(Q) case Q: go(widef_kernel<Q>, Q); break;
     HFREP_WIDEF(1) HFREP_WIDEF(2) HFREP_WIDEF(3) HFREP_WIDEF(4) HFREP_WIDEF(5) HFREP_WIDEF(6) HFREP_WIDEF(7)
     HFREP_WIDEF(8) HFREP_WIDEF(9) HFREP_WIDEF(10) HFREP_WIDEF(11) HFREP_WIDEF(12) HFREP_WIDEF(13) HFREP_WIDEF(14)
     HFREP_WIDEF(15) HFREP_WIDEF(16) HFREP_WIDEF(17) HFREP_WIDEF(18) HFREP_WIDEF(19)
-    default: go(widef_kernel<20>); break;
+    default: go(widef_kernel<20>, 20); break;
 #undef HFREP_WIDEF
   }
 }

@@ -153,6 +153,23 @@ class GradSync:
         self._pending = []
         return n
 
+    def check_errors(self, blocking: bool = False) -> None:
+        """Surface a failed one-shot all-reduce (P2PTimeout).  Non-blocking by default (pinned-host
+        snapshot of the error word, see P2PAllReduce.poll); the runner calls it at every log record."""
+        if self.p2p is None:
+            return
+        if blocking:
+            self.p2p.check()
+        else:
+            self.p2p.poll()
+
+    def close(self) -> None:
+        """Collective teardown of the P2P communicator (every rank, same point); RCCL groups are left
+        to ``destroy_process_group``."""
+        if self.p2p is not None:
+            self.p2p.close()
+            self.p2p = None
+
     def drain_(self, timeout_s: float = 120.0) -> bool:
         """Block the host until the newest async collective (hence every earlier one of the group) has
         COMPLETED on the device (``Work.is_completed``: its end event has been reached), so no eager

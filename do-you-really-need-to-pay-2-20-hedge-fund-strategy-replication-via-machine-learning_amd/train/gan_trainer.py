@@ -271,6 +271,12 @@ class GANTrainer:
             self._g_acc = self._generator_step(noise, gen=gen).reshape(1)
         self.iteration += 1
 
+    def close(self) -> None:
+        """Collective teardown of the data-parallel communicators this trainer owns (every rank, same
+        point; a no-op for a single process)."""
+        if self.grad_sync is not None:
+            self.grad_sync.close()
+
     def losses(self) -> dict:
         d = self._d_acc.detach().float().cpu().numpy()
         return {"iteration": self.iteration, "d_loss": float(d[0]), "d_real": float(d[1]), "d_fake": float(d[2]),

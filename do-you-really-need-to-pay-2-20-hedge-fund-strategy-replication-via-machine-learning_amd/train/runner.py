@@ -84,11 +84,16 @@ class GraphedStep:
             raise RuntimeError("graph capture needs the native (device-counter) RNG")
         if trainer.grad_sync is not None and trainer.world > 1:
             # RCCL collectives are graph-capturable (ProcessGroupNCCL records them on the captured
-            # stream; tests/test_gpu_rccl.py replays them bitwise against the eager step); gloo / CPU
-            # collectives are not.  HFREP_GRAPH_DP=0 keeps DP steps eager.
-            if trainer.grad_sync.backend != "nccl" or os.environ.get("HFREP_GRAPH_DP", "1") == "0":
-                raise RuntimeError("graph capture under data parallelism needs RCCL (HFREP_GRAPH_DP=0 "
-                                   "keeps the collectives eager)")
+            # stream; tests/test_gpu_rccl.py replays them bitwise against the eager step on a 1-rank
+            # communicator); gloo / CPU collectives are not.  Captured collectives across >= 2 real
+            # GPUs have not been checked against the eager step yet (RCCL refuses two ranks on one
+            # GPU, and the pool's boxes have one), so under DP the capture is opt-in:
+            # HFREP_GRAPH_DP=1.  Without it a DP run replays nothing and steps eagerly.
+            if trainer.grad_sync.backend != "nccl":
+                raise RuntimeError("graph capture under data parallelism needs RCCL")
+            if os.environ.get("HFREP_GRAPH_DP", "0") != "1":
+                raise RuntimeError("graph capture under data parallelism is opt-in (HFREP_GRAPH_DP=1): multi-rank "
+                                   "replay parity is unpinned")
         self.t, self.warmup, self.calls = trainer, warmup, 0
         self.graph = None
 
@@ -212,6 +217,8 @@ def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[di
     logger = logger or JSONLLogger(opts.log_path, rank=trainer.rank, echo=opts.echo)
     records: list[dict] = []
 
+    gs = trainer.grad_sync
+
     def emit(rec):
         if rec is None:
             return
@@ -219,6 +226,9 @@ def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[di
             ok = rec.pop("ok")
             if opts.nan_guard and not ok:
                 logger.log({"event": "nonfinite_loss", "iteration": rec["iteration"]})
+                if gs is not None:
+                    # a failed P2P all-reduce writes NaN gradients: name the cause when it is that
+                    gs.check_errors(blocking=True)
                 raise NonFiniteLoss(f"non-finite loss by iteration {rec['iteration']}")
         d = rec.pop("d", None)
         g = rec.pop("g", None)
@@ -246,6 +256,8 @@ def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[di
                 now = time.time()
                 meta = {"iteration": it, "windows_per_s": wpi * (it - it_last) / max(now - t_last, 1e-9)}
                 t_last, it_last = now, it
+                if gs is not None:
+                    gs.check_errors()  # non-blocking: raises P2PTimeout once a give-up has reached the host
                 emit(snap.snapshot(meta, **_log_tensors(trainer, opts.nan_guard)))
             if opts.ckpt_dir and opts.ckpt_every and it % opts.ckpt_every == 0:
                 states = _gather_host_rng(trainer)
@@ -256,6 +268,8 @@ def run(trainer, opts: RunOptions, logger: JSONLLogger | None = None) -> list[di
 
                     dist.barrier(group=trainer.grad_sync.group)  # the file exists before any rank goes on
         emit(snap.collect())
+        if gs is not None:
+            gs.check_errors(blocking=True)
     finally:
         if own_logger:
             logger.close()

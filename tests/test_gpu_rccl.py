@@ -5,7 +5,7 @@ job has 2 ranks, which sends every gradient bucket through ``all_reduce(AVG)`` o
 backend (the async, reverse-pass-overlapped ``start_`` / ``finish_`` path of parallel/dp.py);
 AVG over the one real member is exact, so the trainer must stay bitwise equal to a trainer with
 no sync at all.  The second test captures the same step, collectives included, into a hipGraph
-(the default for RCCL data parallelism, train/runner.py GraphedStep).  Both run in a spawned process so the
+(train/runner.py GraphedStep; opt-in under DP with HFREP_GRAPH_DP=1 until a >= 2-GPU run pins it).  Both run in a spawned process so the
 process group never leaks into other tests.
 """
 import socket
@@ -33,6 +33,7 @@ def _worker(port, graph, key, q):
         from hfrep.parallel.dp import nccl_graph_safe_env
 
         nccl_graph_safe_env()  # (before the process group: RCCL events are not recycled into captures)
+        os.environ["HFREP_GRAPH_DP"] = "1"  # captured DP collectives are opt-in
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)

@@ -5,7 +5,9 @@ not: 2 (and 8, the node's rank count) spawned processes all bind cuda:0, exchang
 handles over a gloo group, and run the same kernel that would read the peers' buffers over xGMI on a
 node.  Checks: every size (1 element to the capacity, vector and scalar tails) equals the fp32
 rank-order sum bit for bit on every rank, the average variant, a hipGraph-captured call replayed with new inputs (device-side
-epochs), GradSync's bucketed start_ / finish_ through the side stream, and a clean error word.
+epochs), GradSync's bucketed start_ / finish_ through the side stream, and a clean error word; and
+the failure path: a peer that skips a call makes the other rank give up after the wall-clock timeout
+with NaN (never a finite stale result), and both ranks raise P2PTimeout.
 """
 import socket
 import traceback
@@ -219,3 +221,95 @@ def test_dp_training_over_p2p_allreduce(cuda):
         assert r["rel"] < 1e-5, r["rel"]
     # identical bits on every rank after three DP iterations
     np.testing.assert_array_equal(res[0]["params"], res[1]["params"])
+
+
+def _timeout_worker(rank, port, q):
+    """Rank 1 skips one call: rank 0's call must give up after its timeout, return NaN (not a finite
+    stale gradient) and raise; rank 1's next call must see the poison at once and raise too."""
+    try:
+        import os
+        import time
+
+        import torch
+        import torch.distributed as dist
+
+        import hfrep  # noqa: F401
+        from hfrep.parallel.p2p import P2PAllReduce, P2PTimeout
+
+        os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        ar = P2PAllReduce(dist.group.WORLD, cap=1 << 16, device=dev, timeout_s=2.0)
+        res = {"rank": rank}
+        x = torch.full((5000,), float(rank + 1), device=dev)
+        dist.barrier()
+        ar.all_reduce_(x)  # a good call first
+        torch.cuda.synchronize()
+        res["first_ok"] = bool((x == 3.0).all())
+        ar.check()
+        dist.barrier()
+        if rank == 0:
+            y = torch.ones(5000, device=dev)
+            ar.poll()  # snapshot before the failing call: clean
+            t0 = time.perf_counter()
+            ar.all_reduce_(y)  # rank 1 never joins this one
+            torch.cuda.synchronize()
+            res["wait_s"] = time.perf_counter() - t0
+            res["nan"] = bool(torch.isnan(y).all())
+            try:
+                ar.poll()  # lands the clean snapshot, takes a new one
+                torch.cuda.synchronize()
+                ar.poll()  # the new snapshot holds the error word
+                res["poll_raised"] = False
+            except P2PTimeout:
+                res["poll_raised"] = True
+            res["epochs"] = int(ar.buf[:4].view(torch.int32).item())
+        dist.barrier()  # rank 1 stays alive (its buffer mapped) until rank 0 has given up
+        if rank == 1:
+            z = torch.ones(5000, device=dev)
+            t0 = time.perf_counter()
+            ar.all_reduce_(z)  # poisoned by rank 0: NaN without waiting
+            torch.cuda.synchronize()
+            res["wait_s"] = time.perf_counter() - t0
+            res["nan"] = bool(torch.isnan(z).all())
+        try:
+            ar.check()
+            res["check_raised"] = False
+        except P2PTimeout as e:
+            res["check_raised"] = True
+            res["msg"] = str(e)
+        ar.close()
+        dist.destroy_process_group()
+        q.put(res)
+    except Exception:
+        q.put(traceback.format_exc())
+
+
+def test_p2p_allreduce_missing_peer_fails_loud(cuda):
+    import torch.multiprocessing as mp
+
+    from _spawn import gather
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_timeout_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = gather(procs, q, 2, timeout=180)
+    for p in procs:
+        p.join(timeout=30)
+    for r in res:
+        assert not isinstance(r, str), r
+        assert r["first_ok"] and r["nan"] and r["check_raised"], r
+        assert "rank 0 gave up" in r["msg"], r
+    r0 = [r for r in res if r["rank"] == 0][0]
+    r1 = [r for r in res if r["rank"] == 1][0]
+    assert 1.5 < r0["wait_s"] < 30, r0  # the time bound, not a poll count
+    assert r0["poll_raised"], r0
+    assert r0["epochs"] == 1, r0  # the failed call did not advance the epoch
+    assert r1["wait_s"] < 1.0, r1  # poisoned: no wait
