@@ -89,6 +89,10 @@ def _measure(args, dtype, rank, world, pg, dev):
 
     for _ in range(args.warmup):
         tr.train_step()
+    gs = tr.grad_sync
+    if gs is not None:
+        gs.exposed_wait_ms()  # (drop any warmup events)
+        gs.timing = True      # event pair around every bucket join of the timed steps
     _sync(dev)
     barrier()
     _sync(dev)
@@ -100,10 +104,18 @@ def _measure(args, dtype, rank, world, pg, dev):
     _sync(dev)
     local = time.perf_counter() - t0
     elapsed = local
+    exposed = [0.0] * world
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # each rank's exposed all-reduce wait per step: compute-stream time blocked in GradSync.finish_
+        w = torch.zeros(world, dtype=torch.float64, device=dev)
+        w[rank] = gs.exposed_wait_ms() / args.steps
+        gs.timing = False
+        dist.all_reduce(w, op=dist.ReduceOp.SUM)
+        exposed = [round(float(v), 3) for v in w.cpu()]
+        gs.check_errors(blocking=True)
     if args.trace_out and rank == 0:
         from hfrep.utils.trace import profile_steps
 
@@ -122,6 +134,9 @@ def _measure(args, dtype, rank, world, pg, dev):
         "peak_mem_gb_rank0": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2) if cuda else 0.0,
         "elapsed_s": elapsed,
         "elapsed_local_s": local,
+        "allreduce": "none" if gs is None else ("p2p" if gs.use_p2p else "rccl" if gs.backend == "nccl" else gs.backend),
+        "buckets": 0 if gs is None else gs.buckets,
+        "allreduce_exposed_ms_per_step": exposed,
     }
     tr.close()
     del tr, ds
@@ -202,11 +217,17 @@ def main():
             # the W-dist half of the metric is a training-quality run, not a throughput step
             "w_dist_parity": "profiles/r03_parity/README.md" if args.model == "mtss_wgan_gp" else None,
             "peak_mem_gb_rank0": res["peak_mem_gb_rank0"],
+            # data-parallel gradient averaging: collective, buckets per model, and each rank's exposed
+            # (non-overlapped) all-reduce wait per step
+            "allreduce": res["allreduce"],
+            "buckets": res["buckets"],
+            "allreduce_exposed_ms_per_step": res["allreduce_exposed_ms_per_step"],
         }
         if sub is not None:
             # same config, same step count, timed after the fp32 run: bf16 MFMA with fp32 accumulation,
             # bf16 activations / tapes, fp32 master weights and optimizer state
-            rec["bf16"] = {k: sub[k] for k in ("value", "ms_per_step", "losses_finite", "peak_mem_gb_rank0")}
+            rec["bf16"] = {k: sub[k] for k in ("value", "ms_per_step", "losses_finite", "peak_mem_gb_rank0",
+                                               "allreduce_exposed_ms_per_step")}
         print(json.dumps(rec))
     if world > 1:
         dist.destroy_process_group()

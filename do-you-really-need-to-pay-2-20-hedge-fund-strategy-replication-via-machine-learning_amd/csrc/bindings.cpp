@@ -167,9 +167,8 @@ void lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<
   if (f32) {
     // impl (fp32): 0 = default, 1 = exact-fp32 MFMA kernel, 2 = three-term bf16 split kernel
     Tensor ws = out_empty({(int64_t)hfrep::lstmf_wgrad_workspace_floats(M, K, (int)impl)}, x.options());
-    hfrep::launch_lstmf_wgrad(x.data_ptr<float>(), hs.data_ptr<float>(), dZ.data_ptr<float>(),
-                              tangent ? xd->data_ptr<float>() : nullptr, tangent ? hds->data_ptr<float>() : nullptr,
-                              tangent ? dZd->data_ptr<float>() : nullptr, gW.data_ptr<float>(), gU.data_ptr<float>(), gbp,
+    hfrep::launch_lstmf_wgrad(x.data_ptr(), hs.data_ptr(), dZ.data_ptr(),
+                              X1, H1, D1, gW.data_ptr<float>(), gU.data_ptr<float>(), gbp,
                               M, K, Tn, ws.data_ptr<float>(), cur_stream(x), (int)impl);
     return;
   }
@@ -366,6 +365,82 @@ Tensor lstmf_dgrad(Tensor dz, Tensor W, int64_t impl) {
   const bool ok = hfrep::launch_lstmf_dgrad(dz.data_ptr<float>(), W.data_ptr<float>(), x.data_ptr<float>(), dz.size(0),
                                             dz.size(1), W.size(0), cur_stream(dz), (int)impl);
   TORCH_CHECK(ok, "lstmf_dgrad: launch failed");
+  return x;
+}
+
+// ---- FP3 planes: an fp32 tensor (..., C) as its three exact bf16 split planes (..., 3, C) ----
+bool is_fp3(const Tensor& t) { return t.scalar_type() == at::kBFloat16 && t.dim() >= 2 && t.size(-2) == 3; }
+
+Tensor fp3_split(Tensor x, bool interleave) {
+  CHECK_F32(x);
+  TORCH_CHECK(x.is_contiguous() && x.dim() >= 1, "fp3_split: a contiguous fp32 tensor");
+  const int64_t C = x.size(-1), M = C ? x.numel() / C : 0;
+  auto sz = x.sizes().vec();
+  sz.insert(sz.end() - 1, 3);
+  GUARD(x);
+  Tensor p = out_empty(sz, x.options().dtype(at::kBFloat16));
+  hfrep::launch_fp3_split(x.data_ptr<float>(), reinterpret_cast<uint16_t*>(p.data_ptr()), M, (int)C, interleave,
+                          cur_stream(x));
+  return p;
+}
+
+Tensor fp3_join(Tensor p, bool interleave) {
+  CHECK_GPU(p);
+  TORCH_CHECK(is_fp3(p) && p.is_contiguous(), "fp3_join: contiguous bf16 planes (..., 3, C)");
+  const int64_t C = p.size(-1), M = C ? p.numel() / (3 * C) : 0;
+  auto sz = p.sizes().vec();
+  sz.erase(sz.end() - 2);
+  GUARD(p);
+  Tensor x = out_empty(sz, p.options().dtype(at::kFloat));
+  hfrep::launch_fp3_join(reinterpret_cast<const uint16_t*>(p.data_ptr()), x.data_ptr<float>(), M, (int)C, interleave,
+                         cur_stream(p));
+  return x;
+}
+
+// fp32 LSTM weight gradients with any of x (B,T,K) / hs (B,T,H) / dZ (B,T,400) given as FP3 planes
+// ((B,T,3,C) bf16; dZ in the interleaved gate order); the tangent segment's operands mirror the primal's
+void lstmf_wgrad_p_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<Tensor> gb, optional<Tensor> xd,
+                    optional<Tensor> hds, optional<Tensor> dZd, int64_t impl) {
+  CHECK_GPU(x); CHECK_GPU(hs); CHECK_GPU(dZ);
+  const int pm = (is_fp3(x) ? 1 : 0) | (is_fp3(hs) ? 2 : 0) | (is_fp3(dZ) ? 4 : 0);
+  for (const Tensor* t : {&x, &hs, &dZ})
+    TORCH_CHECK(t->is_contiguous() && (is_fp3(*t) ? t->dim() == 4 : (t->scalar_type() == at::kFloat && t->dim() == 3)),
+                "lstmf_wgrad_p_: fp32 (B,T,C) or FP3 planes (B,T,3,C), contiguous");
+  const int B = x.size(0), Tn = x.size(1), K = x.size(-1), Hd = hs.size(-1), N = dZ.size(-1);
+  TORCH_CHECK(hs.size(0) == B && dZ.size(0) == B && hs.size(1) == Tn && dZ.size(1) == Tn, "lstmf_wgrad_p_: B/T");
+  TORCH_CHECK(hfrep::lstmf_wgrad_supported(K, Hd, N) && (pm == 0 || K == 32 || K == 100), "lstmf_wgrad_p_: K / H / N");
+  CHECK_F32(gW); CHECK_F32(gU);
+  TORCH_CHECK(gW.numel() == (int64_t)K * N && gU.numel() == (int64_t)Hd * N, "lstmf_wgrad_p_: grad sizes");
+  if (gb.has_value()) { CHECK_F32(*gb); TORCH_CHECK(gb->numel() == N, "gb size"); }
+  const bool tangent = xd.has_value();
+  if (tangent) {
+    TORCH_CHECK(hds.has_value() && dZd.has_value(), "tangent segment needs xd, hds, dZd");
+    TORCH_CHECK(xd->sizes() == x.sizes() && hds->sizes() == hs.sizes() && dZd->sizes() == dZ.sizes() &&
+                xd->scalar_type() == x.scalar_type() && hds->scalar_type() == hs.scalar_type() &&
+                dZd->scalar_type() == dZ.scalar_type() && xd->is_contiguous() && hds->is_contiguous() &&
+                dZd->is_contiguous(), "lstmf_wgrad_p_: tangent operands must mirror the primal ones");
+  }
+  GUARD(x);
+  const int M = B * Tn;
+  Tensor ws = out_empty({(int64_t)hfrep::lstmf_wgrad_workspace_floats(M, K, (int)impl)}, gW.options());
+  hfrep::launch_lstmf_wgrad(x.data_ptr(), hs.data_ptr(), dZ.data_ptr(), tangent ? xd->data_ptr() : nullptr,
+                            tangent ? hds->data_ptr() : nullptr, tangent ? dZd->data_ptr() : nullptr, gW.data_ptr<float>(),
+                            gU.data_ptr<float>(), gb.has_value() ? gb->data_ptr<float>() : nullptr, M, K, Tn,
+                            ws.data_ptr<float>(), cur_stream(x), (int)impl, pm);
+}
+
+// dX (M, KO) = dZ W^T with dZ as FP3 planes (M, 3, 400) in the interleaved gate order
+Tensor lstmf_dgrad_p(Tensor dzp, Tensor W, int64_t impl) {
+  CHECK_GPU(dzp); CHECK_F32(W);
+  TORCH_CHECK(is_fp3(dzp) && dzp.dim() == 3 && dzp.is_contiguous() && W.dim() == 2 && W.is_contiguous() &&
+              W.size(1) == dzp.size(2), "lstmf_dgrad_p: planes (M, 3, N) and W (KO, N), contiguous");
+  TORCH_CHECK(hfrep::lstmf_dgrad_supported(dzp.size(2), W.size(0)), "lstmf_dgrad_p: N must be 400 and KO <= 112");
+  GUARD(dzp);
+  Tensor x = out_empty({dzp.size(0), W.size(0)}, W.options());
+  if (dzp.size(0) == 0) return x;
+  const bool ok = hfrep::launch_lstmf_dgrad(dzp.data_ptr(), W.data_ptr<float>(), x.data_ptr<float>(), dzp.size(0),
+                                            dzp.size(2), W.size(0), cur_stream(dzp), (int)impl, true);
+  TORCH_CHECK(ok, "lstmf_dgrad_p: launch failed");
   return x;
 }
 
@@ -822,6 +897,10 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("linear(Tensor x, Tensor W, Tensor? b, int act, Tensor(a!)? out=None) -> Tensor");  // writes into out when given
   m.def("linear_dgrad(Tensor dz, Tensor W) -> Tensor");
   m.def("linear_wgrad_(Tensor x, Tensor dz, Tensor(a!) gW, Tensor(b!)? gb, int shiftT=0) -> ()");
+  m.def("fp3_split(Tensor x, bool interleave=False) -> Tensor");
+  m.def("fp3_join(Tensor p, bool interleave=False) -> Tensor");
+  m.def("lstmf_wgrad_p_(Tensor x, Tensor hs, Tensor dZ, Tensor(a!) gW, Tensor(b!) gU, Tensor(c!)? gb, Tensor? xd=None, Tensor? hds=None, Tensor? dZd=None, int impl=0) -> ()");
+  m.def("lstmf_dgrad_p(Tensor dzp, Tensor W, int impl=0) -> Tensor");
   m.def("lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor(a!) gW, Tensor(b!) gU, Tensor(c!)? gb, Tensor? xd=None, Tensor? hds=None, Tensor? dZd=None, int impl=0) -> ()");
   m.def("act_fwd(Tensor x, int act) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor y, int act) -> Tensor");
@@ -895,6 +974,10 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("lstmf_bwd", &lstmf_bwd);
   m.impl("lstmf_tbwd", &lstmf_tbwd);
   m.impl("lstmf_dgrad", &lstmf_dgrad);
+  m.impl("fp3_split", &fp3_split);
+  m.impl("fp3_join", &fp3_join);
+  m.impl("lstmf_wgrad_p_", &lstmf_wgrad_p_);
+  m.impl("lstmf_dgrad_p", &lstmf_dgrad_p);
   m.impl("lstm_bwd", &lstm_bwd);
   m.impl("lstm_tfwd", &lstm_tfwd);
   m.impl("lstm_tbwd", &lstm_tbwd);

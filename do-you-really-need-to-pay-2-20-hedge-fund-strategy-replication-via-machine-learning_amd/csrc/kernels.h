@@ -60,8 +60,9 @@ bool lstmf_wgrad_supported(int K, int H, int N);
 // impl: 0 = default (exact under HFREP_FP32_EXACT=1, else the pair split for K <= 36 and the quad split for K = 100), 1 = exact-fp32
 // MFMA, 2 = the three-term bf16 split (pair), 3 = the three-term bf16 split (quad)
 size_t lstmf_wgrad_workspace_floats(int M, int K, int impl = 0);
-bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
-                        float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl = 0);
+bool launch_lstmf_wgrad(const void* X, const void* Hs, const void* D, const void* Xd, const void* Hds, const void* Dd,
+                        float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl = 0,
+                        int pm = 0);  // pm: FP3-plane operands (bit 1 X, 2 H, 4 D interleaved)
 // fp32 input gradient X (M, KO) = D (M, N) W^T, W (KO, N) row-major; N = 400, KO <= 112
 bool lstmf_dgrad_supported(int N, int KO);
 // forward kernel selection: 1 = exact-fp32 everywhere, 2 = split recurrent product for K <= 36 (default);
@@ -69,7 +70,12 @@ bool lstmf_dgrad_supported(int N, int KO);
 int set_lstmf_fwd_impl(int v);  // 1: exact-fp32 forward everywhere, 2: the split-recurrent one for K <= 36
 int set_lstmf_bwd_impl(int v);  // 2: the exact-fp32 BPTT kernel, 3: the split-recurrent one
 // impl: 0 = default (exact under HFREP_FP32_EXACT=1, else the LDS-staged split for KO > 64), 1 = exact, 3 = three-term bf16 split
-bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl = 0);
+bool launch_lstmf_dgrad(const void* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl = 0,
+                        bool pd = false);  // pd: dZ as FP3 planes (interleaved gate order)
+// FP3 planes (csrc/lstm_f32.hip): fp32 (M, C) <-> bf16 (M, 3, C) exact split planes; interleave: C = 400 in
+// the gate-interleaved column order k = 4 u + q
+void launch_fp3_split(const float* x, uint16_t* p, int64_t M, int C, bool interleave, hipStream_t s);
+void launch_fp3_join(const uint16_t* p, float* x, int64_t M, int C, bool interleave, hipStream_t s);
 
 // ---- ae.hip (factor autoencoder: the whole Keras fit -- MSE, Nadam, EarlyStopping -- in one launch) ----
 bool ae_fit_supported(int A, int k, int batch);

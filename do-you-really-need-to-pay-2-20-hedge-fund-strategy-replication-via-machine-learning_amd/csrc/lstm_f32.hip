@@ -36,6 +36,7 @@
 #include <mutex>
 #include <type_traits>
 #include <set>
+#include <stdexcept>
 
 namespace hfrep {
 
@@ -1111,6 +1112,54 @@ __device__ __forceinline__ void split3(const f32x4 v, uint32_t (&p)[3][2]) {
   }
 }
 
+// ---- producer-side split planes ("FP3"): an fp32 tensor (rows, C) stored as its three exact bf16
+// split planes, row-planar: row r = [h (C) | m (C) | l (C)] bf16 (6 bytes per value; h + m + l == a
+// exactly, so the encoding is lossless and a consumer that loads planes instead of splitting fp32 feeds
+// its MFMAs the very same operands: bitwise-identical results).  The gate-column tensors dZ / dZdot
+// (C = 400) are stored in the gate-INTERLEAVED column order k = 4 u + q (unit u, gate q) in which the
+// split BPTT holds its dz planes; consumers map k back to the natural column (k & 3) H + (k >> 2).
+__device__ __forceinline__ constexpr int gate_nat(int k) { return (k & 3) * FH + (k >> 2); }
+__device__ __forceinline__ u32x2_t ld8(rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+
+// fp32 (M, C) -> planes (M, 3, C); IL: column k of the planes is natural column gate_nat(k) (C = 400)
+template <bool IL>
+__global__ void __launch_bounds__(256) fp3_split_kernel(const float* __restrict__ x, uint16_t* __restrict__ p, int64_t M,
+                                                        int C) {
+  const int64_t n4 = M * (C / 4);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / (C / 4);
+    const int c = 4 * (int)(i - r * (C / 4));
+    f32x4 v;
+    if constexpr (IL) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = x[r * C + gate_nat(c + j)];
+    } else {
+      v = *reinterpret_cast<const f32x4*>(x + r * C + c);
+    }
+    uint32_t q[3][2];
+    split3(v, q);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      *reinterpret_cast<u32x2_t*>(p + (r * 3 + pl) * C + c) = u32x2_t{q[pl][0], q[pl][1]};
+  }
+}
+// planes -> fp32 (h + m + l: exact)
+template <bool IL>
+__global__ void __launch_bounds__(256) fp3_join_kernel(const uint16_t* __restrict__ p, float* __restrict__ x, int64_t M,
+                                                       int C) {
+  const int64_t n = M * C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / C;
+    const int k = (int)(i - r * C);
+    float a = 0.f;
+#pragma unroll
+    for (int pl = 2; pl >= 0; --pl) a += __builtin_bit_cast(float, (uint32_t)p[(r * 3 + pl) * C + k] << 16);
+    x[r * C + (IL ? gate_nat(k) : k)] = a;
+  }
+}
+
 // one 16x16x32 operand (8 bf16) of a plane image (row stride ROWB) at column block c0: two
 // transposed reads, chunk rows 4 G + q and 16 + 4 G + q of this lane's group G (k = 8 G + j of the
 // MFMA maps to chunk row 4 G + j (j < 4) / 16 + 4 G + j - 4: any row order works as long as both
@@ -1170,11 +1219,16 @@ __device__ __forceinline__ void ws_chunk(f32x4 (&acc)[NA][NB], const lds_char* A
   }
 }
 
-template <int KX, int XR = KX>  // XR: X row stride in floats (35: a 36-column image, column 35 zero)
+// XR: X row stride in floats (35: a 36-column image, column 35 zero).  PM: FP3-plane operands as in
+// lstmf_wgrad_q4_kernel (bit 1 X -- only with XR == KX --, 2 H, 4 D interleaved)
+template <int KX, int XR = KX, int PM = 0>
 __global__ void __launch_bounds__(512, 1)
-lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ Hs, const float* __restrict__ D,
-                         const float* __restrict__ Xd, const float* __restrict__ Hds, const float* __restrict__ Dd,
+lstmf_wgrad_split_kernel(const void* __restrict__ X, const void* __restrict__ Hs, const void* __restrict__ D,
+                         const void* __restrict__ Xd, const void* __restrict__ Hds, const void* __restrict__ Dd,
                          float* __restrict__ slab, int M, int Tn, int rows_per_z, int Z) {
+  constexpr bool PX = PM & 1, PH = PM & 2, PD = PM & 4;
+  static_assert(!PX || XR == KX, "wgrad split: X planes need XR == KX");
+  constexpr int XRB = PX ? 6 * KX : 4 * XR, HRB = PH ? 6 * FH : 4 * FH, DRB = PD ? 6 * FG : 4 * FG;  // row bytes
   using G = WSGeo<KX>;
   using GI = typename G::Img;
   constexpr int NI = G::NI, NI0 = G::NI0, JX = G::JX, JH = G::JH, JD = G::JD;
@@ -1223,14 +1277,14 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
   for (int j = 0; j < JX; ++j) {
     const int e = tid + 512 * j, r = e / (KX / 4), c4 = e - r * (KX / 4);
     const bool ok = e < 32 * KX / 4;
-    gx[j] = ok ? (r * XR + 4 * c4) * 4 : kOOB;
+    gx[j] = ok ? (PX ? r * XRB + 8 * c4 : (r * XR + 4 * c4) * 4) : kOOB;
     lx[j] = ok ? r * GI::ROWA + 8 * c4 : -1;
   }
 #pragma unroll
   for (int j = 0; j < JH; ++j) {
     const int e = tid + 512 * j, r = e / (FH / 4), c4 = e - r * (FH / 4);
     const bool ok = e < 32 * FH / 4;
-    gh[j] = ok ? (r * FH + 4 * c4) * 4 : kOOB;
+    gh[j] = ok ? (PH ? r * HRB + 8 * c4 : (r * FH + 4 * c4) * 4) : kOOB;
     lh[j] = ok ? r * GI::ROWA + 2 * KX + 8 * c4 : -1;
     rhr[j] = ok ? r : 0;
   }
@@ -1238,24 +1292,25 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
   for (int j = 0; j < JD; ++j) {
     const int e = tid + 512 * j, r = e / 52, c4 = e - r * 52;
     const bool ok = e < 32 * 52 && c4 < nd4;
-    gd[j] = ok ? (r * FG + jbase + 4 * c4) * 4 : kOOB;
+    gd[j] = ok ? (PD ? r * DRB + 2 * (jbase + 4 * c4) : (r * FG + jbase + 4 * c4) * 4) : kOOB;
     ld_[j] = ok ? GI::IMGD + r * GI::ROWD + 8 * c4 : -1;
     rd_[j] = ok ? r : 0;
   }
   const int step32 = 32 % Tn;
 
   f32x4 vx[JX], vh[JH], vd[JD];
+  u32x2_t px[JX][3], ph[JH][3], pd[JD][3];  // plane slots (dead when the operand is fp32)
   for (int seg = 0; seg < (Xd ? 2 : 1); ++seg) {
-    const float* Xs = seg ? Xd : X;
-    const float* Hq = seg ? Hds : Hs;
-    const float* Dq = seg ? Dd : D;
+    const char* Xs = static_cast<const char*>(seg ? Xd : X);
+    const char* Hq = static_cast<const char*>(seg ? Hds : Hs);
+    const char* Dq = static_cast<const char*>(seg ? Dd : D);
     // the H descriptor starts at row mb - 1 (row -1 for mb = 0, whose h_{-1} is never addressed: the
     // t = 0 rows are masked) so every voffset is >= 0 -- the range check is on voffset alone, and a
     // negative voffset with a compensating soffset reads zeros
     const int nr = me > mb ? me - mb : 0;
-    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * XR, nr * XR * 4);
-    const rsrc_t rh = make_rsrc(Hq + ((ptrdiff_t)mb - 1) * FH, (nr ? nr + 1 : 0) * FH * 4);
-    const rsrc_t rd = make_rsrc(Dq + (size_t)mb * FG, nr * FG * 4);
+    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * XRB, nr * XRB);
+    const rsrc_t rh = make_rsrc(Hq + ((ptrdiff_t)mb - 1) * HRB, (nr ? nr + 1 : 0) * HRB);
+    const rsrc_t rd = make_rsrc(Dq + (size_t)mb * DRB, nr * DRB);
     // t = (row) mod Tn of this thread's H slots at the current chunk (h_{-1} = 0 rows)
     int tm[JH];
 #pragma unroll
@@ -1263,12 +1318,35 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
     auto load = [&](int m0) {  // rows past me: voffset out of range, zeros
       const int lim = me - m0;
 #pragma unroll
-      for (int j = 0; j < JX; ++j)
-        vx[j] = ldx4<XR>(rx, (gx[j] >> 2) / XR < lim ? gx[j] : kOOB, (m0 - mb) * XR * 4, (gx[j] >> 2) % XR);
+      for (int j = 0; j < JX; ++j) {
+        if constexpr (PX) {
+          const int vo = gx[j] != kOOB && gx[j] / XRB < lim ? gx[j] : kOOB;
 #pragma unroll
-      for (int j = 0; j < JH; ++j) vh[j] = ld4s(rh, rhr[j] < lim && tm[j] != 0 ? gh[j] : kOOB, (m0 - mb) * FH * 4);
+          for (int q = 0; q < 3; ++q) px[j][q] = ld8(rx, vo + 2 * KX * q, (m0 - mb) * XRB);
+        } else {
+          vx[j] = ldx4<XR>(rx, (gx[j] >> 2) / XR < lim ? gx[j] : kOOB, (m0 - mb) * XRB, (gx[j] >> 2) % XR);
+        }
+      }
 #pragma unroll
-      for (int j = 0; j < JD; ++j) vd[j] = ld4s(rd, rd_[j] < lim ? gd[j] : kOOB, (m0 - mb) * FG * 4);
+      for (int j = 0; j < JH; ++j) {
+        const int vo = rhr[j] < lim && tm[j] != 0 ? gh[j] : kOOB;
+        if constexpr (PH) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) ph[j][q] = ld8(rh, vo + 2 * FH * q, (m0 - mb) * HRB);
+        } else {
+          vh[j] = ld4s(rh, vo, (m0 - mb) * HRB);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < JD; ++j) {
+        const int vo = rd_[j] < lim ? gd[j] : kOOB;
+        if constexpr (PD) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) pd[j][q] = ld8(rd, vo + 2 * FG * q, (m0 - mb) * DRB);
+        } else {
+          vd[j] = ld4s(rd, vo, (m0 - mb) * DRB);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < JH; ++j) {
         tm[j] += step32;
@@ -1285,14 +1363,30 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
           *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(base + lo + q * pl) = u32x2_t{p[q][0], p[q][1]};
       }
     };
+    auto putp = [&](lds_char* base, int lo, const u32x2_t (&p)[3]) {  // a plane slot: stored as loaded
+      if (lo >= 0) {
+        const int pl = lo < GI::IMGD ? GI::PLA : GI::PLD;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(base + lo + q * pl) = p[q];
+      }
+    };
     auto stage = [&](int buf) {
       lds_char* base = wsm + buf * GI::BUF;
 #pragma unroll
-      for (int j = 0; j < JX; ++j) put(base, lx[j], vx[j]);
+      for (int j = 0; j < JX; ++j) {
+        if constexpr (PX) putp(base, lx[j], px[j]);
+        else put(base, lx[j], vx[j]);
+      }
 #pragma unroll
-      for (int j = 0; j < JH; ++j) put(base, lh[j], vh[j]);
+      for (int j = 0; j < JH; ++j) {
+        if constexpr (PH) putp(base, lh[j], ph[j]);
+        else put(base, lh[j], vh[j]);
+      }
 #pragma unroll
-      for (int j = 0; j < JD; ++j) put(base, ld_[j], vd[j]);
+      for (int j = 0; j < JD; ++j) {
+        if constexpr (PD) putp(base, ld_[j], pd[j]);
+        else put(base, ld_[j], vd[j]);
+      }
     };
     // bias column (column KR - 1 of A): 1 in plane h for the primal segment, 0 for the tangent one
     if (tid < 64) {
@@ -1334,7 +1428,7 @@ lstmf_wgrad_split_kernel(const float* __restrict__ X, const float* __restrict__ 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = 16 * (i0 + ii) + 4 * g + r;
-          if (i < G::KR && col < FG) out[(size_t)i * FG + col] = acc[ii][jj][r];
+          if (i < G::KR && col < FG) out[(size_t)i * FG + (PD ? gate_nat(col) : col)] = acc[ii][jj][r];
         }
       }
 }
@@ -1377,11 +1471,15 @@ struct WQGeo {
   using Img = WImg<16 * NI, 16 * WQ_NJ>;
 };
 
-template <int KX>
+// PM: which operands arrive as FP3 planes instead of fp32 (bit 1 X, 2 H, 4 D -- D in the interleaved
+// gate order): a plane slot is three 8-byte loads stored to the LDS images as they are, no split
+template <int KX, int PM>
 __global__ void __launch_bounds__(512, 1)
-lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs, const float* __restrict__ D,
-                      const float* __restrict__ Xd, const float* __restrict__ Hds, const float* __restrict__ Dd,
+lstmf_wgrad_q4_kernel(const void* __restrict__ X, const void* __restrict__ Hs, const void* __restrict__ D,
+                      const void* __restrict__ Xd, const void* __restrict__ Hds, const void* __restrict__ Dd,
                       float* __restrict__ slab, int M, int Tn, int rows_per_z, int Z) {
+  constexpr bool PX = PM & 1, PH = PM & 2, PD = PM & 4;
+  constexpr int XRB = PX ? 6 * KX : 4 * KX, HRB = PH ? 6 * FH : 4 * FH, DRB = PD ? 6 * FG : 4 * FG;  // row bytes
   using G = WQGeo<KX>;
   using GI = typename G::Img;
   constexpr int JX = G::JX, JH = G::JH, NS = G::NS, MAXT = G::MAXT;
@@ -1436,15 +1534,17 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
   };
 
   f32x4 v[NS];
+  u32x2_t pv[NS][3];  // (plane slots; the fp32 / plane element of each slot is dead in the other case)
   for (int seg = 0; seg < (Xd ? 2 : 1); ++seg) {
-    const float* Xs = seg ? Xd : X;
-    const float* Hq = seg ? Hds : Hs;
-    const float* Dq = seg ? Dd : D;
+    const char* Xs = static_cast<const char*>(seg ? Xd : X);
+    const char* Hq = static_cast<const char*>(seg ? Hds : Hs);
+    const char* Dq = static_cast<const char*>(seg ? Dd : D);
     const int nr = me > mb ? me - mb : 0;
-    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * KX, nr * KX * 4);
+    const rsrc_t rx = make_rsrc(Xs + (size_t)mb * XRB, nr * XRB);
     // (row mb - 1 based: every voffset >= 0; h_{-1} rows are masked by t)
-    const rsrc_t rh = make_rsrc(Hq + ((ptrdiff_t)mb - 1) * FH, (nr ? nr + 1 : 0) * FH * 4);
-    const rsrc_t rd = make_rsrc(Dq + (size_t)mb * FG + jbase, nr ? ((nr - 1) * FG + WQ_CD) * 4 : 0);
+    const rsrc_t rh = make_rsrc(Hq + ((ptrdiff_t)mb - 1) * HRB, (nr ? nr + 1 : 0) * HRB);
+    const rsrc_t rd = make_rsrc(Dq + (size_t)mb * DRB + jbase * (PD ? 2 : 4),
+                                nr ? (nr - 1) * DRB + (PD ? (2 * FG + WQ_CD) * 2 : WQ_CD * 4) : 0);
     int tm[JH];  // (row mod Tn) of this thread's H slots at the next chunk to load
 #pragma unroll
     for (int j = 0; j < JH; ++j) {
@@ -1461,14 +1561,32 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
       slot_rc(s, r, c4, ok);
       ok = ok && r < me - m0;
       if (s < JX) {
-        v[s] = ld4s(rx, ok ? (r * KX + 4 * c4) * 4 : kOOB, (m0 - mb) * KX * 4);
+        if constexpr (PX) {
+          const int vo = ok ? r * XRB + 8 * c4 : kOOB;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) pv[s][q] = ld8(rx, vo + 2 * KX * q, (m0 - mb) * XRB);
+        } else {
+          v[s] = ld4s(rx, ok ? (r * KX + 4 * c4) * 4 : kOOB, (m0 - mb) * XRB);
+        }
       } else if (s < JX + JH) {
         int& tmj = tm[s - JX];
-        v[s] = ld4s(rh, ok && tmj != 0 ? (r * FH + 4 * c4) * 4 : kOOB, (m0 - mb) * FH * 4);
+        if constexpr (PH) {
+          const int vo = ok && tmj != 0 ? r * HRB + 8 * c4 : kOOB;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) pv[s][q] = ld8(rh, vo + 2 * FH * q, (m0 - mb) * HRB);
+        } else {
+          v[s] = ld4s(rh, ok && tmj != 0 ? (r * FH + 4 * c4) * 4 : kOOB, (m0 - mb) * HRB);
+        }
         tmj += step32;
         if (tmj >= Tn) tmj -= Tn;
       } else {
-        v[s] = ld4s(rd, ok ? (r * FG + 4 * c4) * 4 : kOOB, (m0 - mb) * FG * 4);
+        if constexpr (PD) {
+          const int vo = ok ? r * DRB + 8 * c4 : kOOB;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) pv[s][q] = ld8(rd, vo + 2 * FG * q, (m0 - mb) * DRB);
+        } else {
+          v[s] = ld4s(rd, ok ? (r * FG + 4 * c4) * 4 : kOOB, (m0 - mb) * DRB);
+        }
       }
     };
     auto stage = [&](lds_char* base, int s) {
@@ -1476,15 +1594,21 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
       bool ok;
       slot_rc(s, r, c4, ok);
       if (!ok) return;
-      uint32_t p[3][2];
-      split3(v[s], p);
       int lo, pl;
-      if (s < JX) { lo = r * GI::ROWA + 8 * c4; pl = GI::PLA; }
-      else if (s < JX + JH) { lo = r * GI::ROWA + 2 * KX + 8 * c4; pl = GI::PLA; }
-      else { lo = GI::IMGD + r * GI::ROWD + 8 * c4; pl = GI::PLD; }
+      bool planes;
+      if (s < JX) { lo = r * GI::ROWA + 8 * c4; pl = GI::PLA; planes = PX; }
+      else if (s < JX + JH) { lo = r * GI::ROWA + 2 * KX + 8 * c4; pl = GI::PLA; planes = PH; }
+      else { lo = GI::IMGD + r * GI::ROWD + 8 * c4; pl = GI::PLD; planes = PD; }
+      if (planes) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
-        *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(base + lo + q * pl) = u32x2_t{p[q][0], p[q][1]};
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(base + lo + q * pl) = pv[s][q];
+      } else {
+        uint32_t p[3][2];
+        split3(v[s], p);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(base + lo + q * pl) = u32x2_t{p[q][0], p[q][1]};
+      }
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -1599,7 +1723,8 @@ lstmf_wgrad_q4_kernel(const float* __restrict__ X, const float* __restrict__ Hs,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = 16 * (i0w + ii) + 4 * g + r;
-        if (ii < niw && jj < njw && i < G::KR && col < WQ_CD) out[(size_t)i * FG + jbase + col] = acc[ii * 4 + jj][r];
+        if (ii < niw && jj < njw && i < G::KR && col < WQ_CD)
+          out[(size_t)i * FG + (PD ? gate_nat(jbase + col) : jbase + col)] = acc[ii * 4 + jj][r];
       }
     }
 }
@@ -2097,9 +2222,12 @@ constexpr int DS4_K0 = DS_KS - DS4_SLOTS;     // first k-step followed by a stag
 // 3.59 vs 3.54 ms at 6.3 M rows: profiles/r04_wgrad/wdma2)
 constexpr int DS4_NS = 2;
 
-template <int NT2>
+// PD: dZ arrives as FP3 planes in the interleaved gate order (W^T's k runs over gate_nat(k) then, and the
+// staging copies the planes as loaded: no split)
+template <int NT2, bool PD = false>
 __global__ void __launch_bounds__(256, 1)
-lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, float* __restrict__ X, int M, int KO) {
+lstmf_dgrad_s4_kernel(const void* __restrict__ D, const float* __restrict__ W, float* __restrict__ X, int M, int KO) {
+  constexpr int DRB = PD ? 6 * FG : 4 * FG;  // dZ row bytes
   extern __shared__ __attribute__((aligned(16))) char dsm_[];
   lds_char* dsm = (lds_char*)dsm_;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2116,8 +2244,16 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
       const int k0 = 32 * ks + 8 * g;
       f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
       if (w < NT2 && col < KO && k0 < FG) {
-        v0 = *reinterpret_cast<const f32x4*>(W + (size_t)col * FG + k0);
-        v1 = *reinterpret_cast<const f32x4*>(W + (size_t)col * FG + k0 + 4);
+        if constexpr (PD) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v0[j] = W[(size_t)col * FG + gate_nat(k0 + j)];
+            v1[j] = W[(size_t)col * FG + gate_nat(k0 + 4 + j)];
+          }
+        } else {
+          v0 = *reinterpret_cast<const f32x4*>(W + (size_t)col * FG + k0);
+          v1 = *reinterpret_cast<const f32x4*>(W + (size_t)col * FG + k0 + 4);
+        }
       }
       uint32_t p0[3][2], p1[3][2];
       split3(v0, p0);
@@ -2133,26 +2269,38 @@ lstmf_dgrad_s4_kernel(const float* __restrict__ D, const float* __restrict__ W, 
     }
   }
   f32x4 v[DS4_NS][DS4_SLOTS];
+  u32x2_t pv[DS4_NS][DS4_SLOTS][3];  // (PD)
   auto load = [&](auto S_, int c) {  // chunk c's rows (past M: zero-size descriptor, zeros)
     constexpr int S = decltype(S_)::value;
     const int r0 = c * 16, nr = c < nch ? min(16, M - r0) : 0;
-    const rsrc_t rd = make_rsrc(D + (nr ? (size_t)r0 * FG : 0), nr * FG * 4);
+    const rsrc_t rd = make_rsrc(static_cast<const char*>(D) + (nr ? (size_t)r0 * DRB : 0), nr * DRB);
 #pragma unroll
     for (int j = 0; j < DS4_SLOTS; ++j) {
       const int e = tid + 256 * j, r = e / 100, c4 = e - 100 * r;
-      v[S][j] = ld4(rd, e < 1600 ? (r * FG + 4 * c4) * 4 : kOOB);
+      if constexpr (PD) {
+        const int vo = e < 1600 ? r * DRB + 8 * c4 : kOOB;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) pv[S][j][q] = ld8(rd, vo + 2 * FG * q, 0);
+      } else {
+        v[S][j] = ld4(rd, e < 1600 ? (r * FG + 4 * c4) * 4 : kOOB);
+      }
     }
   };
   auto stage = [&](auto S_, lds_char* buf, int j) {
     constexpr int S = decltype(S_)::value;
     const int e = tid + 256 * j, r = e / 100, c4 = e - 100 * r;
     if (e >= 1600) return;
-    uint32_t p[3][2];
-    split3(v[S][j], p);
     const int lo = (r * DS4_RS + 4 * c4) * 2;
+    if constexpr (PD) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
-      *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(buf + q * DS4_PL + lo) = u32x2_t{p[q][0], p[q][1]};
+      for (int q = 0; q < 3; ++q) *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(buf + q * DS4_PL + lo) = pv[S][j][q];
+    } else {
+      uint32_t p[3][2];
+      split3(v[S][j], p);
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(buf + q * DS4_PL + lo) = u32x2_t{p[q][0], p[q][1]};
+    }
   };
   // zero the k = 400..415 pad columns of both buffers (never staged; the k-step 12 fragments read them)
   for (int i = tid; i < 2 * 3 * 16 * 2; i += 256) {
@@ -2531,9 +2679,11 @@ size_t lstmf_wgrad_workspace_floats(int M, int K, int impl) {
   return (size_t)z * ((K == 35 ? 36 : K) + FH + 1) * FG;
 }
 
-bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const float* Xd, const float* Hds, const float* Dd,
-                        float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl) {
+bool launch_lstmf_wgrad(const void* X, const void* Hs, const void* D, const void* Xd, const void* Hds, const void* Dd,
+                        float* gW, float* gU, float* gb, int M, int K, int Tn, float* ws, hipStream_t s, int impl, int pm) {
   if (!lstmf_wgrad_supported(K, FH, FG) || M <= 0) return false;
+  if (pm != 0 && (wgradf_pick(impl, K, M) == 1 || K == 35 || K == 36))
+    throw std::runtime_error("lstmf_wgrad: FP3-plane operands need the split kernels and K in {32, 100}");
   if (wgradf_pick(impl, K, M) == 3) {
     const int z0 = wgradq_z(M);
     const int rpz = ((M + z0 - 1) / z0 + 31) / 32 * 32;
@@ -2542,10 +2692,12 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
       allow_lds(reinterpret_cast<const void*>(k));
       hipLaunchKernelGGL(k, dim3(4 * z), dim3(512), sm, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpz, z);
     };
-    switch (K) {
-      case 32: go(lstmf_wgrad_q4_kernel<32>, 2 * WQGeo<32>::Img::BUF); break;
-      case 36: go(lstmf_wgrad_q4_kernel<36>, 2 * WQGeo<36>::Img::BUF); break;
-      default: go(lstmf_wgrad_q4_kernel<100>, 2 * WQGeo<100>::Img::BUF); break;
+    switch (K * 8 + pm) {
+#define HFREP_Q4(KK, PP) case KK * 8 + PP: go(lstmf_wgrad_q4_kernel<KK, PP>, 2 * WQGeo<KK>::Img::BUF); break;
+      HFREP_Q4(32, 0) HFREP_Q4(36, 0) HFREP_Q4(100, 0)
+      HFREP_Q4(32, 4) HFREP_Q4(32, 6) HFREP_Q4(32, 7) HFREP_Q4(100, 4) HFREP_Q4(100, 6) HFREP_Q4(100, 7)
+#undef HFREP_Q4
+      default: throw std::runtime_error("lstmf_wgrad: no quad kernel for this K / plane mask");
     }
     launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s);
     return true;
@@ -2558,11 +2710,14 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
       allow_lds(reinterpret_cast<const void*>(k));
       hipLaunchKernelGGL(k, dim3(2 * z), dim3(512), sm, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpz, z);
     };
-    switch (K) {
-      case 32: go(lstmf_wgrad_split_kernel<32>, 2 * WSGeo<32>::Img::BUF); break;
-      case 35: go(lstmf_wgrad_split_kernel<36, 35>, 2 * WSGeo<36>::Img::BUF); break;
-      case 36: go(lstmf_wgrad_split_kernel<36>, 2 * WSGeo<36>::Img::BUF); break;
-      default: go(lstmf_wgrad_split_kernel<100>, 2 * WSGeo<100>::Img::BUF); break;
+    switch (K * 8 + pm) {
+      case 35 * 8: go(lstmf_wgrad_split_kernel<36, 35>, 2 * WSGeo<36>::Img::BUF); break;
+      case 36 * 8: go(lstmf_wgrad_split_kernel<36>, 2 * WSGeo<36>::Img::BUF); break;
+      case 100 * 8: go(lstmf_wgrad_split_kernel<100>, 2 * WSGeo<100>::Img::BUF); break;
+#define HFREP_WS(PP) case 32 * 8 + PP: go(lstmf_wgrad_split_kernel<32, 32, PP>, 2 * WSGeo<32>::Img::BUF); break;
+      HFREP_WS(0) HFREP_WS(4) HFREP_WS(6) HFREP_WS(7)
+#undef HFREP_WS
+      default: throw std::runtime_error("lstmf_wgrad: no pair kernel for this K / plane mask");
     }
     launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s, K == 35 ? 36 : K);
     return true;
@@ -2570,11 +2725,13 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
   const int grid = wgradf_grid(M);
   const int rpw = ((M + grid - 1) / grid + WF_R - 1) / WF_R * WF_R;
   const int z = (M + rpw - 1) / rpw;
+  const float *Xf = static_cast<const float*>(X), *Hf = static_cast<const float*>(Hs), *Df = static_cast<const float*>(D);
+  const float *Xdf = static_cast<const float*>(Xd), *Hdf = static_cast<const float*>(Hds), *Ddf = static_cast<const float*>(Dd);
   switch (K) {
-    case 32: hipLaunchKernelGGL(lstmf_wgrad_kernel<32>, dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
-    case 35: hipLaunchKernelGGL((lstmf_wgrad_kernel<36, 35>), dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
-    case 36: hipLaunchKernelGGL(lstmf_wgrad_kernel<36>, dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
-    default: hipLaunchKernelGGL(lstmf_wgrad_kernel<100>, dim3(z), dim3(512), 0, s, X, Hs, D, Xd, Hds, Dd, ws, M, Tn, rpw); break;
+    case 32: hipLaunchKernelGGL(lstmf_wgrad_kernel<32>, dim3(z), dim3(512), 0, s, Xf, Hf, Df, Xdf, Hdf, Ddf, ws, M, Tn, rpw); break;
+    case 35: hipLaunchKernelGGL((lstmf_wgrad_kernel<36, 35>), dim3(z), dim3(512), 0, s, Xf, Hf, Df, Xdf, Hdf, Ddf, ws, M, Tn, rpw); break;
+    case 36: hipLaunchKernelGGL(lstmf_wgrad_kernel<36>, dim3(z), dim3(512), 0, s, Xf, Hf, Df, Xdf, Hdf, Ddf, ws, M, Tn, rpw); break;
+    default: hipLaunchKernelGGL(lstmf_wgrad_kernel<100>, dim3(z), dim3(512), 0, s, Xf, Hf, Df, Xdf, Hdf, Ddf, ws, M, Tn, rpw); break;
   }
   launch_lstm_wgrad2_reduce(ws, gW, gU, gb, z, K, FH, FG, s, K == 35 ? 36 : K);
   return true;
@@ -2582,29 +2739,52 @@ bool launch_lstmf_wgrad(const float* X, const float* Hs, const float* D, const f
 
 bool lstmf_dgrad_supported(int N, int KO) { return N == FG && KO >= 1 && KO <= 16 * FNT; }
 
+void launch_fp3_split(const float* x, uint16_t* p, int64_t M, int C, bool interleave, hipStream_t s) {
+  if (M <= 0) return;
+  if (C % 4 != 0 || (interleave && C != FG)) throw std::runtime_error("fp3_split: C % 4 == 0 (400 when interleaved)");
+  const int64_t n4 = M * (C / 4);
+  const int grid = (int)std::min<int64_t>((n4 + 255) / 256, (int64_t)device_cu_count() * 16);
+  if (interleave) hipLaunchKernelGGL(fp3_split_kernel<true>, dim3(grid), dim3(256), 0, s, x, p, M, C);
+  else hipLaunchKernelGGL(fp3_split_kernel<false>, dim3(grid), dim3(256), 0, s, x, p, M, C);
+}
+void launch_fp3_join(const uint16_t* p, float* x, int64_t M, int C, bool interleave, hipStream_t s) {
+  if (M <= 0) return;
+  if (interleave && C != FG) throw std::runtime_error("fp3_join: interleaved planes are 400 wide");
+  const int64_t n = M * C;
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, (int64_t)device_cu_count() * 16);
+  if (interleave) hipLaunchKernelGGL(fp3_join_kernel<true>, dim3(grid), dim3(256), 0, s, p, x, M, C);
+  else hipLaunchKernelGGL(fp3_join_kernel<false>, dim3(grid), dim3(256), 0, s, p, x, M, C);
+}
+
 // impl 1 / 3: the exact-fp32 MFMA kernel / the LDS-staged split kernel lstmf_dgrad_s4_kernel; default
 // (0): exact under HFREP_FP32_EXACT, else s4 for KO > 64 and exact otherwise (s4 keeps one wave busy
 // per 32 output columns, so KO = 32 leaves three SIMDs idle; profiles/r03_split)
 static int dgradf_version() { return fp32_exact() ? 1 : 0; }
 
-bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl) {
+bool launch_lstmf_dgrad(const void* D, const float* W, float* X, int M, int N, int KO, hipStream_t s, int impl, bool pd) {
   if (!lstmf_dgrad_supported(N, KO) || M <= 0) return false;
   const int dv = impl == 1 || impl == 3 ? impl : dgradf_version();
-  if (dv == 3 || (dv == 0 && KO > 64)) {
+  if (pd && dv == 1) throw std::runtime_error("lstmf_dgrad: FP3-plane dZ needs the split kernel");
+  if (pd || dv == 3 || (dv == 0 && KO > 64)) {
     const int chunks = (M + 15) / 16, cus = device_cu_count();
     const int grid = chunks < cus ? chunks : cus;
     auto go = [&](auto k) {
       allow_lds(reinterpret_cast<const void*>(k));
       hipLaunchKernelGGL(k, dim3(grid), dim3(256), (size_t)2 * DS4_BUF, s, D, W, X, M, KO);
     };
-    switch ((KO + 31) / 32) {
+    switch ((KO + 31) / 32 + (pd ? 4 : 0)) {
       case 1: go(lstmf_dgrad_s4_kernel<1>); break;
       case 2: go(lstmf_dgrad_s4_kernel<2>); break;
       case 3: go(lstmf_dgrad_s4_kernel<3>); break;
-      default: go(lstmf_dgrad_s4_kernel<4>); break;
+      case 4: go(lstmf_dgrad_s4_kernel<4>); break;
+      case 5: go(lstmf_dgrad_s4_kernel<1, true>); break;
+      case 6: go(lstmf_dgrad_s4_kernel<2, true>); break;
+      case 7: go(lstmf_dgrad_s4_kernel<3, true>); break;
+      default: go(lstmf_dgrad_s4_kernel<4, true>); break;
     }
     return true;
   }
+  const float* Df = static_cast<const float*>(D);
   // one workgroup per CU (two for NT <= 3: HBM-bound there, and the registers allow a second one
   // in flight); more only if a workgroup's dZ range would pass 2 GB (32-bit buffer offsets)
   const int chunks = (M + 15) / 16, cus = device_cu_count() * (KO <= 48 ? 2 : 1);
@@ -2614,13 +2794,13 @@ bool launch_lstmf_dgrad(const float* D, const float* W, float* X, int M, int N, 
   const int rpw = (chunks + grid - 1) / grid * 16;
   const int z = (M + rpw - 1) / rpw;
   switch ((KO + 15) / 16) {
-    case 1: hipLaunchKernelGGL(lstmf_dgrad_kernel<1>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
-    case 2: hipLaunchKernelGGL(lstmf_dgrad_kernel<2>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
-    case 3: hipLaunchKernelGGL(lstmf_dgrad_kernel<3>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
-    case 4: hipLaunchKernelGGL(lstmf_dgrad_kernel<4>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
-    case 5: hipLaunchKernelGGL(lstmf_dgrad_kernel<5>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
-    case 6: hipLaunchKernelGGL(lstmf_dgrad_kernel<6>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
-    default: hipLaunchKernelGGL(lstmf_dgrad_kernel<7>, dim3(z), dim3(256), 0, s, D, W, X, M, KO, rpw); break;
+    case 1: hipLaunchKernelGGL(lstmf_dgrad_kernel<1>, dim3(z), dim3(256), 0, s, Df, W, X, M, KO, rpw); break;
+    case 2: hipLaunchKernelGGL(lstmf_dgrad_kernel<2>, dim3(z), dim3(256), 0, s, Df, W, X, M, KO, rpw); break;
+    case 3: hipLaunchKernelGGL(lstmf_dgrad_kernel<3>, dim3(z), dim3(256), 0, s, Df, W, X, M, KO, rpw); break;
+    case 4: hipLaunchKernelGGL(lstmf_dgrad_kernel<4>, dim3(z), dim3(256), 0, s, Df, W, X, M, KO, rpw); break;
+    case 5: hipLaunchKernelGGL(lstmf_dgrad_kernel<5>, dim3(z), dim3(256), 0, s, Df, W, X, M, KO, rpw); break;
+    case 6: hipLaunchKernelGGL(lstmf_dgrad_kernel<6>, dim3(z), dim3(256), 0, s, Df, W, X, M, KO, rpw); break;
+    default: hipLaunchKernelGGL(lstmf_dgrad_kernel<7>, dim3(z), dim3(256), 0, s, Df, W, X, M, KO, rpw); break;
   }
   return true;
 }

@@ -85,10 +85,16 @@ class GradSync:
         self._last = None
         # HFREP_DP_P2P=1: buckets of <= HFREP_DP_P2P_CAP floats go through the one-shot IPC all-reduce
         # (parallel/p2p.py, csrc/p2p.hip) on a side stream instead of RCCL; built at the first bucket
-        self.use_p2p = (os.environ.get("HFREP_DP_P2P", "0") == "1" and self.backend == "nccl" and world > 1)
+        # (HFREP_DP_P2P=force: any process group carries the handles -- gloo ranks sharing one GPU in
+        # scripts/bench_dp_shared.py; the buckets must be CUDA tensors of processes on one node)
+        mode = os.environ.get("HFREP_DP_P2P", "0")
+        self.use_p2p = world > 1 and ((mode == "1" and self.backend == "nccl") or mode == "force")
         self.p2p_cap = int(os.environ.get("HFREP_DP_P2P_CAP", str(1 << 21)))
         self.p2p = None
         self._p2p_stream = None
+        # exposed-wait timing (bench.py): per finish_ an event pair on the compute stream around the join
+        self.timing = False
+        self._events = []
 
     def _p2p_for(self, t: torch.Tensor):
         """The one-shot all-reduce for bucket ``t`` (None: RCCL).  The first call is collective."""
@@ -142,6 +148,10 @@ class GradSync:
 
     def finish_(self) -> int:
         n = len(self._pending)
+        timed = self.timing and n > 0 and self._pending_on_gpu()
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         for w in self._pending:
             if isinstance(w, tuple) and w[0] == "p2p":
                 torch.cuda.current_stream(w[1].device).wait_stream(w[1])
@@ -151,7 +161,31 @@ class GradSync:
             else:
                 w.wait()
         self._pending = []
+        if timed:
+            e1.record()
+            self._events.append((e0, e1))
         return n
+
+    def _pending_on_gpu(self) -> bool:
+        return torch.cuda.is_available() and (self.backend == "nccl" or self.p2p is not None)
+
+    def exposed_wait_ms(self, reset: bool = True) -> float:
+        """Total time the compute stream spent waiting for bucket all-reduces at :meth:`finish_` since the
+        last reset (the non-overlapped part of the gradient averaging; needs ``timing = True``).
+        Synchronises on the recorded events."""
+        tot = 0.0
+        for e0, e1 in self._events:
+            e1.synchronize()
+            tot += e0.elapsed_time(e1)
+        if reset:
+            self._events = []
+        return tot
+
+    def graph_capturable(self) -> bool:
+        """Whether a step's bucket all-reduces can be captured into a hipGraph at all: RCCL collectives, or
+        every bucket on the one-shot P2P kernel (device-side epochs; the group only carried the IPC
+        handles).  gloo collectives cannot be captured."""
+        return self.world <= 1 or self.backend == "nccl" or self.use_p2p
 
     def check_errors(self, blocking: bool = False) -> None:
         """Surface a failed one-shot all-reduce (P2PTimeout).  Non-blocking by default (pinned-host
@@ -203,6 +237,8 @@ class GradSync:
         rank, same point); nccl only.  Returns whether the switch happened."""
         if self.backend != "nccl" or self.world <= 1 or self.group is None:
             return False
+        if self.use_p2p:
+            return False  # the buckets go through the P2P kernel: no RCCL work inside the capture
         if self._graph_group is None:
             ranks = dist.get_process_group_ranks(self.group)
             dev = torch.device("cuda", torch.cuda.current_device())

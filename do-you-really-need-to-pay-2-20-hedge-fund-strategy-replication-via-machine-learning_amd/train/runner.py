@@ -89,8 +89,8 @@ class GraphedStep:
             # GPUs have not been checked against the eager step yet (RCCL refuses two ranks on one
             # GPU, and the pool's boxes have one), so under DP the capture is opt-in:
             # HFREP_GRAPH_DP=1.  Without it a DP run replays nothing and steps eagerly.
-            if trainer.grad_sync.backend != "nccl":
-                raise RuntimeError("graph capture under data parallelism needs RCCL")
+            if not trainer.grad_sync.graph_capturable():
+                raise RuntimeError("graph capture under data parallelism needs RCCL or the P2P all-reduce")
             if os.environ.get("HFREP_GRAPH_DP", "0") != "1":
                 raise RuntimeError("graph capture under data parallelism is opt-in (HFREP_GRAPH_DP=1): multi-rank "
                                    "replay parity is unpinned")

@@ -268,6 +268,9 @@ def test_bench_aggregate_uses_max_elapsed_over_ranks():
         per_rank_windows = 5 * 4 + 4  # n_critic * B + B
         assert res[r]["windows_per_step"] == per_rank_windows * world
         assert res[r]["value"] == round(per_rank_windows * world * 2 / max(local), 2)
+        # the DP fields of the record: gloo buckets (no GPU events: zero exposed wait), one entry per rank
+        assert res[r]["allreduce"] == "gloo" and res[r]["buckets"] == 2
+        assert res[r]["allreduce_exposed_ms_per_step"] == [0.0] * world
 
 
 def test_bench_refuses_gpus_world_mismatch():
@@ -309,5 +312,11 @@ def test_gradsync_p2p_selection(monkeypatch):
     assert gs.p2p_cap == 1000
     assert gs._p2p_for(torch.zeros(10)) is None  # CPU tensor
     assert gs._p2p_for(torch.zeros(2000)) is None  # over the cap
+    monkeypatch.setenv("HFREP_DP_P2P", "force")  # any group carries the handles (shared-GPU benches)
+    assert GradSync(None, 2).use_p2p and not GradSync(None, 1).use_p2p
+    assert GradSync(None, 2).graph_capturable()
     monkeypatch.delenv("HFREP_DP_P2P")
     assert not GradSync(None, 2).use_p2p
+    assert not GradSync(None, 2).graph_capturable()  # gloo buckets cannot be captured
+    gs = GradSync(None, 2)
+    assert gs.exposed_wait_ms() == 0.0 and gs.check_errors() is None and gs.close() is None

@@ -313,3 +313,74 @@ def test_p2p_allreduce_missing_peer_fails_loud(cuda):
     assert r0["poll_raised"], r0
     assert r0["epochs"] == 1, r0  # the failed call did not advance the epoch
     assert r1["wait_s"] < 1.0, r1  # poisoned: no wait
+
+
+def _graph_worker(rank, world, port, q):
+    """A hipGraph-replayed DP training step whose gradient buckets go through the P2P all-reduce, against
+    the eager step of an identical trainer: bitwise equal parameters after 5 iterations, on every rank."""
+    try:
+        import os
+
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+
+        import hfrep  # noqa: F401
+        from hfrep.train.gan_trainer import GANConfig, GANTrainer
+        from hfrep.train.runner import GraphedStep
+
+        os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+        os.environ["HFREP_GRAPH_DP"] = "1"  # captured DP collectives are opt-in
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        ds = np.random.RandomState(0).rand(512, 24, 32).astype(np.float32)
+        cfg = GANConfig(arch="lstm", loss="wgan_gp", window=24, features=32, batch_size=64, dtype="float32")
+        trs = []
+        for _ in range(2):
+            tr = GANTrainer(cfg, ds, device=dev, process_group=dist.group.WORLD, rank=rank, world=world)
+            tr.grad_sync.use_p2p = True  # (the env switch is for nccl groups; the handles go over gloo)
+            trs.append(tr)
+        graphed, eager = trs
+        step = GraphedStep(graphed, warmup=2)
+        for _ in range(5):
+            step()
+            eager.train_step()
+        torch.cuda.synchronize()
+        pg = torch.cat([graphed.generator.flat.detach(), graphed.critic.flat.detach()]).cpu()
+        pe = torch.cat([eager.generator.flat.detach(), eager.critic.flat.detach()]).cpu()
+        res = {"rank": rank, "captured": step.graph is not None, "same": bool(torch.equal(pg, pe)),
+               "finite": bool(torch.isfinite(pg).all()), "params": pg.numpy(),
+               "second_comm": graphed.grad_sync._graph_group is not None}
+        for tr in trs:
+            tr.grad_sync.check_errors(blocking=True)
+            tr.close()
+        dist.destroy_process_group()
+        q.put(res)
+    except Exception:
+        q.put(traceback.format_exc())
+
+
+def test_graphed_dp_step_over_p2p(cuda):
+    import numpy as np
+    import torch.multiprocessing as mp
+
+    from _spawn import gather
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_graph_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = gather(procs, q, 2, timeout=240)
+    for p in procs:
+        p.join(timeout=30)
+    for r in res:
+        assert not isinstance(r, str), r
+        assert r["captured"] and r["same"] and r["finite"], {k: v for k, v in r.items() if k != "params"}
+        assert not r["second_comm"], r["rank"]  # P2P buckets: no second (graph-only) communicator
+    np.testing.assert_array_equal(res[0]["params"], res[1]["params"])
