@@ -150,8 +150,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    # per-GPU batch sized for HBM (fp32 ~147 GB, bf16 ~85 GB of 288 GB at 262144 windows per GPU):
-    # bf16 throughput 2.21 M (32k) -> 2.48 M seq/s (262k) on one MI355X (profiles/r01_batch_sweep)
+    # per-GPU batch sized for HBM: 262144 windows per GPU use 194 GB (fp32) / 106 GB (bf16) of the 288 GB
+    # (BENCH_r04.json peak_mem_gb_rank0); larger batches amortise the per-call tails of the persistent
+    # kernels (profiles/r01_batch_sweep)
     ap.add_argument("--batch-per-gpu", type=int, default=262144)
     ap.add_argument("--window", type=int, default=24)
     ap.add_argument("--features", type=int, default=32)
@@ -215,7 +216,7 @@ def main():
             },
             "losses_finite": res["losses_finite"],
             # the W-dist half of the metric is a training-quality run, not a throughput step
-            "w_dist_parity": "profiles/r03_parity/README.md" if args.model == "mtss_wgan_gp" else None,
+            "w_dist_parity": "profiles/r05_parity/README.md" if args.model == "mtss_wgan_gp" else None,
             "peak_mem_gb_rank0": res["peak_mem_gb_rank0"],
             # data-parallel gradient averaging: collective, buckets per model, and each rank's exposed
             # (non-overlapped) all-reduce wait per step

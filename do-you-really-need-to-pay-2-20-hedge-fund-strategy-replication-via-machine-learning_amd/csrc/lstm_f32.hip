@@ -655,6 +655,9 @@ lstmf_bwdp_kernel(const float* __restrict__ dH, const float* __restrict__ tape, 
 // halves (c, cdot and the two adjoint carries) and ONE set of step loads (gates, zdot, c_{t-1},
 // cdot_{t-1}, dH, dHd: 12 per cell): the set for the other half is issued right after a half's
 // cells, and lands while the MFMA waves finish the half-phase.
+#ifndef HFREP_TBWD_CELLGROUP
+#define HFREP_TBWD_CELLGROUP 1
+#endif
 template <int ACT>
 __global__ void __launch_bounds__(512, 1)
 lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, const float* __restrict__ tape,
@@ -848,7 +851,9 @@ lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, 
           }
           tc[m][n] = cp;
           tcd[m][n] = cdp;
-          __builtin_amdgcn_sched_barrier(0);  // one cell's temporaries at a time
+          // one cell's temporaries at a time (HFREP_TBWD_CELLGROUP > 1: that many cells per schedule
+          // region, an A/B knob for the cell role's instruction-level parallelism)
+          if ((n + 1) % HFREP_TBWD_CELLGROUP == 0 || n == FNT - 1) __builtin_amdgcn_sched_barrier(0);
         }
       };
       using I0 = std::integral_constant<int, 0>;

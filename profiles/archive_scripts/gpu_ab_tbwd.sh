@@ -1,6 +1,6 @@
 #!/bin/bash
 # fp32 tangent reverse (lstmf_tbwdp_kernel): numerics, then base vs variants/<v> timing and the step.
-#   bash scripts/gpu_ab_tbwd.sh <outdir> <variant> [<variant> ...]
+#   bash profiles/archive_scripts/gpu_ab_tbwd.sh <outdir> <variant> [<variant> ...]
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"
 OUT=gpurun_out/$1; shift; mkdir -p $OUT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # bf16 LSTM weight gradient (lstm_wgrad3): numerics of variants/<v> (HFREP_NATIVE_LIB), then base vs
 # variant kernel timing and the bf16 step.
-#   bash scripts/gpu_ab_w3.sh <outdir> <variant>
+#   bash profiles/archive_scripts/gpu_ab_w3.sh <outdir> <variant>
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"
 OUT=gpurun_out/$1; V=$2; mkdir -p $OUT

@@ -1,6 +1,6 @@
 #!/bin/bash
 # wgrad3 split count by M: numerics of variants/<v>, then the reference preset (B = 32) and the bench-shape
-# kernel timing, base vs variant.   bash scripts/gpu_ab_w3s.sh <outdir> <variant>
+# kernel timing, base vs variant.   bash profiles/archive_scripts/gpu_ab_w3s.sh <outdir> <variant>
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"
 OUT=gpurun_out/$1; V=$2; mkdir -p $OUT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 closing pass on one GPU: bitwise determinism (small and large batch), the whole GPU suite,
 # smoke(), the headline bench, and rocprofv3 kernel tables of 3 fp32 and 3 bf16 iterations.
-# usage: scripts/gpu_r03_final.sh OUTNAME
+# usage: profiles/archive_scripts/gpu_r03_final.sh OUTNAME
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"
 OUT=gpurun_out/${1:-r03_final}; mkdir -p $OUT

@@ -2,7 +2,7 @@
 # PMC table of the round-3 fp32 LSTM kernels (split BPTT / forward, quad + pair split weight gradients, split
 # dX, exact K = 100 forward and tangent reverse): bench_lstm.py at B = 32768, K = 32 and 100, three passes
 # per K (counter groups within the per-block limits), then scripts/pmc_table.py.
-# usage: scripts/pmc_lstmf_r03.sh OUTNAME
+# usage: profiles/archive_scripts/pmc_lstmf_r03.sh OUTNAME
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"
 OUT=gpurun_out/${1:-pmc_r03}; mkdir -p $OUT

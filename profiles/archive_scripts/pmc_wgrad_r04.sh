@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over the default fp32 weight-gradient kernels (K = 32: split pair, K = 100: quad) at
 # B = 65536 x T = 24: issue mix, MFMA busy, LDS traffic / conflicts, waits, HBM bytes.
-#   bash scripts/pmc_wgrad_r04.sh OUTNAME
+#   bash profiles/archive_scripts/pmc_wgrad_r04.sh OUTNAME
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"
 OUT=gpurun_out/${1:-pmc_wgrad_r04}; mkdir -p $OUT

@@ -1,9 +1,12 @@
 """HIP kernel numerics vs plain PyTorch fp32/fp64 references (run on an MI355X with -m gpu).
 
 Every native op in ``torch.ops.hfrep`` is compared against the reference implementation of the
-same op (``hfrep.ops.reference``) evaluated in fp64 on the CPU.  fp32 kernels use the exact
-f32 MFMA (32x32x2f32), so tolerances are tight; bf16 kernels are compared with bf16-level
-tolerances relative to the output scale.
+same op (``hfrep.ops.reference``) evaluated in fp64 on the CPU.  fp32 kernels run either on the
+exact-f32 MFMA (16x16x4 f32) or -- the default for the recurrent products, weight gradients and the
+K = 100 input gradient -- as the fp32-accurate three-term bf16 split (every operand h + m + l, six
+products); both are held to fp32-level tolerances, and the split kernels to <= 2x the exact kernel's
+error vs fp64 (``test_lstmf_*split*``).  bf16 kernels are compared with bf16-level tolerances relative
+to the output scale.
 """
 import numpy as np
 import pytest
