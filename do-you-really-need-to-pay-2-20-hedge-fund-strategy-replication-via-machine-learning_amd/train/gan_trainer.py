@@ -17,6 +17,11 @@ MI355X-first differences (semantics preserved):
   critic update is the reverse-over-tangent Hessian-vector product (no autograd graph);
 * losses are accumulated on device and read back only at log intervals (the reference prints —
   and therefore syncs — every iteration, GAN/MTSS_WGAN_GP.py:284);
+* small batches run independent chains side by side on HIP streams (``concurrent``): at the
+  reference's batch of 32 one LSTM call occupies a single CU, so the W-terms chain and the gradient
+  penalty's input-gradient chain of a critic update, and the next critic update's generator forward,
+  overlap instead of queueing (same kernels, same inputs, same RNG draw order: bitwise the sequential
+  result, tests/test_gpu_runtime.py);
 * data parallel: each rank samples its own batch; the flat gradient buffer of each model is
   all-reduced (averaged) before the fused optimizer launch (``hfrep.parallel``).
 """
@@ -52,6 +57,7 @@ class GANConfig:
     seed: int = 123
     dtype: str = "float32"        # compute dtype of activations: float32 | bfloat16
     log_every: int = 100
+    concurrent: bool | None = None  # side-stream overlap of independent chains (None: auto, batch <= 2048)
     extra: dict = field(default_factory=dict)
 
     def entry(self) -> zoo.ZooEntry:
@@ -103,6 +109,8 @@ class GANTrainer:
         self._g_acc = torch.zeros(1, device=self.device)
         self._ones_cache = {}
         self.grad_sync = None  # set by hfrep.parallel.DataParallel
+        self.concurrent = self._want_concurrent(cfg)
+        self._streams = None
         if world > 1 and process_group is not None:
             from ..parallel.dp import GradSync
 
@@ -110,6 +118,29 @@ class GANTrainer:
             self.grad_sync.broadcast_params([self.generator, self.critic])
 
     # ------------------------------------------------------------------------------------
+    def _want_concurrent(self, cfg) -> bool:
+        """Side-stream overlap pays only where one chain leaves most CUs idle: the persistent LSTM kernels
+        take one CU per 32-row tile, so up to ~2048 rows per call (HFREP_CONCURRENT=0 / 1 overrides)."""
+        import os
+
+        if self.device.type != "cuda":
+            return False
+        env = os.environ.get("HFREP_CONCURRENT")
+        if env in ("0", "1"):
+            return env == "1"
+        if cfg.concurrent is not None:
+            return bool(cfg.concurrent)
+        return cfg.batch_size <= 2048
+
+    def _side(self, i: int):
+        """Side stream ``i`` (0: the gradient-penalty input-gradient chain, 1: the next generator forward),
+        or None when running sequentially."""
+        if not self.concurrent:
+            return None
+        if self._streams is None:
+            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(2)]
+        return self._streams[i]
+
     def _batch(self, B, out=None):
         real = self.rng.sample_windows(self.dataset, B, out_dtype=self.dtype, out=out)
         noise = self.rng.normal((B, self.cfg.window, self.cfg.features), dtype=self.dtype)
@@ -173,6 +204,46 @@ class GANTrainer:
         self._apply(self.critic)
         return out, ((fake, gtape) if keep_gen_tape else None)
 
+    def _gp_critic_steps_overlapped(self, B):
+        """The n_critic GP critic updates with the generator forward of update k + 1 on a side stream
+        while update k's critic work runs (the critic updates never touch G).  The RNG draws keep the
+        sequential order (real_k, noise_k, alpha_k, real_k+1, noise_k+1, ...), so every update sees the
+        bits it would see sequentially.  Returns (noise, (fake, tape)) of the last update for the
+        generator step."""
+        cfg, G = self.cfg, self.generator
+        side = self._side(1)
+        cur = torch.cuda.current_stream(self.device)
+        last = self.n_critic - 1
+
+        def sample():
+            with trange("critic/sample"):
+                xrf = torch.empty((2 * B, cfg.window, cfg.features), dtype=self.dtype, device=self.device)
+                real, noise = self._batch(B, out=xrf[:B])
+            return xrf, real, noise
+
+        def generate(noise, xrf, keep):
+            with trange("critic/generate"):
+                if keep:
+                    return G.efwd(noise, save=True, out=xrf[B:])
+                return G.predict(noise, out=xrf[B:]), None
+
+        xrf, real, noise = sample()
+        fake, gtape = generate(noise, xrf, self.reuse_gen_forward and last == 0)
+        for k in range(self.n_critic):
+            with trange("critic/generate"):
+                alpha = self.rng.uniform((B,))
+            if k < last:
+                nxt = sample()
+                side.wait_stream(cur)  # (after the sampling kernels of update k + 1)
+                with torch.cuda.stream(side):
+                    gnext = generate(nxt[2], nxt[0], self.reuse_gen_forward and k + 1 == last)
+            self._d_acc = self.critic_gp_grads(real, fake, alpha, xrf=xrf)
+            self._apply(self.critic)
+            if k < last:
+                cur.wait_stream(side)
+                (xrf, real, noise), (fake, gtape) = nxt, gnext
+        return noise, ((fake, gtape) if self.reuse_gen_forward else None)
+
     def critic_gp_grads(self, real, fake, alpha, xrf=None):
         """Accumulate d/dtheta_C of W(real,-1) + W(fake,+1) + lambda*GP(x_hat) into C.flat.grad.
 
@@ -180,19 +251,34 @@ class GANTrainer:
         halves (the sampler and the generator write straight into it: no concatenation copy)."""
         C = self.critic
         xh = Fn.interpolate(real, fake, alpha)
+        if xrf is None:
+            xrf = torch.cat([real, fake], 0)
+        side = self._side(0)
+        if side is not None:
+            # the gradient penalty's input-gradient chain (forward on x_hat, backward with wgrad off)
+            # shares nothing with the W-terms chain until gp_coef_pack: it runs on a side stream.  Every
+            # tensor it allocates lives until after the join below, and the side stream's next use
+            # starts with a fork from this stream, so no allocator block is reused across the streams
+            # while still in use.
+            cur = torch.cuda.current_stream(self.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side), trange("critic/gp_input_grad"):
+                sh, tape_h = C.efwd(xh, save=True)
+                g = C.ebwd(tape_h, self._ones(sh), need_dx=True, wgrad=False)
         # W terms on [real; fake]
         with trange("critic/w_terms"):
-            if xrf is None:
-                xrf = torch.cat([real, fake], 0)
             s, tape = C.efwd(xrf, save=True)
             # W(real, -1) and W(fake, +1): both segment means and the score gradient in one launch
             w, ds = Fn.gan_loss(s, s.numel() // 2, -1.0, 1.0, 0)
             C.ebwd(tape, ds)
+        if side is not None:
+            cur.wait_stream(side)
         # gradient penalty: g = dD/dx_hat (input gradient only), v = dGP/dg, then the
         # theta-gradient of <v, g> as reverse-over-tangent
         with trange("critic/gp_input_grad"):
-            sh, tape_h = C.efwd(xh, save=True)
-            g = C.ebwd(tape_h, self._ones(sh), need_dx=True, wgrad=False)
+            if side is None:
+                sh, tape_h = C.efwd(xh, save=True)
+                g = C.ebwd(tape_h, self._ones(sh), need_dx=True, wgrad=False)
             pack, v = Fn.gp_coef_pack(g, self.gp_weight, w)  # [total, W real, W fake, GP]
         with trange("critic/gp_second_order"):
             sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
@@ -258,6 +344,9 @@ class GANTrainer:
                 lr_ = self._wgan_step(real, -1.0, 0.0)
                 lf_ = self._wgan_step(fake, 1.0, self.clip)
                 self._d_acc = torch.stack([0.5 * (lr_ + lf_), lr_, lf_, torch.zeros_like(lr_)])
+            self._g_acc = self._generator_step(noise, gen=gen).reshape(1)
+        elif self._side(1) is not None:
+            noise, gen = self._gp_critic_steps_overlapped(B)
             self._g_acc = self._generator_step(noise, gen=gen).reshape(1)
         else:
             gen = None
