@@ -885,6 +885,12 @@ void p2p_allreduce_(Tensor x, Tensor buf, std::vector<int64_t> peers, int64_t ra
                               cur_stream(x));
 }
 
+std::vector<int64_t> fwd4_diag(bool reset) {
+  unsigned int c[4];
+  hfrep::lstm2_fwd4_diag(c, reset);
+  return {c[0], c[1], c[2], c[3]};
+}
+
 int64_t p2p_error(Tensor buf) {
   TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kByte, "p2p_error: a p2p_buffer tensor");
   GUARD(buf);
@@ -955,6 +961,7 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("p2p_close(int ptr) -> ()", &p2p_close);
   m.def("p2p_allreduce_(Tensor(a!) x, Tensor buf, int[] peers, int rank, int cap, float scale, float timeout_s) -> ()");
   m.def("p2p_error(Tensor buf) -> int");
+  m.def("fwd4_diag(bool reset=False) -> int[]", &fwd4_diag);  // no tensor inputs: catch-all kernel
 }
 
 TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {

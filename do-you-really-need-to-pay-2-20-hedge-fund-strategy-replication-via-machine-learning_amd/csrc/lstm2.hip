@@ -1141,6 +1141,25 @@ struct XPart {
   }
 };
 
+// Diagnosis build of the act = sigmoid tangent-forward nondeterminism (profiles/r03_race/README.md):
+// HFREP_TFWD4_SIGMOID=1 routes act = sigmoid back to this kernel; HFREP_FWD4_DIAG=1 re-derives, in the
+// last row half, every cell's tangent from accumulator and tape values read again long after the step's
+// MFMAs / loads (inline-asm register reads behind s_nops; tape re-loaded after vmcnt(0)) and counts /
+// prints every cell whose normally scheduled result differs.  Neither is set in the shipped library.
+#ifndef HFREP_TFWD4_SIGMOID
+#define HFREP_TFWD4_SIGMOID 0
+#endif
+#ifndef HFREP_FWD4_DIAG
+#define HFREP_FWD4_DIAG 0
+#endif
+#if HFREP_FWD4_DIAG
+__device__ unsigned int g_fwd4_diag[4];  // cells checked, accumulator mismatches, tape mismatches, printed
+__device__ __forceinline__ float late_read(float v) {  // a fresh VALU read of v's register, here
+  float r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+#endif
 template <int H, int ACT, int KX, bool TAPE, bool TAN>
 __global__ void __launch_bounds__(512)
 lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
@@ -1316,6 +1335,35 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
                 const float ca = act_f(act, cv);
                 float hd = odot * ca + og * act_dy(act, ca) * cdn;
                 if (!uok) { cdn = 0.f; hd = 0.f; }
+#if HFREP_FWD4_DIAG
+                if (m == 1) {
+                  const float cs0 = cs[e + u], cp0 = cprev[e + u];
+                  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+                  float al[4];
+#pragma unroll
+                  for (int q = 0; q < 4; ++q) al[q] = late_read(acc[q][m][i]);
+                  // the tape words again, from memory, after every load of this wave has landed
+                  const Slot8 re0 = ld_slot8(rp, uok, lo8, tape_off(t, wt32) + 0 * SLOT_ELEMS);
+                  const Slot8 re4 = ld_slot8(rp, uok, lo8, tape_off(t, wt32) + 4 * SLOT_ELEMS);
+                  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                  const float ig2 = late_read(ig), cv2 = late_read(cv);
+                  const bool tape_bad = uok && (re0.get(m, i) != ig2 || re4.get(m, i) != cv2);
+                  const float idot2 = ig * (1.f - ig) * al[0], fdot2 = fg * (1.f - fg) * al[1];
+                  const float gdot2 = act_dy(act, gg) * al[2], odot2 = og * (1.f - og) * al[3];
+                  float cdn2 = fdot2 * cp0 + fg * cs0 + idot2 * gg + ig * gdot2;
+                  float hd2 = odot2 * ca + og * act_dy(act, ca) * cdn2;
+                  if (!uok) { cdn2 = 0.f; hd2 = 0.f; }
+                  const bool acc_bad = fabsf(hd2 - hd) > 1e-3f * (fabsf(hd2) + 1e-3f) ||
+                                       fabsf(cdn2 - cdn) > 1e-3f * (fabsf(cdn2) + 1e-3f);
+                  atomicAdd(&g_fwd4_diag[0], 1u);
+                  if (acc_bad) atomicAdd(&g_fwd4_diag[1], 1u);
+                  if (tape_bad) atomicAdd(&g_fwd4_diag[2], 1u);
+                  if ((acc_bad || tape_bad) && atomicAdd(&g_fwd4_diag[3], 1u) < 24u)
+                    printf("fwd4-diag rb %d t %d wave %d lane %d row %d i %d acc_bad %d tape_bad %d hd %g/%g cdn %g/%g "
+                           "acc3 %g ig %g/%g\n", rb, t, wave, lane, 16 * m + 4 * g4 + i, i, (int)acc_bad, (int)tape_bad,
+                           hd, hd2, cdn, cdn2, al[3], ig, re0.get(m, i));
+                }
+#endif
                 cs[e + u] = cdn;
                 cprev[e + u] = cv;
                 cd2[u] = cdn; hd2[u] = hd;
@@ -1380,6 +1428,20 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 // ==========================================================================================
 // host side
 // ==========================================================================================
+// counters of the HFREP_FWD4_DIAG build (zeros otherwise): cells checked, accumulator / tape mismatches
+void lstm2_fwd4_diag(unsigned int out[4], bool reset) {
+#if HFREP_FWD4_DIAG
+  HFREP_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd4_diag), 4 * sizeof(unsigned int)));
+  if (reset) {
+    const unsigned int z[4] = {0, 0, 0, 0};
+    HFREP_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_fwd4_diag), z, sizeof(z)));
+  }
+#else
+  (void)reset;
+  for (int i = 0; i < 4; ++i) out[i] = 0;
+#endif
+}
+
 size_t lstm2_tape_elems(int B, int Tn) { return (size_t)((B + 31) / 32) * Tn * NW2 * TAPE_SLOTS * SLOT_ELEMS; }
 
 static size_t tfwd2_smem(int H, int K) {
@@ -1441,7 +1503,7 @@ static int lstm_dbg() {
   switch (act) {                                                                                 \
     case 0: launch(lstm_fwd4_kernel<100, 0, KXV, TP, TN>, __VA_ARGS__); break;                   \
     case 1:                                                                                      \
-      if constexpr (!TN) launch(lstm_fwd4_kernel<100, 1, KXV, TP, false>, __VA_ARGS__);          \
+      if constexpr (!TN || HFREP_TFWD4_SIGMOID) launch(lstm_fwd4_kernel<100, 1, KXV, TP, TN>, __VA_ARGS__); \
       break;                                                                                     \
     default: launch(lstm_fwd4_kernel<100, 2, KXV, TP, TN>, __VA_ARGS__); break;                  \
   }
@@ -1479,7 +1541,7 @@ void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const voi
                        int Tn, int K, int H, int act, hipStream_t s) {
   const bf16_t* xp = (const bf16_t*)xd;
   const int g = persistent_grid(B);
-  if (act == 1) {
+  if (act == 1 && !HFREP_TFWD4_SIGMOID) {
     // act = sigmoid: lstm_fwd4_kernel<.., TAN = true> differs run to run in rows 30 / 31 of a few row
     // blocks at B = 32772 (profiles/r03_race/README.md); the v2 tangent forward is bitwise there
     // (tests/test_kernels_gpu.py test_lstm2_tfwd_bitwise_large_batch).  Off the MTSS critic's path (tanh).
