@@ -702,6 +702,17 @@ std::tuple<Tensor, Tensor> gp_coef_pack(Tensor g, double weight, Tensor w) {
   return {pack, v};
 }
 
+// pack [w0 + w1 + weight pen, w0, w1, pen] from gp_coef's penalty and the W terms (gp_coef_pack's record)
+Tensor gp_pack(Tensor pen, double weight, Tensor w) {
+  CHECK_GPU(pen); GUARD(pen);
+  TORCH_CHECK(pen.scalar_type() == at::kFloat && pen.numel() == 1 && w.scalar_type() == at::kFloat && w.numel() == 2 &&
+              w.is_contiguous() && w.device() == pen.device(), "gp_pack: fp32 penalty [1] and W terms [2]");
+  Tensor pack = out_empty({4}, pen.options());
+  hfrep::launch_gp_pack(pen.data_ptr<float>(), w.data_ptr<float>(), (float)weight, pack.data_ptr<float>(),
+                        cur_stream(pen));
+  return pack;
+}
+
 // (segment losses [2] fp32, dL/dp like p): see csrc/misc.hip gan_loss_kernel
 std::tuple<Tensor, Tensor> gan_loss(Tensor p, int64_t split, double la, double lb, int64_t kind) {
   CHECK_GPU(p); GUARD(p);
@@ -940,6 +951,7 @@ TORCH_LIBRARY(hfrep, m) {
         "Tensor(a!) ggamma, Tensor(b!) gbeta, bool need_dx) -> (Tensor, Tensor)");
   m.def("gp_coef(Tensor g, float weight) -> (Tensor, Tensor)");
   m.def("gp_coef_pack(Tensor g, float weight, Tensor w) -> (Tensor, Tensor)");
+  m.def("gp_pack(Tensor pen, float weight, Tensor w) -> Tensor");
   m.def("gan_loss(Tensor p, int split, float la, float lb, int kind) -> (Tensor, Tensor)");
   m.def("im2col_causal(Tensor x, int k, int dil) -> Tensor");
   m.def("col2im_causal(Tensor dcols, int k, int dil, int C) -> Tensor");
@@ -998,6 +1010,7 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("layernorm_tbwd_", &layernorm_tbwd_);
   m.impl("gp_coef", &gp_coef);
   m.impl("gp_coef_pack", &gp_coef_pack);
+  m.impl("gp_pack", &gp_pack);
   m.impl("gan_loss", &gan_loss);
   m.impl("im2col_causal", &im2col_causal);
   m.impl("col2im_causal", &col2im_causal);

@@ -162,6 +162,7 @@ void launch_layernorm_tbwd(int dt, const void* dy, const void* dyd, const void* 
 void launch_gan_loss(int dt, const void* p, int64_t n, int64_t split, float la, float lb, int kind, void* grad,
                      float* partial, float* out, hipStream_t s);
 int gan_loss_partials();
+void launch_gp_pack(const float* pen, const float* w, float weight, float* pack, hipStream_t s);
 void launch_gp_coef(int dt, const void* g, void* v, float* pen, float* rowpen, int B, int64_t D, float weight,
                     hipStream_t s, const float* w = nullptr, float* pack = nullptr);
 void launch_interpolate(int dt, const void* real, const void* fake, const float* alpha, void* out, int B,

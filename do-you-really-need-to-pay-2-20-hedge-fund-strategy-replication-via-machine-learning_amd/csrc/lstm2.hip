@@ -1152,6 +1152,9 @@ struct XPart {
 #ifndef HFREP_FWD4_DIAG
 #define HFREP_FWD4_DIAG 0
 #endif
+#ifndef HFREP_FWD4_TAILNOP
+#define HFREP_FWD4_TAILNOP 0
+#endif
 #if HFREP_FWD4_DIAG
 __device__ unsigned int g_fwd4_diag[4];  // cells checked, accumulator mismatches, tape mismatches, printed
 __device__ __forceinline__ float late_read(float v) {  // a fresh VALU read of v's register, here
@@ -1298,6 +1301,13 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 #pragma unroll
               for (int q = 0; q < 4; ++q) acc[q][m] = mma16k16(ah4, uf4[q], acc[q][m]);
             }
+#if HFREP_FWD4_TAILNOP
+            // A/B of the act = sigmoid tangent-forward drift: nothing issues in the 8 wait states after
+            // the last tail MFMAs (the cell math overwrote their SrcC registers 3-4 instructions after issue)
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 7" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#endif
           }
         }
 #pragma unroll

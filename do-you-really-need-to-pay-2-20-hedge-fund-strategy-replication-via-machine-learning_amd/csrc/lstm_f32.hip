@@ -656,7 +656,7 @@ lstmf_bwdp_kernel(const float* __restrict__ dH, const float* __restrict__ tape, 
 // cdot_{t-1}, dH, dHd: 12 per cell): the set for the other half is issued right after a half's
 // cells, and lands while the MFMA waves finish the half-phase.
 #ifndef HFREP_TBWD_CELLGROUP
-#define HFREP_TBWD_CELLGROUP 1
+#define HFREP_TBWD_CELLGROUP 2
 #endif
 template <int ACT>
 __global__ void __launch_bounds__(512, 1)
@@ -851,8 +851,9 @@ lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, 
           }
           tc[m][n] = cp;
           tcd[m][n] = cdp;
-          // one cell's temporaries at a time (HFREP_TBWD_CELLGROUP > 1: that many cells per schedule
-          // region, an A/B knob for the cell role's instruction-level parallelism)
+          // HFREP_TBWD_CELLGROUP cells' temporaries per schedule region: 2 (13.80 -> 13.45 ms per call at
+          // B = 262 144; one cell at a time was the round-4 schedule, seven 13.56 ms:
+          // profiles/r05_tbwd/README.md)
           if ((n + 1) % HFREP_TBWD_CELLGROUP == 0 || n == FNT - 1) __builtin_amdgcn_sched_barrier(0);
         }
       };

@@ -577,6 +577,23 @@ __global__ void __launch_bounds__(1024) gp_sum_kernel(const float* __restrict__ 
   }
 }
 
+// the loss record pack [w0 + w1 + weight pen, w0, w1, pen] from an already reduced penalty: the same
+// arithmetic as gp_sum_kernel's pack (the concurrent small-batch critic step forms it after the join)
+__global__ void gp_pack_kernel(const float* __restrict__ pen, const float* __restrict__ w, float weight,
+                               float* __restrict__ pack) {
+  if (threadIdx.x == 0) {
+    const float s = pen[0];
+    pack[0] = w[0] + w[1] + weight * s;
+    pack[1] = w[0];
+    pack[2] = w[1];
+    pack[3] = s;
+  }
+}
+
+void launch_gp_pack(const float* pen, const float* w, float weight, float* pack, hipStream_t s) {
+  hipLaunchKernelGGL(gp_pack_kernel, dim3(1), dim3(64), 0, s, pen, w, weight, pack);
+}
+
 void launch_gp_coef(int dt, const void* g, void* v, float* pen, float* rowpen, int B, int64_t D, float weight,
                     hipStream_t s, const float* w, float* pack) {
   const int grid = (B + 3) / 4;

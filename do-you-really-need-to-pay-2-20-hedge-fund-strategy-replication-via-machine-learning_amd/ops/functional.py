@@ -256,6 +256,15 @@ def gp_coef_pack(g: torch.Tensor, weight: float, w: torch.Tensor):
     return torch.stack([w[0] + w[1] + weight * pen, w[0], w[1], pen]), v
 
 
+def gp_pack(pen: torch.Tensor, weight: float, w: torch.Tensor) -> torch.Tensor:
+    """gp_coef_pack's loss record [w0 + w1 + weight*pen, w0, w1, pen] from gp_coef's penalty (the same
+    arithmetic as the fused launch: the concurrent small-batch critic step forms it after its join)."""
+    if _nat(pen) and pen.dtype == torch.float32 and w.dtype == torch.float32:
+        return _ops().gp_pack(pen.reshape(1).contiguous(), float(weight), w.contiguous())
+    w = w.to(pen.dtype)
+    return torch.stack([w[0] + w[1] + weight * pen.reshape(()), w[0], w[1], pen.reshape(())])
+
+
 def interpolate(real: torch.Tensor, fake: torch.Tensor, alpha: torch.Tensor) -> torch.Tensor:
     """alpha (B,) per-sample: alpha*real + (1-alpha)*fake (GAN/MTSS_WGAN_GP.py:197-199)."""
     if _nat(real):

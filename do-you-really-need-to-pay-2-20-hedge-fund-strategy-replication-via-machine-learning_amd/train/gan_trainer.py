@@ -255,16 +255,19 @@ class GANTrainer:
             xrf = torch.cat([real, fake], 0)
         side = self._side(0)
         if side is not None:
-            # the gradient penalty's input-gradient chain (forward on x_hat, backward with wgrad off)
-            # shares nothing with the W-terms chain until gp_coef_pack: it runs on a side stream.  Every
-            # tensor it allocates lives until after the join below, and the side stream's next use
-            # starts with a fork from this stream, so no allocator block is reused across the streams
-            # while still in use.
+            # the gradient penalty's input-gradient chain (forward on x_hat, backward with wgrad off) and
+            # the tangent forward along v = dGP/dg write no gradient and share nothing with the W-terms
+            # chain: they run on a side stream; only the tangent reverse (whose weight gradient
+            # accumulates into C.flat.grad after the W terms') waits for the join.  Every tensor the side
+            # chain allocates lives until after the join, and the side stream's next use starts with a
+            # fork from this stream, so no allocator block is reused across the streams while in use.
             cur = torch.cuda.current_stream(self.device)
             side.wait_stream(cur)
             with torch.cuda.stream(side), trange("critic/gp_input_grad"):
                 sh, tape_h = C.efwd(xh, save=True)
                 g = C.ebwd(tape_h, self._ones(sh), need_dx=True, wgrad=False)
+                pen, v = Fn.gp_coef(g, self.gp_weight)
+                sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
         # W terms on [real; fake]
         with trange("critic/w_terms"):
             s, tape = C.efwd(xrf, save=True)
@@ -275,13 +278,16 @@ class GANTrainer:
             cur.wait_stream(side)
         # gradient penalty: g = dD/dx_hat (input gradient only), v = dGP/dg, then the
         # theta-gradient of <v, g> as reverse-over-tangent
-        with trange("critic/gp_input_grad"):
-            if side is None:
+        if side is None:
+            with trange("critic/gp_input_grad"):
                 sh, tape_h = C.efwd(xh, save=True)
                 g = C.ebwd(tape_h, self._ones(sh), need_dx=True, wgrad=False)
-            pack, v = Fn.gp_coef_pack(g, self.gp_weight, w)  # [total, W real, W fake, GP]
+                pack, v = Fn.gp_coef_pack(g, self.gp_weight, w)  # [total, W real, W fake, GP]
+            with trange("critic/gp_second_order"):
+                sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
+        else:
+            pack = Fn.gp_pack(pen, self.gp_weight, w)
         with trange("critic/gp_second_order"):
-            sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
             C.etbwd(tape_h, ttape, None, self._ones(sd), hook=self._hook(C))
         return pack.to(self._acc)
 
