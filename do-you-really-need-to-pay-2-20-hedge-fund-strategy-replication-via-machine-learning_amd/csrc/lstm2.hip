@@ -693,11 +693,14 @@ struct Slot8 {  // 8 bf16 of one 16x16-layout lane: block m = 0, 1 (rows 16 m + 
     return (i & 1) ? hi_bf(w) : lo_bf(w);
   }
 };
+#ifndef HFREP_SLOT8_AUX
+#define HFREP_SLOT8_AUX 0  // (race A/B knob: cache-policy bits of the primal-tape loads)
+#endif
 __device__ __forceinline__ Slot8 ld_slot8(rsrc_t rs, bool on, int lane_off, int uoff) {
   Slot8 s;
   const int v = on ? lane_off * 2 : kOOB;
-  s.m0 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, v, uoff * 2, 0));
-  s.m1 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, v, (uoff + SLOT_HALF) * 2, 0));
+  s.m0 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, v, uoff * 2, HFREP_SLOT8_AUX));
+  s.m1 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, v, (uoff + SLOT_HALF) * 2, HFREP_SLOT8_AUX));
   return s;
 }
 __device__ __forceinline__ f32x4 mma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
@@ -1062,6 +1065,12 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 // worse, stalled the compute waves at issue, so tape traffic and the recurrence did not overlap.
 // Lanes of padded units (unit >= H) get the out-of-range offset: no bytes written for them.
 constexpr int FW4_STAGE = NW2 * TAPE_SLOTS * SLOT_ELEMS;
+#ifndef HFREP_TAPE_STORE_AUX
+#define HFREP_TAPE_STORE_AUX 2  // (race A/B knob: the cache-policy bits of the tape stream, 2 = nt)
+#endif
+#ifndef HFREP_FWD4_DATA_VMWAIT
+#define HFREP_FWD4_DATA_VMWAIT 0  // (race A/B knob: the data wave waits for its stores at every step)
+#endif
 template <int H>
 __device__ __forceinline__ void tape_image_store(const bf16_t* img, rsrc_t rt, int t, bool on, int lane) {
   constexpr int NCH = FW4_STAGE / 512, G = 5;  // 1 KiB chunks, stored in groups of G
@@ -1082,7 +1091,7 @@ __device__ __forceinline__ void tape_image_store(const bf16_t* img, rsrc_t rt, i
       // forward 2.72 -> 2.55 ms, tangent 3.33 -> 3.03 ms at B = 262144; sc1 / sc0 sc1: no gain;
       // nt on the reverse kernels' dZ stores: BPTT +8 %; nt tape loads: tangent reverse +3-4 %.  profiles/archive_scripts/gpu_store_policy.sh,
       // profiles/archive_scripts/gpu_ab_lstm.sh, profiles/r01_fwd5/store_policy.jsonl)
-      __builtin_amdgcn_raw_buffer_store_b128(d[j], rt, ok ? base + ch * 1024 : kOOB, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128(d[j], rt, ok ? base + ch * 1024 : kOOB, 0, HFREP_TAPE_STORE_AUX);
     }
   }
 }
@@ -1418,6 +1427,9 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
         tile8_store_w<H>(hb + (t & 1) * 32 * LH, LH, rh, Tn, t - 1, t > 0 && !(dbg & 2), lane);
         if constexpr (TAPE)
           tape_image_store<H>(tsg + ((t + 1) & 1) * FW4_STAGE, rt, (dbg & 256) ? 0 : t - 1, t > 0 && ton, lane);
+#if HFREP_FWD4_DATA_VMWAIT
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         lds_barrier();
       }
       tile8_store_w<H>(hb + (Tn & 1) * 32 * LH, LH, rh, Tn, Tn - 1, true, lane);

@@ -40,6 +40,10 @@ for r in range(reps):
         dr = d[row]
         steps = dr.any(dim=1).nonzero().flatten().tolist()
         s0 = steps[0]
+        # per differing step: how many units differ and which 16-unit groups (compute wave of the unit)
+        per_step = {int(st): [int(dr[st].sum()), sorted(set((dr[st].nonzero().flatten() // 16).tolist()))]
+                    for st in steps}
+        print(json.dumps({"row": row, "per_step": per_step}), flush=True)
         units = dr[s0].nonzero().flatten().tolist()
         print(json.dumps({"row": row, "row_mod32": row % 32, "block": row // 32, "first_step": s0,
                           "units_at_first": units[:12], "n_units_at_first": len(units),

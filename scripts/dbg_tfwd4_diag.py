@@ -29,11 +29,14 @@ for act in (1, 2):
         hs, tape = Fn.lstm_layer_fwd(x, W, b, U, act, True)
         ops.fwd4_diag(True)
         t0 = Fn.lstm_layer_tfwd(xd, W, tape, U, act)
-        nd = []
+        nd, nprev = [], []
+        prev = t0
         for _ in range(reps):
             t1 = Fn.lstm_layer_tfwd(xd, W, tape, U, act)
             d = (t0[0].view(torch.int16) != t1[0].view(torch.int16))
             nd.append(int(d.sum().item()))
+            nprev.append(int((prev[0].view(torch.int16) != t1[0].view(torch.int16)).sum().item()))
+            prev = t1
             if nd[-1]:
                 idx = d.nonzero()
                 rows = sorted(set((idx[:, 0] % 32).tolist()))
@@ -42,5 +45,5 @@ for act in (1, 2):
                                   "steps": sorted(set(idx[:, 1].tolist()))[:12]}), flush=True)
         torch.cuda.synchronize()
         c = ops.fwd4_diag(True)
-        print(json.dumps({"act": act, "K": K, "B": B, "hd_ndiff_per_rep": nd, "diag_checked": c[0], "diag_acc_bad": c[1],
+        print(json.dumps({"act": act, "K": K, "B": B, "hd_ndiff_per_rep": nd, "hd_ndiff_vs_previous_rep": nprev, "diag_checked": c[0], "diag_acc_bad": c[1],
                           "diag_tape_bad": c[2], "lib": os.environ.get("HFREP_NATIVE_LIB", "default")}), flush=True)
