@@ -4,9 +4,9 @@ An MFMA reads its SrcA / SrcB at issue, but its SrcC (the accumulator input, 4 V
 16x16 tile) is read by the matrix pipe while the op is in flight.  A VALU / LDS-read / VMEM-load that
 OVERWRITES one of those SrcC registers a few instructions after the MFMA issued can land before the
 pipe has read it: the MFMA then accumulates onto the new value for the lanes / registers read last.
-This is the mechanism of the act = sigmoid bf16 tangent forward's run-to-run rows-30/31 drift
-(profiles/r03_race, profiles/r05_race/README.md): LLVM put 4 instructions between the last
-v_mfma_f32_16x16x16_bf16 of the step and the VALU writes of registers 2 / 3 of its SrcC.
+Written as a candidate for the act = sigmoid bf16 tangent forward's run-to-run rows-30/31 drift; the
+A/B refuted it there (profiles/r05_race/README.md: an s_nop 7 behind the tails keeps the drift, and the
+clean tanh instantiation has the same 3-4 wait-state pairs).  Kept as a census tool.
 
 For every MFMA this walks forward in straight-line code (stopping at labels and branches) and records
 the wait states (1 per instruction, N + 1 per s_nop N) before the first non-MFMA instruction that
