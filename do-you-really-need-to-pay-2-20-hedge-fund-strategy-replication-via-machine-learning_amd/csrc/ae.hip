@@ -1,6 +1,8 @@
 // Factor-autoencoder training in ONE launch (gfx950): the whole Keras `fit` of
 // Autoencoder_encapsulate.py:72-105 -- MSE loss, Nadam, batch 48, the last 25 % of rows as the
-// validation set, EarlyStopping(val_loss, patience) -- runs inside a single persistent workgroup.
+// validation set, EarlyStopping(val_loss, patience) -- runs inside one persistent workgroup, and a
+// launch carries any number of independent fits (one workgroup each: a whole latent sweep, or every
+// (seed, latent) pair of a study, trains side by side across the CUs).
 //
 // The model is tiny (22 -> k -> 22, no bias, k <= 21: <= 924 weights) and one epoch is 3 batches of
 // <= 48 rows, so the eager engine was launch-bound: ~15 kernel launches and a loss copy per batch
@@ -66,11 +68,24 @@ __device__ __forceinline__ void dense_lrelu(const float* x, int na, const float*
 
 template <bool BF>
 __global__ void __launch_bounds__(AE_THREADS, 1)
-ae_fit_kernel(const float* __restrict__ Xt, int nt, const float* __restrict__ Xv, int nv, const int* __restrict__ order,
-              int epochs, int batch, int patience, float* __restrict__ We, float* __restrict__ Wd, float* __restrict__ mWe,
-              float* __restrict__ vWe, float* __restrict__ mWd, float* __restrict__ vWd, float* __restrict__ step,
-              float* __restrict__ m_cache, float lr, float b1, float b2, float eps, int A, int k,
-              double* __restrict__ hist, int* __restrict__ nep) {
+ae_fit_kernel(const AeFitJob* __restrict__ jobs, int batch, float lr, float b1, float b2, float eps, int A) {
+  // one workgroup per fit: every (latent size, seed, panel) of a study trains side by side, each on
+  // its own CU (the fits are independent; their per-fit state lives in the job record)
+  const AeFitJob& J = jobs[blockIdx.x];
+  const float* __restrict__ Xt = J.Xt;
+  const float* __restrict__ Xv = J.Xv;
+  const int* __restrict__ order = J.order;
+  float* __restrict__ We = J.We;
+  float* __restrict__ Wd = J.Wd;
+  float* __restrict__ mWe = J.mWe;
+  float* __restrict__ vWe = J.vWe;
+  float* __restrict__ mWd = J.mWd;
+  float* __restrict__ vWd = J.vWd;
+  float* __restrict__ step = J.step;
+  float* __restrict__ m_cache = J.m_cache;
+  double* __restrict__ hist = J.hist;
+  int* __restrict__ nep = J.nep;
+  const int nt = J.nt, nv = J.nv, epochs = J.epochs, patience = J.patience, k = J.k;
   static_assert(AE_MAXK <= AE_MAXA, "zb / dzb share the activation tile size");
   __shared__ float xb[AE_MAXB * AE_MAXA], zb[AE_MAXB * AE_MAXK], yb[AE_MAXB * AE_MAXA];
   __shared__ float dyb[AE_MAXB * AE_MAXA], dzb[AE_MAXB * AE_MAXK];
@@ -207,16 +222,13 @@ bool ae_fit_supported(int A, int k, int batch) {
   return A >= 1 && A <= AE_MAXA && k >= 1 && k <= AE_MAXK && batch >= 1 && batch <= AE_MAXB;
 }
 
-void launch_ae_fit(bool bf16, const float* Xt, int nt, const float* Xv, int nv, const int* order, int epochs, int batch,
-                   int patience, float* We, float* Wd, float* mWe, float* vWe, float* mWd, float* vWd, float* step,
-                   float* m_cache, float lr, float b1, float b2, float eps, int A, int k, double* hist, int* nep,
+void launch_ae_fit(bool bf16, const AeFitJob* jobs, int njobs, int batch, float lr, float b1, float b2, float eps, int A,
                    hipStream_t s) {
+  if (njobs <= 0) return;
   if (bf16)
-    hipLaunchKernelGGL(ae_fit_kernel<true>, dim3(1), dim3(AE_THREADS), 0, s, Xt, nt, Xv, nv, order, epochs, batch,
-                       patience, We, Wd, mWe, vWe, mWd, vWd, step, m_cache, lr, b1, b2, eps, A, k, hist, nep);
+    hipLaunchKernelGGL(ae_fit_kernel<true>, dim3(njobs), dim3(AE_THREADS), 0, s, jobs, batch, lr, b1, b2, eps, A);
   else
-    hipLaunchKernelGGL(ae_fit_kernel<false>, dim3(1), dim3(AE_THREADS), 0, s, Xt, nt, Xv, nv, order, epochs, batch,
-                       patience, We, Wd, mWe, vWe, mWd, vWd, step, m_cache, lr, b1, b2, eps, A, k, hist, nep);
+    hipLaunchKernelGGL(ae_fit_kernel<false>, dim3(njobs), dim3(AE_THREADS), 0, s, jobs, batch, lr, b1, b2, eps, A);
 }
 
 }  // namespace hfrep

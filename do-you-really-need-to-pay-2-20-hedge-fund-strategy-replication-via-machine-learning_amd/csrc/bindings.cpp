@@ -15,6 +15,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 namespace {
 
@@ -773,31 +774,68 @@ Tensor sample_windows(Tensor data, int64_t batch, int64_t seed, Tensor ctr, at::
 // (train loss, val loss) history (epochs, 2) fp64 and the number of epochs run (int32 scalar tensor).
 bool ae_fit_supported(int64_t A, int64_t k, int64_t batch) { return hfrep::ae_fit_supported((int)A, (int)k, (int)batch); }
 
-std::tuple<Tensor, Tensor> ae_fit(Tensor Xt, Tensor Xv, Tensor order, Tensor We, Tensor Wd, Tensor mWe, Tensor vWe,
-                                  Tensor mWd, Tensor vWd, Tensor step, Tensor m_cache, double lr, double b1, double b2,
-                                  double eps, int64_t batch, int64_t patience, bool bf16) {
-  for (const Tensor* t : {&Xt, &Xv, &We, &Wd, &mWe, &vWe, &mWd, &vWd, &step, &m_cache}) {
-    CHECK_F32(*t);
-    TORCH_CHECK(t->is_contiguous() && t->device() == Xt.device(), "ae_fit: contiguous fp32 tensors on one device");
+// every fit of the lists trains in ONE launch (one workgroup per fit, csrc/ae.hip); shared: A (the
+// inputs' width), batch, the Nadam hyper-parameters and the dtype.  Returns hist (n, max epochs, 2)
+// fp64 and the epochs each fit ran (n,) int32.
+std::tuple<Tensor, Tensor> ae_fit(at::TensorList Xt, at::TensorList Xv, at::TensorList order, at::TensorList We,
+                                  at::TensorList Wd, at::TensorList mWe, at::TensorList vWe, at::TensorList mWd,
+                                  at::TensorList vWd, at::TensorList step, at::TensorList m_cache, at::IntArrayRef patience, double lr, double b1, double b2, double eps,
+                                  int64_t batch, bool bf16) {
+  const size_t n = Xt.size();
+  TORCH_CHECK(n >= 1, "ae_fit: at least one fit");
+  for (at::TensorList l : {Xv, order, We, Wd, mWe, vWe, mWd, vWd, step, m_cache})
+    TORCH_CHECK(l.size() == n, "ae_fit: every per-fit list needs ", n, " entries");
+  TORCH_CHECK(patience.size() == n, "ae_fit: one patience per fit");
+  const auto dev = Xt[0].device();
+  TORCH_CHECK(Xt[0].is_cuda() && Xt[0].dim() == 2, "ae_fit: Xt (nt, A) on the GPU");
+  const int A = Xt[0].size(1);
+  int max_ep = 0;
+  std::vector<hfrep::AeFitJob> jobs(n);
+  for (size_t i = 0; i < n; ++i) {
+    for (const Tensor* t : {&Xt[i], &Xv[i], &We[i], &Wd[i], &mWe[i], &vWe[i], &mWd[i], &vWd[i], &step[i], &m_cache[i]}) {
+      CHECK_F32(*t);
+      TORCH_CHECK(t->is_contiguous() && t->device() == dev, "ae_fit: contiguous fp32 tensors on one device");
+    }
+    const Tensor& o = order[i];
+    TORCH_CHECK(o.device() == dev && o.scalar_type() == at::kInt && o.is_contiguous() && o.dim() == 2,
+                "ae_fit: order must be a contiguous (epochs, nt) int32 tensor");
+    TORCH_CHECK(Xt[i].dim() == 2 && Xv[i].dim() == 2 && Xt[i].size(1) == A && Xv[i].size(1) == A,
+                "ae_fit: Xt (nt, A), Xv (nv, A) with one A for every fit");
+    const int nt = Xt[i].size(0), k = We[i].numel() / A, epochs = o.size(0);
+    TORCH_CHECK(o.size(1) == nt && nt > 0 && epochs > 0, "ae_fit: order shape");
+    TORCH_CHECK(We[i].numel() == (int64_t)A * k && Wd[i].numel() == We[i].numel() && mWe[i].numel() == We[i].numel() &&
+                    vWe[i].numel() == We[i].numel() && mWd[i].numel() == We[i].numel() && vWd[i].numel() == We[i].numel(),
+                "ae_fit: weight / slot sizes");
+    TORCH_CHECK(step[i].numel() == 1 && m_cache[i].numel() == 1, "ae_fit: scalar counters");
+    TORCH_CHECK(hfrep::ae_fit_supported(A, k, (int)batch) && patience[i] >= 1, "ae_fit: A, k <= 32 and batch <= 64");
+    max_ep = std::max(max_ep, epochs);
+    hfrep::AeFitJob& J = jobs[i];
+    J.Xt = Xt[i].data_ptr<float>();
+    J.Xv = Xv[i].data_ptr<float>();
+    J.order = o.data_ptr<int>();
+    J.We = We[i].data_ptr<float>(); J.Wd = Wd[i].data_ptr<float>();
+    J.mWe = mWe[i].data_ptr<float>(); J.vWe = vWe[i].data_ptr<float>();
+    J.mWd = mWd[i].data_ptr<float>(); J.vWd = vWd[i].data_ptr<float>();
+    J.step = step[i].data_ptr<float>(); J.m_cache = m_cache[i].data_ptr<float>();
+    J.nt = nt; J.nv = Xv[i].size(0); J.epochs = epochs; J.patience = (int)patience[i]; J.k = k; J.pad_ = 0;
   }
-  TORCH_CHECK(order.is_cuda() && order.device() == Xt.device() && order.scalar_type() == at::kInt && order.is_contiguous() &&
-                  order.dim() == 2, "ae_fit: order must be a contiguous (epochs, nt) int32 tensor");
-  TORCH_CHECK(Xt.dim() == 2 && Xv.dim() == 2 && Xv.size(1) == Xt.size(1), "ae_fit: Xt (nt, A), Xv (nv, A)");
-  const int nt = Xt.size(0), nv = Xv.size(0), A = Xt.size(1), k = We.numel() / A, epochs = order.size(0);
-  TORCH_CHECK(order.size(1) == nt && nt > 0 && epochs > 0, "ae_fit: order shape");
-  TORCH_CHECK(We.numel() == (int64_t)A * k && Wd.numel() == We.numel() && mWe.numel() == We.numel() &&
-                  vWe.numel() == We.numel() && mWd.numel() == We.numel() && vWd.numel() == We.numel(),
-              "ae_fit: weight / slot sizes");
-  TORCH_CHECK(step.numel() == 1 && m_cache.numel() == 1, "ae_fit: scalar counters");
-  TORCH_CHECK(hfrep::ae_fit_supported(A, k, (int)batch) && patience >= 1, "ae_fit: A, k <= 32 and batch <= 64");
-  GUARD(Xt);
-  Tensor hist = at::zeros({epochs, 2}, Xt.options().dtype(at::kDouble));
-  Tensor nep = at::zeros({1}, Xt.options().dtype(at::kInt));
-  hfrep::launch_ae_fit(bf16, Xt.data_ptr<float>(), nt, Xv.data_ptr<float>(), nv, order.data_ptr<int>(), epochs, (int)batch,
-                       (int)patience, We.data_ptr<float>(), Wd.data_ptr<float>(), mWe.data_ptr<float>(), vWe.data_ptr<float>(),
-                       mWd.data_ptr<float>(), vWd.data_ptr<float>(), step.data_ptr<float>(), m_cache.data_ptr<float>(),
-                       (float)lr, (float)b1, (float)b2, (float)eps, A, k, hist.data_ptr<double>(), nep.data_ptr<int>(),
-                       cur_stream(Xt));
+  GUARD(Xt[0]);
+  const auto fopt = Xt[0].options();
+  Tensor hist = at::zeros({(int64_t)n, max_ep, 2}, fopt.dtype(at::kDouble));
+  Tensor nep = at::zeros({(int64_t)n}, fopt.dtype(at::kInt));
+  for (size_t i = 0; i < n; ++i) {
+    jobs[i].hist = hist.data_ptr<double>() + i * (size_t)max_ep * 2;
+    jobs[i].nep = nep.data_ptr<int>() + i;
+  }
+  // the job records: host bytes -> device (ordered on the current stream before the launch)
+  const int64_t bytes = (int64_t)(n * sizeof(hfrep::AeFitJob));
+  Tensor host = at::empty({bytes}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(host.data_ptr(), jobs.data(), bytes);
+  Tensor dj = host.to(dev);
+  hfrep::launch_ae_fit(bf16, reinterpret_cast<const hfrep::AeFitJob*>(dj.data_ptr()), (int)n, (int)batch, (float)lr,
+                       (float)b1, (float)b2, (float)eps, A, cur_stream(Xt[0]));
+  const hipError_t err = hipGetLastError();
+  TORCH_CHECK(err == hipSuccess, "ae_fit: launch failed: ", hipGetErrorString(err));
   return {hist, nep};
 }
 
@@ -959,9 +997,9 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("philox_fill_(Tensor(a!) out, int seed, Tensor(b!) ctr, int dist) -> ()");
   m.def("sample_windows(Tensor data, int batch, int seed, Tensor(a!) ctr, ScalarType out_dtype, Tensor(b!)? dst=None) -> Tensor");
   m.def("ae_fit_supported(int A, int k, int batch) -> bool", &ae_fit_supported);  // no tensor inputs: catch-all kernel
-  m.def("ae_fit(Tensor Xt, Tensor Xv, Tensor order, Tensor(a!) We, Tensor(b!) Wd, Tensor(c!) mWe, Tensor(d!) vWe, "
-        "Tensor(e!) mWd, Tensor(f!) vWd, Tensor(g!) step, Tensor(h!) m_cache, float lr, float b1, float b2, float eps, "
-        "int batch, int patience, bool bf16) -> (Tensor, Tensor)");
+  m.def("ae_fit(Tensor[] Xt, Tensor[] Xv, Tensor[] order, Tensor(a!)[] We, Tensor(b!)[] Wd, Tensor(c!)[] mWe, "
+        "Tensor(d!)[] vWe, Tensor(e!)[] mWd, Tensor(f!)[] vWd, Tensor(g!)[] step, Tensor(h!)[] m_cache, int[] patience, "
+        "float lr, float b1, float b2, float eps, int batch, bool bf16) -> (Tensor, Tensor)");
   m.def("rmsprop_(Tensor(a!) p, Tensor g, Tensor(b!) ms, float lr, float rho, float eps, float clip, float gscale) -> ()");
   m.def("adam_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, float lr, float b1, float b2, float eps, float clip, float gscale) -> ()");
   m.def("nadam_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, Tensor m_cache, float lr, float b1, float b2, float eps, float gscale) -> ()");

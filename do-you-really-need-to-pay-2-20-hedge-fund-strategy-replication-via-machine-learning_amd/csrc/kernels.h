@@ -79,9 +79,19 @@ void launch_fp3_join(const uint16_t* p, float* x, int64_t M, int C, bool interle
 
 // ---- ae.hip (factor autoencoder: the whole Keras fit -- MSE, Nadam, EarlyStopping -- in one launch) ----
 bool ae_fit_supported(int A, int k, int batch);
-void launch_ae_fit(bool bf16, const float* Xt, int nt, const float* Xv, int nv, const int* order, int epochs, int batch,
-                   int patience, float* We, float* Wd, float* mWe, float* vWe, float* mWd, float* vWd, float* step,
-                   float* m_cache, float lr, float b1, float b2, float eps, int A, int k, double* hist, int* nep,
+// one independent fit: its data, batch orders (epochs, nt), weights (A x k), Nadam slots and shared
+// counters, and the per-epoch (loss, val_loss) history + epochs-run outputs
+struct AeFitJob {
+  const float* Xt;
+  const float* Xv;
+  const int* order;
+  float *We, *Wd, *mWe, *vWe, *mWd, *vWd, *step, *m_cache;
+  double* hist;
+  int* nep;
+  int nt, nv, epochs, patience, k, pad_;
+};
+// `jobs` is a device array of njobs records (one workgroup each)
+void launch_ae_fit(bool bf16, const AeFitJob* jobs, int njobs, int batch, float lr, float b1, float b2, float eps, int A,
                    hipStream_t s);
 
 // ---- gemm.hip ----

@@ -120,28 +120,58 @@ class AETrainer:
 
     @torch.no_grad()
     def _fit_fused(self, x, split, epochs, batch_size, patience, shuffle, rs, dtype, verbose):
+        return fit_fused_many([self._fused_job(x, split, epochs, patience, shuffle, rs)], batch_size, dtype,
+                              verbose)[0]
+
+    def _fused_job(self, x, split, epochs, patience, shuffle, rs):
+        """One fit's operands for csrc/ae.hip: row-major fp32 train / validation rows, the epochs' batch
+        permutations (drawn up front from the fit's numpy stream, the eager trainer's draws), the
+        weights and Nadam slots (updated in place) and the shared counters."""
         n, A = x.shape
         enc, dec = self.model.parts()
-        k = self.model.latent_dim
+        nw = A * self.model.latent_dim
         orders = np.stack([rs.permutation(split) if shuffle else np.arange(split) for _ in range(epochs)])
         dev = self.device
         # row-major copies: the scaler's output can be column-major (MinMaxScaler keeps Fortran order)
         xt = torch.as_tensor(np.ascontiguousarray(x[:split]), dtype=torch.float32, device=dev).contiguous()
         xv = torch.as_tensor(np.ascontiguousarray(x[split:]), dtype=torch.float32, device=dev).reshape(-1, A).contiguous()
-        order_t = torch.as_tensor(orders.astype(np.int32), device=dev)
-        nw = A * k
         (mWe, vWe), (mWd, vWd) = self.opt._slots(enc.flat), self.opt._slots(dec.flat)
-        hist_t, nep_t = _native.native().ae_fit(
-            xt, xv, order_t, enc.flat.data[:nw], dec.flat.data[:nw], mWe[:nw], vWe[:nw], mWd[:nw], vWd[:nw],
-            self.opt.iterations, self.opt.m_cache, self.opt.lr, self.opt.b1, self.opt.b2, self.opt.eps, batch_size,
-            patience if split < n else epochs + 1, dtype == torch.bfloat16)
-        ne = int(nep_t.item())
-        h = hist_t[:ne].cpu().numpy()
-        hist = {"loss": h[:, 0].tolist(), "val_loss": h[:, 1].tolist() if split < n else []}
+        return dict(trainer=self, Xt=xt, Xv=xv, order=torch.as_tensor(orders.astype(np.int32), device=dev),
+                    We=enc.flat.data[:nw], Wd=dec.flat.data[:nw], mWe=mWe[:nw], vWe=vWe[:nw], mWd=mWd[:nw],
+                    vWd=vWd[:nw], step=self.opt.iterations, m_cache=self.opt.m_cache,
+                    patience=patience if split < n else epochs + 1, has_val=split < n)
+
+
+@torch.no_grad()
+def fit_fused_many(jobs: list, batch_size: int, dtype, verbose: int = 0) -> list:
+    """Train every job (``AETrainer._fused_job`` records) in ONE launch of csrc/ae.hip: one workgroup per
+    fit, so a latent sweep (21 fits) or a multi-seed study (hundreds) trains side by side across the
+    CUs instead of one single-workgroup launch after another.  The fits share the input width, batch
+    size, dtype and the Nadam hyper-parameters (every trainer's optimizer must agree).  Returns one
+    Keras-style history dict per job."""
+    if not jobs:
+        return []
+    o0 = jobs[0]["trainer"].opt
+    for j in jobs:
+        o = j["trainer"].opt
+        if (o.lr, o.b1, o.b2, o.eps) != (o0.lr, o0.b1, o0.b2, o0.eps):
+            raise ValueError("fit_fused_many: every fit must use the same Nadam hyper-parameters")
+    L = lambda key: [j[key] for j in jobs]  # noqa: E731
+    hist_t, nep_t = _native.native().ae_fit(
+        L("Xt"), L("Xv"), L("order"), L("We"), L("Wd"), L("mWe"), L("vWe"), L("mWd"), L("vWd"), L("step"),
+        L("m_cache"), [int(j["patience"]) for j in jobs], o0.lr, o0.b1, o0.b2, o0.eps, batch_size,
+        dtype == torch.bfloat16)
+    nep = nep_t.cpu().tolist()
+    hall = hist_t.cpu().numpy()
+    out = []
+    for i, j in enumerate(jobs):
+        h = hall[i, :nep[i]]
+        hist = {"loss": h[:, 0].tolist(), "val_loss": h[:, 1].tolist() if j["has_val"] else []}
         if verbose:
-            for ep in range(ne):
+            for ep in range(nep[i]):
                 print(f"epoch {ep + 1}: loss {h[ep, 0]:.6f} val_loss {h[ep, 1]:.6f}")
-        return hist
+        out.append(hist)
+    return out
 
 
 # ------------------------------------------------------------------------------------------
@@ -171,25 +201,60 @@ class AE:
         self._ante = self._post = None
 
     # -- training ------------------------------------------------------------------------------
-    def train(self, patience=5, verbose=2, plot=True):
+    def _new_trainer(self) -> AETrainer:
         self.autoencoder = FactorAutoencoder(self._latent_dim, self._x_train.shape[1], seed=self.seed, dtype=torch.float32,
                                              device=self.device)
-        tr = AETrainer(self.autoencoder, device=self.device)
+        return AETrainer(self.autoencoder, device=self.device)
+
+    def train(self, patience=5, verbose=2, plot=True):
+        tr = self._new_trainer()
         self.history = tr.fit(self._x_train, epochs=1000, batch_size=48, validation_split=0.25, patience=patience,
                               seed=self.seed, dtype=self.dtype, verbose=1 if verbose == 1 else 0)
         if plot:
-            import matplotlib.pyplot as plt
-
-            print(self.autoencoder.encoder.summary())
-            print(self.autoencoder.decoder.summary())
-            plt.plot(self.history["loss"])
-            plt.plot(self.history["val_loss"])
-            plt.title("Model Loss")
-            plt.ylabel("loss")
-            plt.xlabel("epoch")
-            plt.legend(["train", "val"], loc="upper left")
-            plt.show()
+            self.plot_history()
         return self.history
+
+    def plot_history(self):
+        import matplotlib.pyplot as plt
+
+        print(self.autoencoder.encoder.summary())
+        print(self.autoencoder.decoder.summary())
+        plt.plot(self.history["loss"])
+        plt.plot(self.history["val_loss"])
+        plt.title("Model Loss")
+        plt.ylabel("loss")
+        plt.xlabel("epoch")
+        plt.legend(["train", "val"], loc="upper left")
+        plt.show()
+
+    @staticmethod
+    def train_many(aes: list, patience: int = 5) -> list:
+        """``ae.train(patience, plot=False)`` for every AE, the same fits and results; on a native GPU
+        build all of them (any latent sizes, seeds and panels with one input width and dtype) train in
+        ONE launch, one workgroup per fit (``fit_fused_many``).  Otherwise they train one by one."""
+        if not aes:
+            return []
+        a0 = aes[0]
+        A = a0._x_train.shape[1]
+        batched = (all(a.device.type == "cuda" and a.device == a0.device and a.dtype == a0.dtype
+                       and a._x_train.shape[1] == A for a in aes)
+                   and a0.dtype in (torch.float32, torch.bfloat16)
+                   and all(bool(_native.native().ae_fit_supported(A, a._latent_dim, 48)) for a in aes))
+        if batched:
+            jobs = []
+            for a in aes:
+                tr = a._new_trainer()
+                if not _native.use_native_for(a.autoencoder.parts()[0].flat):
+                    batched = False
+                    break
+                x = np.asarray(a._x_train, dtype=np.float64)
+                split = int(len(x) * 0.75)
+                jobs.append(tr._fused_job(x, split, 1000, patience, True, np.random.RandomState(a.seed)))
+        if not batched:
+            return [a.train(patience=patience, verbose=0, plot=False) for a in aes]
+        for a, h in zip(aes, fit_fused_many(jobs, 48, a0.dtype)):
+            a.history = h
+        return [a.history for a in aes]
 
     def _predict(self, x) -> np.ndarray:
         xt = torch.as_tensor(np.asarray(x, dtype=np.float64), dtype=self.dtype, device=self.device)

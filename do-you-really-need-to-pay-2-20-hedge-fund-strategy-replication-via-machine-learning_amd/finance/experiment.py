@@ -51,40 +51,62 @@ def latent_sweep(cleaned: dict, latents=range(1, 22), window: int = 24, frac: fl
     ``x_extra`` / ``y_extra``: extra (generated) training rows appended to the real training rows
     (the augmented study); the test period is always real data.  ``device`` / ``dtype``: where and
     in which compute dtype the autoencoders train and predict (fp32 on the CPU by default; ``cuda``
-    runs the engine's native Dense / optimizer kernels, BASELINE config 2).
+    runs the engine's native Dense / optimizer kernels, BASELINE config 2).  On the GPU the sweep's
+    fits train in one launch (``AE.train_many``).
     """
+    return latent_sweep_many(cleaned, seeds=[seed], latents=latents, window=window, frac=frac,
+                             x_extras=[x_extra], y_extras=[y_extra], device=device, verbose=verbose, dtype=dtype)[0]
+
+
+def latent_sweep_many(cleaned: dict, seeds, latents=range(1, 22), window: int = 24, frac: float = 0.5,
+                      x_extras=None, y_extras=None, device="cpu", verbose: bool = False, dtype=None) -> list:
+    """``latent_sweep`` for several seeds (``x_extras[i]`` / ``y_extras[i]``: seed i's extra rows or None):
+    every (seed, latent) autoencoder is built first and all of them train together (one csrc/ae.hip
+    launch on a native GPU build), then each is evaluated.  Returns one SweepResult per seed."""
+    seeds = list(seeds)
+    latents = list(latents)
+    x_extras = list(x_extras) if x_extras is not None else [None] * len(seeds)
+    y_extras = list(y_extras) if y_extras is not None else [None] * len(seeds)
     x_tr, y_tr, x_te, y_te = chronological_split(cleaned, frac)
-    xtr, ytr = x_tr.to_numpy(), y_tr.to_numpy()
-    if x_extra is not None:
-        xtr = np.vstack([xtr, x_extra])
-        ytr = np.vstack([ytr, y_extra])
     rf = cleaned["rf"]
     names = cleaned.get("hfd_fullname", {c: c for c in y_te.columns})
-    rows, s_ante, s_post, turns, posts = [], [], [], [], []
-    for k in latents:
-        ae = AE(xtr, ytr, x_te, y_te, k, device=device, seed=seed, **({"dtype": dtype} if dtype is not None else {}))
-        ae.train(verbose=0, plot=False)
-        oos_r2, oos_rmse = ae.model_OOS_r2(), ae.model_OOS_RMSE()
-        rows.append({"latent": k, "IS_r2": float(ae.model_IS_r2()), "IS_RMSE": float(ae.model_IS_RMSE()),
-                     "OOS_r2": float(np.mean(oos_r2)), "OOS_RMSE": float(np.mean(oos_rmse))})
-        ante = ae.ante(rf.iloc[-len(y_te):], y_te, window=window)
-        post = ae.post(cleaned["factor_etf_data"])
-        to = ae.turnover(names)
-        rf_slice = pd.DataFrame(np.asarray(rf.iloc[-len(post):], dtype=np.float64)[:, :1], index=post.index)
-        s_ante.append({c: float(analytics.annualized_sharpe_ratio(ante[c], rf_slice)) for c in ante.columns})
-        s_post.append({c: float(analytics.annualized_sharpe_ratio(post[c], rf_slice)) for c in post.columns})
-        turns.append(dict(zip(post.columns, to["Turnover"].to_numpy())))
-        posts.append(pd.DataFrame({"Annualized_Sharpe": [s_post[-1][c] for c in post.columns]},
-                                  index=list(post.columns)))
-        if verbose:
-            print(f"latent {k}: {rows[-1]}")
-    idx = pd.Index(list(latents), name="latent")
-    best, bidx = analytics.res_sort(posts)
-    best["latent"] = [b + 1 for b in bidx] if list(latents) == list(range(1, len(posts) + 1)) else \
-        [list(latents)[b] for b in bidx]
-    return SweepResult(metrics=pd.DataFrame(rows).set_index("latent"), sharpe_ante=pd.DataFrame(s_ante, index=idx),
-                       sharpe_post=pd.DataFrame(s_post, index=idx), turnover=pd.DataFrame(turns, index=idx),
-                       best=best, post_tables=posts)
+    aes = []
+    for s, xe, ye in zip(seeds, x_extras, y_extras):
+        xtr, ytr = x_tr.to_numpy(), y_tr.to_numpy()
+        if xe is not None:
+            xtr = np.vstack([xtr, xe])
+            ytr = np.vstack([ytr, ye])
+        for k in latents:
+            aes.append(AE(xtr, ytr, x_te, y_te, k, device=device, seed=s,
+                          **({"dtype": dtype} if dtype is not None else {})))
+    AE.train_many(aes)
+    out = []
+    for si in range(len(seeds)):
+        rows, s_ante, s_post, turns, posts = [], [], [], [], []
+        for ki, k in enumerate(latents):
+            ae = aes[si * len(latents) + ki]
+            oos_r2, oos_rmse = ae.model_OOS_r2(), ae.model_OOS_RMSE()
+            rows.append({"latent": k, "IS_r2": float(ae.model_IS_r2()), "IS_RMSE": float(ae.model_IS_RMSE()),
+                         "OOS_r2": float(np.mean(oos_r2)), "OOS_RMSE": float(np.mean(oos_rmse))})
+            ante = ae.ante(rf.iloc[-len(y_te):], y_te, window=window)
+            post = ae.post(cleaned["factor_etf_data"])
+            to = ae.turnover(names)
+            rf_slice = pd.DataFrame(np.asarray(rf.iloc[-len(post):], dtype=np.float64)[:, :1], index=post.index)
+            s_ante.append({c: float(analytics.annualized_sharpe_ratio(ante[c], rf_slice)) for c in ante.columns})
+            s_post.append({c: float(analytics.annualized_sharpe_ratio(post[c], rf_slice)) for c in post.columns})
+            turns.append(dict(zip(post.columns, to["Turnover"].to_numpy())))
+            posts.append(pd.DataFrame({"Annualized_Sharpe": [s_post[-1][c] for c in post.columns]},
+                                      index=list(post.columns)))
+            if verbose:
+                print(f"seed {seeds[si]} latent {k}: {rows[-1]}")
+        idx = pd.Index(latents, name="latent")
+        best, bidx = analytics.res_sort(posts)
+        best["latent"] = [b + 1 for b in bidx] if latents == list(range(1, len(posts) + 1)) else \
+            [latents[b] for b in bidx]
+        out.append(SweepResult(metrics=pd.DataFrame(rows).set_index("latent"),
+                               sharpe_ante=pd.DataFrame(s_ante, index=idx), sharpe_post=pd.DataFrame(s_post, index=idx),
+                               turnover=pd.DataFrame(turns, index=idx), best=best, post_tables=posts))
+    return out
 
 
 def generated_augmentation(generated: np.ndarray, cleaned: dict, split_pos: int = 22, include_rf: bool = True):

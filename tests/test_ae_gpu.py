@@ -84,3 +84,28 @@ def test_ae_fused_fit_early_stopping(cuda):
     for a, b in zip(m1.parts(), m2.parts()):
         rel = ((a.flat - b.flat).norm() / b.flat.norm()).item()
         assert rel < 1e-4, rel
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_ae_train_many_matches_one_by_one(cuda, cleaned, dt):
+    """AE.train_many trains every fit in ONE csrc/ae.hip launch (one workgroup per fit): for a mix of
+    latent sizes, seeds and training panels (different row counts) the histories, epochs run and
+    weights equal the one-launch-per-fit path bitwise (each workgroup runs the same fixed-order code)."""
+    etf, hfd = cleaned["factor_etf_data"].to_numpy(), cleaned["hfd"].to_numpy()
+    half = len(hfd) // 2
+    rs = np.random.RandomState(0)
+    xa = np.vstack([etf[:half], rs.rand(40, etf.shape[1]) * 0.1])  # an "augmented" panel: more rows
+    ya = np.vstack([hfd[:half], rs.rand(40, hfd.shape[1]) * 0.1])
+    specs = [(etf[:half], hfd[:half], 1, 3), (etf[:half], hfd[:half], 7, 3), (xa, ya, 4, 11), (etf[:half], hfd[:half], 21, 5)]
+
+    def make():
+        return [AE(x, y, etf[half:], hfd[half:], k, device=cuda, dtype=dt, seed=s) for x, y, k, s in specs]
+
+    many, single = make(), make()
+    AE.train_many(many)
+    for a in single:
+        a.train(verbose=0, plot=False)
+    for a, b in zip(many, single):
+        assert a.history["loss"] == b.history["loss"] and a.history["val_loss"] == b.history["val_loss"]
+        for pa, pb in zip(a.autoencoder.parts(), b.autoencoder.parts()):
+            assert torch.equal(pa.flat, pb.flat)
