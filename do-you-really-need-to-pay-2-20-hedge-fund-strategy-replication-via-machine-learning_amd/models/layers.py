@@ -139,7 +139,7 @@ class Dense(Layer):
     def ebwd(self, ctx, dy, need_dx, wgrad=True):
         dz = Fn.act_backward(dy, ctx["y"], self.act_code)
         if wgrad:
-            Fn.linear_wgrad_(ctx["x"], dz, self.g("kernel"), self.g("bias") if self.use_bias else None)
+            Fn.run_wgrad(Fn.linear_wgrad_, ctx["x"], dz, self.g("kernel"), self.g("bias") if self.use_bias else None)
         return self._dgrad(dz) if need_dx else None
 
     def etfwd(self, ctx, xd):
@@ -154,8 +154,8 @@ class Dense(Layer):
         zero_dz = dy is None and self.act_code in (0, 3, 4)
         if not zero_dz:
             dz = Fn.act_tangent_backward(dy, dyd, ctx["y"], tctx["zd"], self.act_code)
-            Fn.linear_wgrad_(ctx["x"], dz, self.g("kernel"), self.g("bias") if self.use_bias else None)
-        Fn.linear_wgrad_(tctx["xd"], dzd, self.g("kernel"), None)
+            Fn.run_wgrad(Fn.linear_wgrad_, ctx["x"], dz, self.g("kernel"), self.g("bias") if self.use_bias else None)
+        Fn.run_wgrad(Fn.linear_wgrad_, tctx["xd"], dzd, self.g("kernel"), None)
         if not need_dx:
             return None, None
         return (None if zero_dz else self._dgrad(dz)), self._dgrad(dzd)
@@ -197,7 +197,7 @@ class LSTM(Layer):
         else:
             dZ = Fn.lstm_layer_bwd(dy, ctx["tape"], U, self.act_code)
         if wgrad:
-            Fn.lstm_wgrad_(ctx["x"], ctx["hs"], dZ, self.g("kernel"), self.g("recurrent_kernel"), self.g("bias"))
+            Fn.run_wgrad(Fn.lstm_wgrad_, ctx["x"], ctx["hs"], dZ, self.g("kernel"), self.g("recurrent_kernel"), self.g("bias"))
         return dx
 
     def etfwd(self, ctx, xd):
@@ -212,7 +212,7 @@ class LSTM(Layer):
                                                   W=self.p("kernel"))
         else:
             dZ, dZd = Fn.lstm_layer_tbwd(dy, dyd, ctx["tape"], tctx["ttape"], U, self.act_code)
-        Fn.lstm_wgrad_(ctx["x"], ctx["hs"], dZ, self.g("kernel"), self.g("recurrent_kernel"), self.g("bias"),
+        Fn.run_wgrad(Fn.lstm_wgrad_, ctx["x"], ctx["hs"], dZ, self.g("kernel"), self.g("recurrent_kernel"), self.g("bias"),
                        tctx["xd"], tctx["hds"], dZd)
         return dx, dxd
 
@@ -343,7 +343,7 @@ class Conv1D(Layer):
     def ebwd(self, ctx, dy, need_dx, wgrad=True):
         dz = Fn.act_backward(dy, ctx["y"], self.act_code)
         if wgrad:
-            Fn.linear_wgrad_(ctx["cols"], dz, self.g("kernel").reshape(-1, self.filters), self.g("bias"))
+            Fn.run_wgrad(Fn.linear_wgrad_, ctx["cols"], dz, self.g("kernel").reshape(-1, self.filters), self.g("bias"))
         if not need_dx:
             return None
         dcols = Fn.linear_dgrad(dz, self.p("kernel").reshape(-1, self.filters))
@@ -361,8 +361,8 @@ class Conv1D(Layer):
             dy = torch.zeros_like(ctx["y"])
         dzd = Fn.act_backward(dyd, ctx["y"], self.act_code)
         dz = Fn.act_tangent_backward(dy, dyd, ctx["y"], tctx["zd"], self.act_code)
-        Fn.linear_wgrad_(ctx["cols"], dz, gk, self.g("bias"))
-        Fn.linear_wgrad_(tctx["cols_d"], dzd, gk, None)
+        Fn.run_wgrad(Fn.linear_wgrad_, ctx["cols"], dz, gk, self.g("bias"))
+        Fn.run_wgrad(Fn.linear_wgrad_, tctx["cols_d"], dzd, gk, None)
         if not need_dx:
             return None, None
         return (Fn.col2im_causal(Fn.linear_dgrad(dz, Wk), self.k, self.dil, self.cin),

@@ -10,6 +10,7 @@ dtype of the explicit engine); gradients are always fp32.
 """
 from __future__ import annotations
 
+import contextlib
 
 import torch
 
@@ -27,6 +28,47 @@ def _ops():
 
 def _2d(x: torch.Tensor) -> torch.Tensor:
     return x.reshape(-1, x.shape[-1])
+
+
+# ---------------------------------------------------------------------------------------
+# weight gradients off the reverse pass's critical path
+# ---------------------------------------------------------------------------------------
+class _WgradDefer:
+    stream = None  # the side stream weight-gradient launches go to (None: inline)
+    keep: list = []  # operands of the deferred launches, alive until the join
+
+
+@contextlib.contextmanager
+def wgrad_on(stream):
+    """Inside the block every layer's weight-gradient launch (:func:`run_wgrad`) runs on ``stream``,
+    after everything issued so far on the current stream, while the current stream goes on with the
+    next layer's backward; at the end the current stream waits for ``stream``.  The launches keep
+    their order on the one side stream, so every gradient accumulates in the sequential order (bitwise
+    the same result).  Their operands stay referenced until the join, so the caching allocator never
+    hands their blocks to the current stream while the side stream still reads them.  ``stream`` None:
+    a no-op (the launches run inline)."""
+    if stream is None or _WgradDefer.stream is not None:
+        yield
+        return
+    cur = torch.cuda.current_stream(stream.device)
+    _WgradDefer.stream, _WgradDefer.keep = stream, []
+    try:
+        yield
+    finally:
+        _WgradDefer.stream = None
+        cur.wait_stream(stream)
+        _WgradDefer.keep = []
+
+
+def run_wgrad(fn, *args, **kw):
+    """``fn(*args, **kw)`` (a weight-gradient launch), on the :func:`wgrad_on` stream when one is set."""
+    s = _WgradDefer.stream
+    if s is None:
+        return fn(*args, **kw)
+    s.wait_stream(torch.cuda.current_stream(s.device))
+    with torch.cuda.stream(s):
+        fn(*args, **kw)
+    _WgradDefer.keep.append((args, kw))
 
 
 # ---------------------------------------------------------------------------------------

@@ -27,6 +27,7 @@ MI355X-first differences (semantics preserved):
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -133,13 +134,22 @@ class GANTrainer:
         return cfg.batch_size <= 2048
 
     def _side(self, i: int):
-        """Side stream ``i`` (0: the gradient-penalty input-gradient chain, 1: the next generator forward),
-        or None when running sequentially."""
+        """Side stream ``i`` (0: the gradient-penalty input-gradient chain, 1: the next generator forward,
+        2: the layers' weight gradients, off the reverse pass's critical path), or None when running
+        sequentially."""
         if not self.concurrent:
             return None
         if self._streams is None:
-            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(2)]
+            self._streams = [torch.cuda.Stream(device=self.device) for _ in range(3)]
         return self._streams[i]
+
+    def _wgrad_side(self, hook):
+        """Stream for the layers' weight gradients (``Fn.wgrad_on``): side stream 2 when concurrent and no
+        per-layer all-reduce hook needs final gradients layer by layer; ``HFREP_WGRAD_SIDE=0`` keeps
+        them inline (A/B)."""
+        if hook is not None or os.environ.get("HFREP_WGRAD_SIDE", "1") == "0":
+            return None
+        return self._side(2)
 
     def _batch(self, B, out=None):
         real = self.rng.sample_windows(self.dataset, B, out_dtype=self.dtype, out=out)
@@ -268,27 +278,31 @@ class GANTrainer:
                 g = C.ebwd(tape_h, self._ones(sh), need_dx=True, wgrad=False)
                 pen, v = Fn.gp_coef(g, self.gp_weight)
                 sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
-        # W terms on [real; fake]
-        with trange("critic/w_terms"):
-            s, tape = C.efwd(xrf, save=True)
-            # W(real, -1) and W(fake, +1): both segment means and the score gradient in one launch
-            w, ds = Fn.gan_loss(s, s.numel() // 2, -1.0, 1.0, 0)
-            C.ebwd(tape, ds)
-        if side is not None:
-            cur.wait_stream(side)
-        # gradient penalty: g = dD/dx_hat (input gradient only), v = dGP/dg, then the
-        # theta-gradient of <v, g> as reverse-over-tangent
-        if side is None:
-            with trange("critic/gp_input_grad"):
-                sh, tape_h = C.efwd(xh, save=True)
-                g = C.ebwd(tape_h, self._ones(sh), need_dx=True, wgrad=False)
-                pack, v = Fn.gp_coef_pack(g, self.gp_weight, w)  # [total, W real, W fake, GP]
+        hook = self._hook(C)
+        # (concurrent, no per-layer all-reduce hook: every layer's weight gradient runs on side stream
+        # 2 beside the next layer's backward, in the sequential order; joined before the return)
+        with Fn.wgrad_on(self._wgrad_side(hook)):
+            # W terms on [real; fake]
+            with trange("critic/w_terms"):
+                s, tape = C.efwd(xrf, save=True)
+                # W(real, -1) and W(fake, +1): both segment means and the score gradient in one launch
+                w, ds = Fn.gan_loss(s, s.numel() // 2, -1.0, 1.0, 0)
+                C.ebwd(tape, ds)
+            if side is not None:
+                cur.wait_stream(side)
+            # gradient penalty: g = dD/dx_hat (input gradient only), v = dGP/dg, then the
+            # theta-gradient of <v, g> as reverse-over-tangent
+            if side is None:
+                with trange("critic/gp_input_grad"):
+                    sh, tape_h = C.efwd(xh, save=True)
+                    g = C.ebwd(tape_h, self._ones(sh), need_dx=True, wgrad=False)
+                    pack, v = Fn.gp_coef_pack(g, self.gp_weight, w)  # [total, W real, W fake, GP]
+                with trange("critic/gp_second_order"):
+                    sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
+            else:
+                pack = Fn.gp_pack(pen, self.gp_weight, w)
             with trange("critic/gp_second_order"):
-                sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
-        else:
-            pack = Fn.gp_pack(pen, self.gp_weight, w)
-        with trange("critic/gp_second_order"):
-            C.etbwd(tape_h, ttape, None, self._ones(sd), hook=self._hook(C))
+                C.etbwd(tape_h, ttape, None, self._ones(sd), hook=hook)
         return pack.to(self._acc)
 
     def _ones(self, like):
@@ -322,7 +336,9 @@ class GANTrainer:
             out, ds = Fn.gan_loss(s, s.numel(), -1.0, -1.0, 0)
         loss = out[0].to(self._acc)
         dfake = C.ebwd(tc, ds, need_dx=True, wgrad=False)
-        G.ebwd(tg, dfake, hook=self._hook(G))
+        hook = self._hook(G)
+        with Fn.wgrad_on(self._wgrad_side(hook)):
+            G.ebwd(tg, dfake, hook=hook)
         return loss
 
     # ---- one reference "epoch" (= iteration) ----------------------------------------------------
