@@ -21,8 +21,10 @@
 //   buffer descriptors, tile movers, tape slot I/O ........ shared device helpers
 //   lstm_tfwd2 .............................................. v2 tangent forward (32x32x16, 32 units per
 //                                                            wave): dispatched for act = sigmoid only
-//   lstm_bwd3 ............................................... BPTT: 4 recurrence + 4 data waves
-//   lstm_tbwd4 .............................................. tangent reverse: 16x16x32, 7 + 1 waves
+//   lstm_bwd3 ............................................... BPTT v3: 4 recurrence + 4 data waves
+//                                                            (HFREP_LSTM_BWD=3; A/B only)
+//   lstm_tbwd4 .............................................. tangent reverse: 16x16x32, 7 + 1 waves;
+//                                                            TG = false: the default BPTT
 //   lstm_fwd4 ............................................... forward + tangent forward: 16x16x32
 //   host side ............................................... launchers
 // Every v3 / v4 kernel: one persistent workgroup per CU walking 32-row tiles, 2 waves per SIMD
@@ -783,7 +785,7 @@ struct Tb4Geo {
   static constexpr size_t smem = (size_t)(4 * 32 * LG + 4 * 32 * LH) * 2;
 };
 
-template <int H, int ACT, bool DX, bool GEN = false>
+template <int H, int ACT, bool DX, bool GEN = false, bool TG = true>
 __global__ void __launch_bounds__(512)
 lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd, const bf16_t* __restrict__ tape,
                   const bf16_t* __restrict__ ttape, const float* __restrict__ U, bf16_t* __restrict__ dZ,
@@ -859,20 +861,21 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 #pragma unroll
       for (int e = 0; e < 8; ++e) { ac[e] = 0.f; acd[e] = 0.f; }
       Slot8 cc = ld_slot8(rt, uok, lo8, tape_off(Tn - 1, wt32) + 4 * SLOT_ELEMS);
-      Slot8 cdc = ld_slot8(rtt, uok, lo8, tape_off(Tn - 1, wt32) + 4 * SLOT_ELEMS);
+      Slot8 cdc = {};
+      if constexpr (TG) cdc = ld_slot8(rtt, uok, lo8, tape_off(Tn - 1, wt32) + 4 * SLOT_ELEMS);
       __syncthreads();  // (A) LDS free (previous row block stored)
       __syncthreads();  // (B) dH_{T-1} / dHd_{T-1} staged
       for (int t = Tn - 1; t >= 0; --t) {
         const int cb = t & 1, nb = (t + 1) & 1;
         const bool pv = t > 0, live = t < Tn - 1;
-        Slot8 tg[4], zd[4], cp, cdp;
+        Slot8 tg[4], zd[TG ? 4 : 1], cp, cdp = {};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           tg[s] = ld_slot8(rt, uok, lo8, tape_off(t, wt32) + s * SLOT_ELEMS);
-          zd[s] = ld_slot8(rtt, uok, lo8, tape_off(t, wt32) + s * SLOT_ELEMS);
+          if constexpr (TG) zd[s] = ld_slot8(rtt, uok, lo8, tape_off(t, wt32) + s * SLOT_ELEMS);
         }
         cp = ld_slot8(rt, uok && pv, lo8, tape_off(max(t - 1, 0), wt32) + 4 * SLOT_ELEMS);
-        cdp = ld_slot8(rtt, uok && pv, lo8, tape_off(max(t - 1, 0), wt32) + 4 * SLOT_ELEMS);
+        if constexpr (TG) cdp = ld_slot8(rtt, uok && pv, lo8, tape_off(max(t - 1, 0), wt32) + 4 * SLOT_ELEMS);
         f32x4 ah[2], ahd[2], ax[2], axd[2];
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
@@ -889,89 +892,113 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 #pragma unroll
               for (int ks = 0; ks < NK; ++ks) {
                 const bf16x8 a = *reinterpret_cast<const bf16x8*>(arow + 32 * ks);
-                const bf16x8 ad = *reinterpret_cast<const bf16x8*>(drow + 32 * ks);
                 ah[m] = mma16(a, ut[ks], ah[m]);
-                ahd[m] = mma16(ad, ut[ks], ahd[m]);
-                if constexpr (DX) {
-                  ax[m] = mma16(a, wt[ks], ax[m]);
-                  axd[m] = mma16(ad, wt[ks], axd[m]);
+                if constexpr (DX) ax[m] = mma16(a, wt[ks], ax[m]);
+                if constexpr (TG) {
+                  const bf16x8 ad = *reinterpret_cast<const bf16x8*>(drow + 32 * ks);
+                  ahd[m] = mma16(ad, ut[ks], ahd[m]);
+                  if constexpr (DX) axd[m] = mma16(ad, wt[ks], axd[m]);
                 }
               }
               if constexpr (TAIL) {
                 const bf16x4 a = *reinterpret_cast<const bf16x4*>(rowz + 32 * NK + 4 * g4);
-                const bf16x4 ad = *reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4);
+                const bf16x4 ad = TG ? *reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4) : a;
                 xdl_switch();
                 ah[m] = mma16k16(a, ut4, ah[m]);
-                ahd[m] = mma16k16(ad, ut4, ahd[m]);
+                if constexpr (TG) ahd[m] = mma16k16(ad, ut4, ahd[m]);
                 if constexpr (DX) {
                   ax[m] = mma16k16(a, wt4, ax[m]);
-                  axd[m] = mma16k16(ad, wt4, axd[m]);
+                  if constexpr (TG) axd[m] = mma16k16(ad, wt4, axd[m]);
                 }
               }
             } else {
 #pragma unroll
               for (int ks = 0; ks < NK; ++ks) {
                 ah[m] = mma16(*reinterpret_cast<const bf16x8*>(arow + 32 * ks), ut[ks], ah[m]);
-                ahd[m] = mma16(*reinterpret_cast<const bf16x8*>(drow + 32 * ks), ut[ks], ahd[m]);
+                if constexpr (TG) ahd[m] = mma16(*reinterpret_cast<const bf16x8*>(drow + 32 * ks), ut[ks], ahd[m]);
               }
               if constexpr (TAIL) {
                 const bf16x4 a = *reinterpret_cast<const bf16x4*>(rowz + 32 * NK + 4 * g4);
-                const bf16x4 ad = *reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4);
+                const bf16x4 ad = TG ? *reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4) : a;
                 xdl_switch();
                 ah[m] = mma16k16(a, ut4, ah[m]);
-                ahd[m] = mma16k16(ad, ut4, ahd[m]);
+                if constexpr (TG) ahd[m] = mma16k16(ad, ut4, ahd[m]);
               }
             }
           }
         }
         if constexpr (DX) {
           store_dx16(ax, rdx, Tn, t + 1, xw && live, nr, K, c, g4);
-          store_dx16(axd, rdxd, Tn, t + 1, xw && live, nr, K, c, g4);
+          if constexpr (TG) store_dx16(axd, rdxd, Tn, t + 1, xw && live, nr, K, c, g4);
         }
         const bf16_t* dh_t = dhb + cb * 32 * LH;
         const bf16_t* dhd_t = dhdb + cb * 32 * LH;
+        if constexpr (!TG) {
+          // BPTT only (the bwd3 contract): dz from the output adjoint and the carried cell adjoint
 #pragma unroll
-        for (int m = 0; m < 2; ++m)
+          for (int m = 0; m < 2; ++m)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int e = 4 * m + i, rr = 16 * m + 4 * g4 + i;
-            const float ig = tg[0].get(m, i), fg = tg[1].get(m, i), gg = tg[2].get(m, i), og = tg[3].get(m, i);
-            const float cv = cc.get(m, i), cpv = cp.get(m, i), cd = cdc.get(m, i), cdpv = cdp.get(m, i);
-            const float zdi = zd[0].get(m, i), zdf = zd[1].get(m, i), zdg = zd[2].get(m, i), zdo = zd[3].get(m, i);
-            const float si = ig * (1.f - ig), sf = fg * (1.f - fg), so = og * (1.f - og);
-            const float sg = act_dy(act, gg);
-            const float idot = si * zdi, fdot = sf * zdf, gdot = sg * zdg, odot = so * zdo;
-            const float ca = act_f(act, cv);
-            const float e1 = act_dy(act, ca), e2 = act_d2y(act, ca);
-            const float a_h = (uok ? bf2f(dh_t[rr * LH + c]) : 0.f) + ah[m][i];
-            const float a_hd = (uok ? bf2f(dhd_t[rr * LH + c]) : 0.f) + ahd[m][i];
-            const float a_od = a_hd * ca;
-            const float a_o = a_h * ca + a_hd * e1 * cd;
-            const float a_cd = acd[e] + a_hd * og * e1;
-            const float a_c = ac[e] + a_h * og * e1 + a_hd * (odot * e1 + og * e2 * cd);
-            const float a_fd = a_cd * cpv, a_id = a_cd * gg, a_gd = a_cd * ig;
-            const float a_f = a_c * cpv + a_cd * cdpv;
-            const float a_i = a_c * gg + a_cd * gdot;
-            const float a_g = a_c * ig + a_cd * idot;
-            ac[e] = uok ? a_c * fg + a_cd * fdot : 0.f;
-            acd[e] = uok ? a_cd * fg : 0.f;
-            const float s2i = si * (1.f - 2.f * ig), s2f = sf * (1.f - 2.f * fg), s2o = so * (1.f - 2.f * og);
-            const float s2g = act_d2y(act, gg);
-            if (uok) {
-              bf16_t* zr = zb + cb * 32 * LG + rr * LG + c;
-              bf16_t* dr = zdb + cb * 32 * LG + rr * LG + c;
-              zr[0] = f2bf(a_i * si + a_id * s2i * zdi);
-              zr[H] = f2bf(a_f * sf + a_fd * s2f * zdf);
-              zr[2 * H] = f2bf(a_g * sg + a_gd * s2g * zdg);
-              zr[3 * H] = f2bf(a_o * so + a_od * s2o * zdo);
-              dr[0] = f2bf(a_id * si);
-              dr[H] = f2bf(a_fd * sf);
-              dr[2 * H] = f2bf(a_gd * sg);
-              dr[3 * H] = f2bf(a_od * so);
+            for (int i = 0; i < 4; ++i) {
+              const int e = 4 * m + i, rr = 16 * m + 4 * g4 + i;
+              const float ig = tg[0].get(m, i), fg = tg[1].get(m, i), gg = tg[2].get(m, i), og = tg[3].get(m, i);
+              const float cv = cc.get(m, i), cpv = cp.get(m, i);
+              const float a_h = (uok ? bf2f(dh_t[rr * LH + c]) : 0.f) + ah[m][i];
+              const float ca = act_f(act, cv);
+              const float dov = a_h * ca;
+              const float dct = ac[e] + a_h * og * act_dy(act, ca);
+              ac[e] = uok ? dct * fg : 0.f;
+              if (uok) {
+                bf16_t* zr = zb + cb * 32 * LG + rr * LG + c;
+                zr[0] = f2bf(dct * gg * ig * (1.f - ig));
+                zr[H] = f2bf(dct * cpv * fg * (1.f - fg));
+                zr[2 * H] = f2bf(dct * ig * act_dy(act, gg));
+                zr[3 * H] = f2bf(dov * og * (1.f - og));
+              }
             }
-          }
+        } else {
+  #pragma unroll
+          for (int m = 0; m < 2; ++m)
+  #pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int e = 4 * m + i, rr = 16 * m + 4 * g4 + i;
+              const float ig = tg[0].get(m, i), fg = tg[1].get(m, i), gg = tg[2].get(m, i), og = tg[3].get(m, i);
+              const float cv = cc.get(m, i), cpv = cp.get(m, i), cd = cdc.get(m, i), cdpv = cdp.get(m, i);
+              const float zdi = zd[0].get(m, i), zdf = zd[1].get(m, i), zdg = zd[2].get(m, i), zdo = zd[3].get(m, i);
+              const float si = ig * (1.f - ig), sf = fg * (1.f - fg), so = og * (1.f - og);
+              const float sg = act_dy(act, gg);
+              const float idot = si * zdi, fdot = sf * zdf, gdot = sg * zdg, odot = so * zdo;
+              const float ca = act_f(act, cv);
+              const float e1 = act_dy(act, ca), e2 = act_d2y(act, ca);
+              const float a_h = (uok ? bf2f(dh_t[rr * LH + c]) : 0.f) + ah[m][i];
+              const float a_hd = (uok ? bf2f(dhd_t[rr * LH + c]) : 0.f) + ahd[m][i];
+              const float a_od = a_hd * ca;
+              const float a_o = a_h * ca + a_hd * e1 * cd;
+              const float a_cd = acd[e] + a_hd * og * e1;
+              const float a_c = ac[e] + a_h * og * e1 + a_hd * (odot * e1 + og * e2 * cd);
+              const float a_fd = a_cd * cpv, a_id = a_cd * gg, a_gd = a_cd * ig;
+              const float a_f = a_c * cpv + a_cd * cdpv;
+              const float a_i = a_c * gg + a_cd * gdot;
+              const float a_g = a_c * ig + a_cd * idot;
+              ac[e] = uok ? a_c * fg + a_cd * fdot : 0.f;
+              acd[e] = uok ? a_cd * fg : 0.f;
+              const float s2i = si * (1.f - 2.f * ig), s2f = sf * (1.f - 2.f * fg), s2o = so * (1.f - 2.f * og);
+              const float s2g = act_d2y(act, gg);
+              if (uok) {
+                bf16_t* zr = zb + cb * 32 * LG + rr * LG + c;
+                bf16_t* dr = zdb + cb * 32 * LG + rr * LG + c;
+                zr[0] = f2bf(a_i * si + a_id * s2i * zdi);
+                zr[H] = f2bf(a_f * sf + a_fd * s2f * zdf);
+                zr[2 * H] = f2bf(a_g * sg + a_gd * s2g * zdg);
+                zr[3 * H] = f2bf(a_o * so + a_od * s2o * zdo);
+                dr[0] = f2bf(a_id * si);
+                dr[H] = f2bf(a_fd * sf);
+                dr[2 * H] = f2bf(a_gd * sg);
+                dr[3 * H] = f2bf(a_od * so);
+              }
+            }
+        }
         cc = cp;
-        cdc = cdp;
+        if constexpr (TG) cdc = cdp;
         lds_barrier();  // step hand-off
       }
       if constexpr (DX) {  // dx_0 / dxdot_0 from the last dz tiles (final after the last barrier)
@@ -985,19 +1012,19 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 #pragma unroll
             for (int ks = 0; ks < NK; ++ks) {
               ax[m] = mma16(*reinterpret_cast<const bf16x8*>(rowz + 8 * g4 + 32 * ks), wt[ks], ax[m]);
-              axd[m] = mma16(*reinterpret_cast<const bf16x8*>(rowd + 8 * g4 + 32 * ks), wt[ks], axd[m]);
+              if constexpr (TG) axd[m] = mma16(*reinterpret_cast<const bf16x8*>(rowd + 8 * g4 + 32 * ks), wt[ks], axd[m]);
             }
             if constexpr (TAIL) {
               const bf16x4 a = *reinterpret_cast<const bf16x4*>(rowz + 32 * NK + 4 * g4);
-              const bf16x4 ad = *reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4);
+              const bf16x4 ad = TG ? *reinterpret_cast<const bf16x4*>(rowd + 32 * NK + 4 * g4) : a;
               xdl_switch();
               ax[m] = mma16k16(a, wt4, ax[m]);
-              axd[m] = mma16k16(ad, wt4, axd[m]);
+              if constexpr (TG) axd[m] = mma16k16(ad, wt4, axd[m]);
             }
           }
         }
         store_dx16(ax, rdx, Tn, 0, xw, nr, K, c, g4);
-        store_dx16(axd, rdxd, Tn, 0, xw, nr, K, c, g4);
+        if constexpr (TG) store_dx16(axd, rdxd, Tn, 0, xw, nr, K, c, g4);
       }
       __syncthreads();  // (C)
     }
@@ -1011,26 +1038,26 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
       head_rsrc<H, GEN>(rdhd, rhw, dHd, hdd, hw, row0, B, Tn);
       TileSrc<H, 64, GEN> a, ad;
       a.load(rdh, rhw, Tn, Tn - 1, true, lane);
-      ad.load(rdhd, rhw, Tn, Tn - 1, true, lane);
+      if constexpr (TG) ad.load(rdhd, rhw, Tn, Tn - 1, true, lane);
       __syncthreads();  // (A)
       a.to_lds(dhb + ((Tn - 1) & 1) * 32 * LH, LH, lane);
-      ad.to_lds(dhdb + ((Tn - 1) & 1) * 32 * LH, LH, lane);
+      if constexpr (TG) ad.to_lds(dhdb + ((Tn - 1) & 1) * 32 * LH, LH, lane);
       __syncthreads();  // (B)
       for (int t = Tn - 1; t >= 0; --t) {
         const int nb = (t + 1) & 1;
         const bool pv = t > 0, live = t < Tn - 1;
         a.load(rdh, rhw, Tn, t - 1, pv, lane);  // loads first: their wait covers no store of this step
-        ad.load(rdhd, rhw, Tn, t - 1, pv, lane);
+        if constexpr (TG) ad.load(rdhd, rhw, Tn, t - 1, pv, lane);
         tile16_store_w<G>(zb + nb * 32 * LG, LG, rz, Tn, t + 1, live, lane);
-        tile16_store_w<G>(zdb + nb * 32 * LG, LG, rzd, Tn, t + 1, live, lane);
+        if constexpr (TG) tile16_store_w<G>(zdb + nb * 32 * LG, LG, rzd, Tn, t + 1, live, lane);
         if (pv) {
           a.to_lds(dhb + nb * 32 * LH, LH, lane);  // dH_{t-1}: (t - 1) & 1 == nb
-          ad.to_lds(dhdb + nb * 32 * LH, LH, lane);
+          if constexpr (TG) ad.to_lds(dhdb + nb * 32 * LH, LH, lane);
         }
         lds_barrier();
       }
       tile16_store_w<G>(zb, LG, rz, Tn, 0, true, lane);
-      tile16_store_w<G>(zdb, LG, rzd, Tn, 0, true, lane);
+      if constexpr (TG) tile16_store_w<G>(zdb, LG, rzd, Tn, 0, true, lane);
       __syncthreads();  // (C)
     }
   } else {
@@ -1583,6 +1610,29 @@ void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const voi
 #define HFREP_BWD3_LAUNCH(DXV, ...)                                                            \
   if (hw) HFREP_BWD3_ACT(DXV, true, __VA_ARGS__) else HFREP_BWD3_ACT(DXV, false, __VA_ARGS__)
 
+// bf16 BPTT kernel: 4 (default) = lstm_tbwd4 with its tangent stream compiled out (TG = false: 7
+// compute waves of 16 units on 16x16x32 MFMAs, two per SIMD, + 1 data wave); 3 = lstm_bwd3 (4
+// recurrence waves of 32 units on 32x32x16, one per SIMD, + 4 data waves).  At the bench shape 4 is
+// 2-5 % faster per call (bench step -3.0 %), at B = 32 the iteration 9.06 -> 8.51 ms: with two compute
+// waves per SIMD one wave's cell math runs under the other's MFMA chain (profiles/r05_bwd4).
+// HFREP_LSTM_BWD=3 selects the v3 kernel (A/B).
+static int lstm_bwd_impl() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("HFREP_LSTM_BWD");
+    v = e ? atoi(e) : 4;
+  }
+  return v;
+}
+#define HFREP_BWD4_ACT(DXV, GV, ...)                                                           \
+  switch (act) {                                                                                 \
+    case 0: launch(lstm_tbwd4_kernel<100, 0, DXV, GV, false>, __VA_ARGS__); break;               \
+    case 1: launch(lstm_tbwd4_kernel<100, 1, DXV, GV, false>, __VA_ARGS__); break;               \
+    default: launch(lstm_tbwd4_kernel<100, 2, DXV, GV, false>, __VA_ARGS__); break;              \
+  }
+#define HFREP_BWD4_LAUNCH(DXV, ...)                                                            \
+  if (hw) HFREP_BWD4_ACT(DXV, true, __VA_ARGS__) else HFREP_BWD4_ACT(DXV, false, __VA_ARGS__)
+
 void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ, const float* W, void* dX, int K,
                       int B, int Tn, int H, int act, hipStream_t s, const void* head_d, const float* hw) {
   const bf16_t* dh = (const bf16_t*)dH;
@@ -1593,6 +1643,17 @@ void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ
   if (dX && act == 2 && !hw && (lstm_dbg() & 128)) {  // diagnostic phase-timer build
     launch(lstm_bwd3_kernel<100, 2, true, false, true>, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn,
            K, hd, hw);
+    return;
+  }
+  if (lstm_bwd_impl() == 4) {  // the tangent reverse v4 with its tangent stream compiled out
+    const bf16_t* nb = nullptr;
+    bf16_t* nw = nullptr;
+    if (dX)
+      HFREP_BWD4_LAUNCH(true, g, 512, Tb4Geo<100>::smem, s, dh, nb, tp, nb, U, (bf16_t*)dZ, nw, W, (bf16_t*)dX, nw, B, Tn,
+                        K, hd, nb, hw)
+    else
+      HFREP_BWD4_LAUNCH(false, g, 512, Tb4Geo<100>::smem, s, dh, nb, tp, nb, U, (bf16_t*)dZ, nw, (const float*)nullptr, nw,
+                        nw, B, Tn, 0, hd, nb, hw)
     return;
   }
   if (dX)
