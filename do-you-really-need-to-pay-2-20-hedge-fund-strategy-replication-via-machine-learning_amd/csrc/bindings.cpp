@@ -468,11 +468,6 @@ std::tuple<Tensor, Tensor> lstm2_fwd(Tensor x, Tensor W, optional<Tensor> b, Ten
   return {hs, tape};
 }
 
-Tensor lstm2_stamps() {
-  Tensor out = at::empty({4096, 8}, at::TensorOptions().dtype(at::kLong));
-  hfrep::lstm2_read_stamps(reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>()), 4096 * 8);
-  return out;
-}
 
 // W given: also returns dX = dZ W^T (B, T, K) from the same launch; otherwise dX is empty
 static int check_dx_W(const optional<Tensor>& W, int H) {
@@ -976,7 +971,6 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("lstm2_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
   m.def("lstm2_bwd(Tensor? dH, Tensor tape, Tensor U, int act, Tensor? W=None, bool need_dz=True, Tensor? head_d=None, "
         "Tensor? head_w=None) -> (Tensor, Tensor)");
-  m.def("lstm2_stamps() -> Tensor", &lstm2_stamps);  // no tensor inputs: catch-all kernel
   m.def("lstm2_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int act) -> (Tensor, Tensor)");
   m.def("lstm2_tbwd(Tensor? dH, Tensor? dHd, Tensor tape, Tensor ttape, Tensor U, int act, Tensor? W=None, "
         "Tensor? head_d=None, Tensor? head_dd=None, Tensor? head_w=None) -> (Tensor, Tensor, Tensor, Tensor)");

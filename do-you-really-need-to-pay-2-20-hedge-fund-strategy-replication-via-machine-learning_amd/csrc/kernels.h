@@ -22,7 +22,6 @@ bool launch_lstm_tbwd(int dt, const void* dH, const void* dHd, const void* gates
 
 // ---- lstm2.hip (bf16, fused input projection, blocked tapes; H == 100, K <= 128) ----
 size_t lstm2_tape_elems(int B, int Tn);
-void lstm2_read_stamps(uint64_t* out, int n);  // diagnostic BPTT phase timers (HFREP_LSTM_DBG & 128)
 bool lstm2_supported(int H, int K);
 void launch_lstm2_fwd(const void* x, const float* W, const float* b, const float* U, void* hs, void* tape, int B, int Tn,
                       int K, int H, int act, hipStream_t s);

@@ -21,10 +21,8 @@
 //   buffer descriptors, tile movers, tape slot I/O ........ shared device helpers
 //   lstm_tfwd2 .............................................. v2 tangent forward (32x32x16, 32 units per
 //                                                            wave): dispatched for act = sigmoid only
-//   lstm_bwd3 ............................................... BPTT v3: 4 recurrence + 4 data waves
-//                                                            (HFREP_LSTM_BWD=3; A/B only)
 //   lstm_tbwd4 .............................................. tangent reverse: 16x16x32, 7 + 1 waves;
-//                                                            TG = false: the default BPTT
+//                                                            TG = false: the BPTT
 //   lstm_fwd4 ............................................... forward + tangent forward: 16x16x32
 //   host side ............................................... launchers
 // Every v3 / v4 kernel: one persistent workgroup per CU walking 32-row tiles, 2 waves per SIMD
@@ -198,55 +196,6 @@ __device__ __forceinline__ void x_store_lds(const XPref& p, bf16_t* xb, int K, i
   }
 }
 
-// [32 x W] bf16 tile in LDS (row stride LD) -> step t of the tile descriptor `rd` in 16-byte
-// chunks; W % 8 == 0 and LD % 8 == 0.  16 threads per row, two rows per pass of the tile's 256
-// threads, 16 consecutive threads write 256 contiguous bytes of a row.  Every thread issues
-// 2 * ceil(W / 128) stores; chunks past the row end (and `on` == false) go out of range.
-template <int W>
-__device__ __forceinline__ void tile16_store(const bf16_t* buf, int LD, rsrc_t rd, int Tn, int t, bool on, int ltid) {
-  static_assert(W % 8 == 0, "16-byte chunks");
-  constexpr int CPR = W / 8, NK = (CPR + 15) / 16;
-  const int c0 = ltid & 15;
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    const int r = (ltid >> 4) + 16 * pass;
-    const int row_off = (r * Tn * W + 8 * c0) * 2;  // row in voffset (range-checked), step + chunk uniform
-#pragma unroll
-    for (int k = 0; k < NK; ++k) {
-      const int c = c0 + 16 * k;
-      const bool ok = c < CPR;
-      const v4i v = *reinterpret_cast<const v4i*>(buf + r * LD + 8 * (ok ? c : CPR - 1));
-      // (16-byte store: soffset 0, see st_slot)
-      __builtin_amdgcn_raw_buffer_store_b128(v, rd, (on && ok) ? row_off + (t * W + 128 * k) * 2 : kOOB, 0, 0);
-    }
-  }
-}
-
-// row-major [32 x W] tile <-> step t of a tile descriptor in 8-byte chunks (W % 4 == 0), moved by
-// the 256 threads of one row tile (ltid = thread index within the tile); a fixed NJ chunks per
-// thread, the ones past the tile out of range
-template <int W>
-struct Tile8 {
-  static constexpr int CPR = W / 4, NJ = (32 * CPR + 255) / 256;
-  static_assert(W % 4 == 0, "8-byte chunks");
-  v2i v[NJ];
-  __device__ __forceinline__ void load(rsrc_t rs, int Tn, int t, bool on, int ltid) {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int e = ltid + 256 * j;
-      const int r = e / CPR, c = e - r * CPR;
-      v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, (on && r < 32) ? (r * Tn * W + 4 * c) * 2 : kOOB, t * W * 2, 0);
-    }
-  }
-  __device__ __forceinline__ void to_lds(bf16_t* buf, int LD, int ltid) const {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int e = ltid + 256 * j;
-      const int r = e / CPR, c = e - r * CPR;
-      if (r < 32) *reinterpret_cast<v2i*>(buf + r * LD + 4 * c) = v[j];
-    }
-  }
-};
 // Source of the dH (dHdot) tiles of the reverse kernels, moved by NT threads in 8-byte chunks:
 // GEN = false: a row-major (B, T, W) tensor (`rs` = its tile descriptor);
 // GEN = true: the outer product d[b] * w[t W + h] of a Flatten -> Dense(1) critic head, generated
@@ -318,46 +267,7 @@ __device__ __forceinline__ void tile8_store(const bf16_t* buf, int LD, rsrc_t rd
   }
 }
 
-// dx = dz W^T fused into the backward kernels: wave w owns input columns kc = 32 w + (lane & 31)
-// (K <= 128), W^T fragments live in registers like U^T, and each finished dz tile of step t is
-// multiplied as it is consumed by the recurrence, so the separate dgrad pass that re-read dZ is gone.
-template <int NKG>
-__device__ __forceinline__ void make_wt(typename MF<bf16_t>::frag (&wt)[NKG], const float* __restrict__ W, int K, int G,
-                                        int kc, int lane) {
-#pragma unroll
-  for (int ks = 0; ks < NKG; ++ks)
-    wt[ks] = MF<bf16_t>::make([&](int n) {
-      const float v = W[(size_t)min(kc, K - 1) * G + min(n, G - 1)];
-      return (kc < K && n < G) ? v : 0.f;
-    }, ks, lane);
-}
-// 16 two-byte stores per lane, always issued (rows >= nr, columns >= K and `on` == false out of
-// range).  The range check covers voffset only (soffset is added to the base), so each row's
-// validity is decided in voffset: lane part of the row + column there, register-dependent row
-// part + step in soffset.
-__device__ __forceinline__ void store_dx(const f32x16& ax, rsrc_t rd, int Tn, int t, bool on, int nr, int K, int kc,
-                                         int lane) {
-  const int off = (on && kc < K) ? (4 * (lane >> 5) * Tn * K + kc) * 2 : kOOB;
-#pragma unroll
-  for (int r = 0; r < 16; ++r)
-    __builtin_amdgcn_raw_buffer_store_b16(f2bf(ax[r]), rd, acc32_row(r, lane) < nr ? off : kOOB,
-                                          (((r & 3) + 8 * (r >> 2)) * Tn * K + t * K) * 2, 0);
-}
-
 }  // namespace
-
-// diagnostic phase timers (HFREP_LSTM_DBG & 128 -> an ST=true instantiation of the BPTT kernel):
-// s_memtime deltas per phase summed per wave, read back by lstm2_read_stamps().  Only the
-// diagnostic build executes them; its absolute time is not a benchmark.
-__device__ unsigned long long g_lstm_stamps[4096 * 8];
-#define HFREP_STAMP(i)                                     \
-  if constexpr (ST) {                                      \
-    __builtin_amdgcn_sched_barrier(0);                     \
-    const uint64_t _t = __builtin_amdgcn_s_memtime();      \
-    __builtin_amdgcn_sched_barrier(0);                     \
-    st_acc[i] += _t - st_last;                             \
-    st_last = _t;                                          \
-  }
 
 // ==========================================================================================
 // tangent forward at the taped primal point: zdot_t = xdot_t W + hdot_{t-1} U
@@ -489,165 +399,6 @@ lstm_tfwd2_kernel(const bf16_t* __restrict__ xd, const float* __restrict__ W, co
 // (their waits never cover a store).  The two roles run separate loops with the same barrier
 // sequence (3 per row block + 1 per step).
 // ==========================================================================================
-template <int H, int ACT, bool DX, bool GEN = false, bool ST = false>
-__global__ void __launch_bounds__(512)
-lstm_bwd3_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ tape, const float* __restrict__ U,
-                 bf16_t* __restrict__ dZ, const float* __restrict__ W, bf16_t* __restrict__ dX, int B, int Tn, int K,
-                 const bf16_t* __restrict__ hd, const float* __restrict__ hw) {
-  constexpr int act = ACT;
-  // diagnostic phase timers (ST: HFREP_LSTM_DBG & 128): recurrence waves 0 prefetch issue,
-  // 1 MFMA, 2 gate math, 3 barrier; data waves 4 dH load issue, 5 dz tile stores, 6 dX MFMA +
-  // stores + dH to LDS, 7 barrier
-  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
-  if constexpr (ST) st_last = __builtin_amdgcn_s_memtime();
-  using P = MF<bf16_t>;
-  constexpr int G = 4 * H, NKG = (G + 15) / 16, LG = NKG * 16 + 8, NKH = (H + 15) / 16, LH = NKH * 16 + 8;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* zb = reinterpret_cast<bf16_t*>(smem);  // [2][32][LG]  dz_t tiles
-  bf16_t* dhb = zb + 2 * 32 * LG;                 // [2][32][LH]  dH_t tiles
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, w = wave & 3;
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  const int ltid = threadIdx.x & 255;  // thread index within the role group
-  const int u = w * 32 + (lane & 31);
-  const bool uok = u < H;
-  const int nrb = (B + 31) / 32;
-
-  if (wave < 4) {
-    // ---------------- recurrence waves ----------------
-    typename P::frag ut[NKG];
-#pragma unroll
-    for (int ks = 0; ks < NKG; ++ks)
-      ut[ks] = P::make([&](int k) {
-        const float v = U[(uok ? u : H - 1) * G + min(k, G - 1)];
-        return (uok && k < G) ? v : 0.f;
-      }, ks, lane);
-    const int lo = lane * 8;
-    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
-      const rsrc_t rt = tape_rsrc(tape, rb, nrb, Tn);
-      float dc[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dc[r] = 0.f;
-      Slot16 tg[4], cc, cp;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) tg[s] = ld_slot(rt, uok, lo, tape_off(Tn - 1, wu) + s * SLOT_ELEMS);
-      cc = ld_slot(rt, uok, lo, tape_off(Tn - 1, wu) + 4 * SLOT_ELEMS);
-      cp = ld_slot(rt, uok && Tn > 1, lo, tape_off(max(Tn - 2, 0), wu) + 4 * SLOT_ELEMS);
-      __syncthreads();  // (A) previous row block done with the LDS tiles
-      __syncthreads();  // (B) dH_{T-1} staged
-      for (int t = Tn - 1; t >= 0; --t) {
-        const bf16_t* zprev = zb + ((t + 1) & 1) * 32 * LG;  // dz_{t+1}
-        bf16_t* zcur = zb + (t & 1) * 32 * LG;               // dz_t
-        const bf16_t* dhcur = dhb + (t & 1) * 32 * LH;
-        // next step's tape (gates t-1, cell t-2): this wave issues loads only
-        const bool pv = t > 0;
-        Slot16 ng[4], ncp;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) ng[s] = ld_slot(rt, uok && pv, lo, tape_off(max(t - 1, 0), wu) + s * SLOT_ELEMS);
-        ncp = ld_slot(rt, uok && t > 1, lo, tape_off(max(t - 2, 0), wu) + 4 * SLOT_ELEMS);
-        HFREP_STAMP(0)
-        f32x16 acc = zero16();
-        if (t < Tn - 1) {
-          const bf16_t* arow = zprev + (lane & 31) * LG;
-#pragma unroll
-          for (int ks = 0; ks < NKG; ++ks) acc = P::mma(P::lda(arow, ks, lane), ut[ks], acc);
-        }
-        if constexpr (ST) {  // (the MFMA result is consumed below; fence its issue here)
-          __builtin_amdgcn_sched_barrier(0);
-          asm volatile("s_nop 0" ::"v"(acc[0]));
-        }
-        HFREP_STAMP(1)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rr = acc32_row(r, lane);
-          const float ig = tg[0].get(r), fg = tg[1].get(r), gg = tg[2].get(r), og = tg[3].get(r);
-          const float c = cc.get(r), cpv = cp.get(r);
-          const float dht = (uok ? bf2f(dhcur[rr * LH + u]) : 0.f) + acc[r];
-          const float ca = act_f(act, c);
-          const float dov = dht * ca;
-          const float dct = dc[r] + dht * og * act_dy(act, ca);
-          dc[r] = uok ? dct * fg : 0.f;
-          if (uok) {
-            bf16_t* zr = zcur + rr * LG + u;
-            zr[0] = f2bf(dct * gg * ig * (1.f - ig));
-            zr[H] = f2bf(dct * cpv * fg * (1.f - fg));
-            zr[2 * H] = f2bf(dct * ig * act_dy(act, gg));
-            zr[3 * H] = f2bf(dov * og * (1.f - og));
-          }
-        }
-        HFREP_STAMP(2)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) tg[s] = ng[s];
-        cc = cp;
-        cp = ncp;
-        lds_barrier();  // step hand-off
-        HFREP_STAMP(3)
-      }
-      __syncthreads();  // (C) the data waves have stored dz_0 / dx_0
-    }
-  } else {
-    // ---------------- data / input-gradient waves ----------------
-    const int kc = u;
-    typename P::frag wt[DX ? NKG : 1];
-    if constexpr (DX) make_wt<NKG>(wt, W, K, G, kc, lane);
-    for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
-      const int row0 = rb * 32;
-      const int nr = min(32, B - row0);
-      const rsrc_t rz = tile_rsrc(dZ, row0, B, Tn, G);
-      const rsrc_t rdx = tile_rsrc(DX ? dX : nullptr, row0, B, Tn, DX ? K : 1);
-      rsrc_t rdh, rhw;
-      head_rsrc<H, GEN>(rdh, rhw, dH, hd, hw, row0, B, Tn);
-      TileSrc<H, 256, GEN> d0, d1;  // dH_{t-1}, dH_{t-2} in flight (two steps of prefetch)
-      d0.load(rdh, rhw, Tn, Tn - 1, true, ltid);
-      d1.load(rdh, rhw, Tn, Tn - 2, Tn > 1, ltid);
-      __syncthreads();  // (A)
-      d0.to_lds(dhb + ((Tn - 1) & 1) * 32 * LH, LH, ltid);
-      d0 = d1;
-      d1.load(rdh, rhw, Tn, Tn - 3, Tn > 2, ltid);
-      __syncthreads();  // (B)
-      for (int t = Tn - 1; t >= 0; --t) {
-        const bf16_t* zprev = zb + ((t + 1) & 1) * 32 * LG;  // dz_{t+1}, final since the last barrier
-        const bool live = t < Tn - 1;
-        HFREP_STAMP(4)
-        tile16_store<G>(zprev, LG, rz, Tn, t + 1, live, ltid);
-        HFREP_STAMP(5)
-        if constexpr (DX) {
-          f32x16 ax = zero16();
-          if (live && wu * 32 < K) {  // (K = 32: waves 5-7 own no input column)
-            const bf16_t* arow = zprev + (lane & 31) * LG;
-#pragma unroll
-            for (int ks = 0; ks < NKG; ++ks) ax = P::mma(P::lda(arow, ks, lane), wt[ks], ax);
-          }
-          store_dx(ax, rdx, Tn, t + 1, live, nr, K, kc, lane);
-        }
-        if (t > 0) d0.to_lds(dhb + ((t - 1) & 1) * 32 * LH, LH, ltid);  // dH_{t-1} for the next step
-        d0 = d1;
-        d1.load(rdh, rhw, Tn, t - 3, t > 2, ltid);
-        HFREP_STAMP(6)
-        lds_barrier();  // step hand-off
-        HFREP_STAMP(7)
-      }
-      tile16_store<G>(zb, LG, rz, Tn, 0, true, ltid);
-      if constexpr (DX) {
-        f32x16 ax = zero16();
-        if (wu * 32 < K) {
-          const bf16_t* arow = zb + (lane & 31) * LG;
-#pragma unroll
-          for (int ks = 0; ks < NKG; ++ks) ax = P::mma(P::lda(arow, ks, lane), wt[ks], ax);
-        }
-        store_dx(ax, rdx, Tn, 0, true, nr, K, kc, lane);
-      }
-      __syncthreads();  // (C)
-    }
-  }
-  if constexpr (ST) {
-    if (lane == 0) {
-      const int slot = blockIdx.x * 8 + wave;
-      if (slot < 4096)
-        for (int i = 0; i < 8; ++i) g_lstm_stamps[slot * 8 + i] = st_acc[i];
-    }
-  }
-}
-
 // ==========================================================================================
 // Tangent reverse v4: 16x16x32 MFMAs, 16 units per wave.
 //
@@ -934,7 +685,7 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
         const bf16_t* dh_t = dhb + cb * 32 * LH;
         const bf16_t* dhd_t = dhdb + cb * 32 * LH;
         if constexpr (!TG) {
-          // BPTT only (the bwd3 contract): dz from the output adjoint and the carried cell adjoint
+          // BPTT only (the former lstm_bwd3's contract): dz from the output adjoint and the carried cell adjoint
 #pragma unroll
           for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -1497,10 +1248,6 @@ static size_t tfwd2_smem(int H, int K) {
   const int KP = (K + 15) & ~15, LX = KP + 8, LH = ((H + 15) / 16) * 16 + 8;
   return (size_t)(4 * H * LX + 2 * 32 * LX + 2 * 32 * LH) * 2;
 }
-static size_t bwd_smem(int H) {
-  const int LG = ((4 * H + 15) / 16) * 16 + 8, LH = ((H + 15) / 16) * 16 + 8;
-  return (size_t)(2 * 32 * LG + 2 * 32 * LH) * 2;
-}
 constexpr size_t LDS_MAX = 160 * 1024;
 
 // Dynamic LDS above 64 KB needs the per-kernel attribute; set it once per kernel.
@@ -1534,7 +1281,7 @@ static void launch(Kern k, int grid, int threads, size_t smem, hipStream_t s, Ar
 
 // timing-only ablation mask of the forward kernel (HFREP_LSTM_DBG; 0 in every real run):
 // 1 no tape store, 2 no h store, 4 no x load, 256 every step's tape stores to step 0's slots
-// (L2-resident); 128 selects the BPTT phase-timer build
+// (L2-resident)
 static int lstm_dbg() {
   static int d = -1;
   if (d < 0) {
@@ -1601,29 +1348,11 @@ void launch_lstm2_tfwd(const void* xd, const float* W, const float* U, const voi
                (bf16_t*)hds, (bf16_t*)ttape, B, Tn, K, lstm_dbg())
 }
 
-#define HFREP_BWD3_ACT(DXV, GV, ...)                                                           \
-  switch (act) {                                                                                 \
-    case 0: launch(lstm_bwd3_kernel<100, 0, DXV, GV>, __VA_ARGS__); break;                       \
-    case 1: launch(lstm_bwd3_kernel<100, 1, DXV, GV>, __VA_ARGS__); break;                       \
-    default: launch(lstm_bwd3_kernel<100, 2, DXV, GV>, __VA_ARGS__); break;                      \
-  }
-#define HFREP_BWD3_LAUNCH(DXV, ...)                                                            \
-  if (hw) HFREP_BWD3_ACT(DXV, true, __VA_ARGS__) else HFREP_BWD3_ACT(DXV, false, __VA_ARGS__)
-
-// bf16 BPTT kernel: 4 (default) = lstm_tbwd4 with its tangent stream compiled out (TG = false: 7
-// compute waves of 16 units on 16x16x32 MFMAs, two per SIMD, + 1 data wave); 3 = lstm_bwd3 (4
-// recurrence waves of 32 units on 32x32x16, one per SIMD, + 4 data waves).  At the bench shape 4 is
-// 2-5 % faster per call (bench step -3.0 %), at B = 32 the iteration 9.06 -> 8.51 ms: with two compute
-// waves per SIMD one wave's cell math runs under the other's MFMA chain (profiles/r05_bwd4).
-// HFREP_LSTM_BWD=3 selects the v3 kernel (A/B).
-static int lstm_bwd_impl() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("HFREP_LSTM_BWD");
-    v = e ? atoi(e) : 4;
-  }
-  return v;
-}
+// The bf16 BPTT is the tangent reverse v4 with its tangent stream compiled out (TG = false): 7 compute
+// waves of 16 units on 16x16x32 MFMAs, two per SIMD, + 1 data wave.  It replaced lstm_bwd3 (4 recurrence
+// waves of 32 units on 32x32x16, one per SIMD): 2-5 % faster per call at the bench shape, 9.06 -> 8.51 ms
+// per B = 32 iteration -- with two compute waves per SIMD one wave's cell math runs under the other's
+// MFMA chain (profiles/r05_bwd4).
 #define HFREP_BWD4_ACT(DXV, GV, ...)                                                           \
   switch (act) {                                                                                 \
     case 0: launch(lstm_tbwd4_kernel<100, 0, DXV, GV, false>, __VA_ARGS__); break;               \
@@ -1638,29 +1367,15 @@ void launch_lstm2_bwd(const void* dH, const void* tape, const float* U, void* dZ
   const bf16_t* dh = (const bf16_t*)dH;
   const bf16_t* tp = (const bf16_t*)tape;
   const bf16_t* hd = (const bf16_t*)head_d;
+  const bf16_t* nb = nullptr;
+  bf16_t* nw = nullptr;
   const int g = persistent_grid(B);
-  const size_t sm = bwd_smem(H);
-  if (dX && act == 2 && !hw && (lstm_dbg() & 128)) {  // diagnostic phase-timer build
-    launch(lstm_bwd3_kernel<100, 2, true, false, true>, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn,
-           K, hd, hw);
-    return;
-  }
-  if (lstm_bwd_impl() == 4) {  // the tangent reverse v4 with its tangent stream compiled out
-    const bf16_t* nb = nullptr;
-    bf16_t* nw = nullptr;
-    if (dX)
-      HFREP_BWD4_LAUNCH(true, g, 512, Tb4Geo<100>::smem, s, dh, nb, tp, nb, U, (bf16_t*)dZ, nw, W, (bf16_t*)dX, nw, B, Tn,
-                        K, hd, nb, hw)
-    else
-      HFREP_BWD4_LAUNCH(false, g, 512, Tb4Geo<100>::smem, s, dh, nb, tp, nb, U, (bf16_t*)dZ, nw, (const float*)nullptr, nw,
-                        nw, B, Tn, 0, hd, nb, hw)
-    return;
-  }
+  const size_t sm = Tb4Geo<100>::smem;
   if (dX)
-    HFREP_BWD3_LAUNCH(true, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, W, (bf16_t*)dX, B, Tn, K, hd, hw)
+    HFREP_BWD4_LAUNCH(true, g, 512, sm, s, dh, nb, tp, nb, U, (bf16_t*)dZ, nw, W, (bf16_t*)dX, nw, B, Tn, K, hd, nb, hw)
   else
-    HFREP_BWD3_LAUNCH(false, g, 512, sm, s, dh, tp, U, (bf16_t*)dZ, (const float*)nullptr, (bf16_t*)nullptr, B, Tn, 0,
-                      hd, hw)
+    HFREP_BWD4_LAUNCH(false, g, 512, sm, s, dh, nb, tp, nb, U, (bf16_t*)dZ, nw, (const float*)nullptr, nw, nw, B, Tn, 0,
+                      hd, nb, hw)
 }
 
 #define HFREP_TBWD4_ACT(DXV, GV, ...)                                                          \
@@ -1689,11 +1404,6 @@ void launch_lstm2_tbwd(const void* dH, const void* dHd, const void* tape, const 
     HFREP_TBWD4_LAUNCH(false, g, 512, sm, s, (const bf16_t*)dH, (const bf16_t*)dHd, (const bf16_t*)tape,
                        (const bf16_t*)ttape, U, (bf16_t*)dZ, (bf16_t*)dZd, (const float*)nullptr, (bf16_t*)nullptr,
                        (bf16_t*)nullptr, B, Tn, 0, hd, hdd, hw)
-}
-
-void lstm2_read_stamps(uint64_t* out, int n) {
-  HFREP_CHECK_HIP(hipDeviceSynchronize());
-  HFREP_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstm_stamps), (size_t)n * sizeof(uint64_t)));
 }
 
 }  // namespace hfrep
