@@ -133,3 +133,17 @@ def test_latent_sweep_and_augmentation(cleaned):
     assert (x >= lo[:22] - 1e-9).all() and (x <= hi[:22] + 1e-9).all()
     aug = latent_sweep(cleaned, latents=[2], x_extra=x, y_extra=y)
     assert np.isfinite(aug.metrics.to_numpy()).all()
+
+
+def test_latent_sweep_many_equals_single_sweeps(cleaned):
+    """latent_sweep_many (every (seed, latent) AE built first and trained together -- one launch on a GPU)
+    gives each seed exactly the sweep latent_sweep gives it alone (here on the CPU, fits one by one)."""
+    from hfrep.finance.experiment import generated_augmentation, latent_sweep, latent_sweep_many
+
+    gen = np.random.RandomState(1).rand(3, 10, 36).astype(np.float32)
+    x, y = generated_augmentation(gen, cleaned)
+    many = latent_sweep_many(cleaned, seeds=[123, 7], latents=[2], x_extras=[None, x], y_extras=[None, y])
+    one = [latent_sweep(cleaned, latents=[2], seed=123), latent_sweep(cleaned, latents=[2], seed=7, x_extra=x, y_extra=y)]
+    for a, b in zip(many, one):
+        pd.testing.assert_frame_equal(a.metrics, b.metrics)
+        pd.testing.assert_frame_equal(a.sharpe_post, b.sharpe_post)
