@@ -660,6 +660,34 @@ def test_lstm2_tbwd_bitwise_large_batch(cuda, act):
 
 @pytest.mark.parametrize("act", [1, 2])
 @pytest.mark.parametrize("K", [32, 100])
+def test_lstm2_bwd_bitwise_large_batch(cuda, act, K):
+    """The bf16 BPTT (lstm_tbwd4 with its tangent stream compiled out, round 5) run three times at
+    B = 32 772 on one tape is bitwise equal: dZ alone, dZ + fused dX, and dX from the generated head
+    adjoint (the paths of the critic's W-terms backward, GP input gradient and generator step)."""
+    from hfrep.ops import functional as Fn
+
+    H, T, B = 100, 24, 32772
+    g = torch.Generator(device=cuda).manual_seed(2)
+    mk = lambda *s_, sc=0.5: (torch.randn(*s_, device=cuda, generator=g) * sc).to(torch.bfloat16)
+    x, dH = mk(B, T, K), mk(B, T, H)
+    W = torch.randn(K, 4 * H, device=cuda, generator=g) * 0.1
+    U = torch.randn(H, 4 * H, device=cuda, generator=g) * 0.1
+    b = torch.randn(4 * H, device=cuda, generator=g) * 0.1
+    _, tape = Fn.lstm_layer_fwd(x, W, b, U, act, True)
+    oa = Fn.OuterAdjoint(mk(B, 1), torch.randn(T * H, 1, device=cuda, generator=g) * 0.1, (B, T, H))
+    runs = []
+    for _ in range(3):
+        z = Fn.lstm_layer_bwd(dH, tape, U, act)
+        zx = Fn.lstm_layer_bwd(dH, tape, U, act, W=W, need_dz=True)
+        gx = Fn.lstm_layer_bwd(oa, tape, U, act, W=W, need_dz=False)
+        runs.append([z, *zx, *(gx if isinstance(gx, tuple) else (gx,))])
+    for r in runs[1:]:
+        assert all(a is None and c is None or torch.equal(a, c) for a, c in zip(runs[0], r))
+    assert torch.isfinite(runs[0][0].float()).all() and runs[0][0].abs().max() > 0
+
+
+@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("K", [32, 100])
 def test_lstm2_tfwd_bitwise_large_batch(cuda, act, K):
     """The bf16 tangent forward (hdot and the tangent tape) run three times at B = 32 772 on one primal
     tape is bitwise equal (act = sigmoid differed run to run in rows 30 / 31 of a few row blocks with
