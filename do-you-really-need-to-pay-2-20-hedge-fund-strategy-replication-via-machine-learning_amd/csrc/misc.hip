@@ -147,28 +147,44 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict_
     slab[(size_t)blockIdx.x * 2 * D + D + j] = b;
   }
 }
-
-// bf16, D <= 128, D % 4 == 0 (the models' H = 100): one row per HALF wave, each lane holds 4
-// contiguous values (one 8-byte load / store), mean and variance from registers (one read of x),
-// and without SAVE (no-grad forwards: the generator in every critic step) no xhat / rstd traffic.
-// The generic kernel above re-read x three times with 2-byte accesses and always wrote xhat:
-// 146 us per (16384 x 24) x 100 call, ~1.6 TB/s (profiles/r01_buf).
-template <bool SAVE, bool PRE>
-__global__ void __launch_bounds__(256) layernorm_fwd_x4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
-                                                               const float* __restrict__ beta, bf16_t* __restrict__ y,
-                                                               bf16_t* __restrict__ xhat, float* __restrict__ rstd_out,
-                                                               int64_t rows, int D, float eps, float pre_alpha) {
-  const int hl = threadIdx.x & 31;
-  const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
-  if (row >= rows) return;  // a whole half wave (the reductions stay inside a half)
-  const int j = 4 * hl;
-  const bool on = j < D;
-  const uint2 raw = on ? *reinterpret_cast<const uint2*>(x + row * D + j) : make_uint2(0, 0);
-  float v[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u), __uint_as_float(raw.y << 16),
-                __uint_as_float(raw.y & 0xffff0000u)};
+// D <= 128, D % 4 == 0 (bf16 or fp32): one row per half wave, 4 contiguous values per lane (one 8- /
+// 16-byte load / store), mean and variance from registers (one read of x), and without SAVE (no-grad
+// forwards: the generator in every critic step) no xhat / rstd traffic.  bf16: a fixed grid (8 workgroups
+// per CU) strides over the rows, two rows per half wave per pass with both loads issued before either
+// reduction (the one-pass-per-8-rows grid launched ~786 k workgroups per (262 144 x 24) call and moved
+// 2.7-3.3 TB/s); fp32 keeps one row per half wave and pass, which its 16-byte lanes already stream at
+// 4.4-5.3 TB/s (profiles/r05_ln).  The generic kernel above re-read x three times with
+// 2-byte accesses (146 us per (16384 x 24) x 100 call, ~1.6 TB/s, profiles/r01_buf).
+template <typename T>
+struct LnIO;
+template <>
+struct LnIO<bf16_t> {
+  static __device__ __forceinline__ void load(const bf16_t* p, bool on, float (&v)[4]) {
+    const uint2 r = on ? *reinterpret_cast<const uint2*>(p) : make_uint2(0, 0);
+    v[0] = __uint_as_float(r.x << 16); v[1] = __uint_as_float(r.x & 0xffff0000u);
+    v[2] = __uint_as_float(r.y << 16); v[3] = __uint_as_float(r.y & 0xffff0000u);
+  }
+  static __device__ __forceinline__ void store(bf16_t* p, float a, float b, float c, float d) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pk2bf(a, b), pk2bf(c, d));
+  }
+};
+template <>
+struct LnIO<float> {
+  static __device__ __forceinline__ void load(const float* p, bool on, float (&v)[4]) {
+    const float4 r = on ? *reinterpret_cast<const float4*>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[0] = r.x; v[1] = r.y; v[2] = r.z; v[3] = r.w;
+  }
+  static __device__ __forceinline__ void store(float* p, float a, float b, float c, float d) {
+    *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+  }
+};
+template <typename T, bool SAVE, bool PRE>
+__device__ __forceinline__ void ln_row(float (&v)[4], int64_t row, int j, bool on, int D, float eps, float pre_alpha,
+                                       const float4& g, const float4& b, T* __restrict__ y, T* __restrict__ xhat,
+                                       float* __restrict__ rstd_out, int hl) {
   if constexpr (PRE) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = pre_lrelu<bf16_t>(v[i], pre_alpha);
+    for (int i = 0; i < 4; ++i) v[i] = pre_lrelu<T>(v[i], pre_alpha);
   }
   const float mu = halfwave_sum((v[0] + v[1]) + (v[2] + v[3])) / D;
   float q = 0.f;
@@ -179,89 +195,62 @@ __global__ void __launch_bounds__(256) layernorm_fwd_x4_kernel(const bf16_t* __r
   }
   const float rstd = rsqrtf(halfwave_sum(q) / D + eps);
   if (on) {
-    const float4 g = *reinterpret_cast<const float4*>(gamma + j), b = *reinterpret_cast<const float4*>(beta + j);
     const float h0 = v[0] * rstd, h1 = v[1] * rstd, h2 = v[2] * rstd, h3 = v[3] * rstd;
-    *reinterpret_cast<uint2*>(y + row * D + j) =
-        make_uint2(pk2bf(h0 * g.x + b.x, h1 * g.y + b.y), pk2bf(h2 * g.z + b.z, h3 * g.w + b.w));
-    if constexpr (SAVE) *reinterpret_cast<uint2*>(xhat + row * D + j) = make_uint2(pk2bf(h0, h1), pk2bf(h2, h3));
+    LnIO<T>::store(y + row * D + j, h0 * g.x + b.x, h1 * g.y + b.y, h2 * g.z + b.z, h3 * g.w + b.w);
+    if constexpr (SAVE) LnIO<T>::store(xhat + row * D + j, h0, h1, h2, h3);
   }
   if (SAVE && hl == 0) rstd_out[row] = rstd;
 }
-
-// fp32 twin of the kernel above (D <= 128, D % 4 == 0): one row per half wave, one 16-byte load /
-// store per lane; the generic fp32 kernel re-read x three times with 4-byte accesses (411 us per
-// (32768 x 24) x 100 call at 2.3 TB/s, profiles/r02_fp32_262k)
-template <bool SAVE, bool PRE>
-__global__ void __launch_bounds__(256) layernorm_fwd_x4f_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
-                                                                const float* __restrict__ beta, float* __restrict__ y,
-                                                                float* __restrict__ xhat, float* __restrict__ rstd_out,
-                                                                int64_t rows, int D, float eps, float pre_alpha) {
+template <typename T, bool SAVE, bool PRE, int NR>
+__global__ void __launch_bounds__(256) layernorm_fwd_x4_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, T* __restrict__ y,
+                                                               T* __restrict__ xhat, float* __restrict__ rstd_out,
+                                                               int64_t rows, int D, float eps, float pre_alpha) {
+  static_assert(NR == 1 || NR == 2, "rows per half wave and pass");
   const int hl = threadIdx.x & 31;
-  const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
-  if (row >= rows) return;  // a whole half wave (the reductions stay inside a half)
   const int j = 4 * hl;
   const bool on = j < D;
-  const float4 raw = on ? *reinterpret_cast<const float4*>(x + row * D + j) : make_float4(0.f, 0.f, 0.f, 0.f);
-  float v[4] = {raw.x, raw.y, raw.z, raw.w};
-  if constexpr (PRE) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = pre_lrelu<float>(v[i], pre_alpha);
+  const float4 g = on ? *reinterpret_cast<const float4*>(gamma + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 b = on ? *reinterpret_cast<const float4*>(beta + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int64_t stride = (int64_t)gridDim.x * 8 * NR;
+  // (the row index is uniform over a half wave: every branch below keeps the half wave together, and the
+  // reductions stay inside it)
+  for (int64_t r0 = (int64_t)blockIdx.x * 8 * NR + (threadIdx.x >> 5); r0 < rows; r0 += stride) {
+    float v0[4], v1[4];
+    LnIO<T>::load(x + r0 * D + j, on, v0);
+    if constexpr (NR == 2) {
+      const int64_t r1 = r0 + 8;
+      const bool two = r1 < rows;
+      LnIO<T>::load(x + (two ? r1 : r0) * D + j, on && two, v1);
+      ln_row<T, SAVE, PRE>(v0, r0, j, on, D, eps, pre_alpha, g, b, y, xhat, rstd_out, hl);
+      if (two) ln_row<T, SAVE, PRE>(v1, r1, j, on, D, eps, pre_alpha, g, b, y, xhat, rstd_out, hl);
+    } else {
+      ln_row<T, SAVE, PRE>(v0, r0, j, on, D, eps, pre_alpha, g, b, y, xhat, rstd_out, hl);
+    }
   }
-  const float mu = halfwave_sum((v[0] + v[1]) + (v[2] + v[3])) / D;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[i] = on ? v[i] - mu : 0.f;
-    q += v[i] * v[i];
-  }
-  const float rstd = rsqrtf(halfwave_sum(q) / D + eps);
-  if (on) {
-    const float4 g = *reinterpret_cast<const float4*>(gamma + j), b = *reinterpret_cast<const float4*>(beta + j);
-    const float h0 = v[0] * rstd, h1 = v[1] * rstd, h2 = v[2] * rstd, h3 = v[3] * rstd;
-    *reinterpret_cast<float4*>(y + row * D + j) = make_float4(h0 * g.x + b.x, h1 * g.y + b.y, h2 * g.z + b.z, h3 * g.w + b.w);
-    if constexpr (SAVE) *reinterpret_cast<float4*>(xhat + row * D + j) = make_float4(h0, h1, h2, h3);
-  }
-  if (SAVE && hl == 0) rstd_out[row] = rstd;
 }
 
 void launch_layernorm_fwd(int dt, const void* x, const float* gamma, const float* beta, void* y, void* xhat,
                           float* rstd, int64_t rows, int D, float eps, float pre_alpha, hipStream_t s) {
-  if (dt == DT_F32 && D <= 128 && D % 4 == 0) {
-    const int grid = (int)std::max<int64_t>(1, (rows + 7) / 8);
-    const float* xp = (const float*)x;
-    float* yp = (float*)y;
-    float* hp = (float*)xhat;
-    if (xhat && pre_alpha >= 0.f)
-      hipLaunchKernelGGL((layernorm_fwd_x4f_kernel<true, true>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp, hp,
-                         rstd, rows, D, eps, pre_alpha);
-    else if (xhat)
-      hipLaunchKernelGGL((layernorm_fwd_x4f_kernel<true, false>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp, hp,
-                         rstd, rows, D, eps, pre_alpha);
-    else if (pre_alpha >= 0.f)
-      hipLaunchKernelGGL((layernorm_fwd_x4f_kernel<false, true>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp,
-                         (float*)nullptr, (float*)nullptr, rows, D, eps, pre_alpha);
-    else
-      hipLaunchKernelGGL((layernorm_fwd_x4f_kernel<false, false>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp,
-                         (float*)nullptr, (float*)nullptr, rows, D, eps, pre_alpha);
-    return;
-  }
-  if (dt == DT_BF16 && D <= 128 && D % 4 == 0) {
-    const int grid = (int)std::max<int64_t>(1, (rows + 7) / 8);
-    const bf16_t* xp = (const bf16_t*)x;
-    bf16_t* yp = (bf16_t*)y;
-    bf16_t* hp = (bf16_t*)xhat;
-    if (xhat && pre_alpha >= 0.f)
-      hipLaunchKernelGGL((layernorm_fwd_x4_kernel<true, true>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp, hp,
-                         rstd, rows, D, eps, pre_alpha);
-    else if (xhat)
-      hipLaunchKernelGGL((layernorm_fwd_x4_kernel<true, false>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp, hp,
-                         rstd, rows, D, eps, pre_alpha);
-    else if (pre_alpha >= 0.f)
-      hipLaunchKernelGGL((layernorm_fwd_x4_kernel<false, true>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp,
-                         (bf16_t*)nullptr, (float*)nullptr, rows, D, eps, pre_alpha);
-    else
-      hipLaunchKernelGGL((layernorm_fwd_x4_kernel<false, false>), dim3(grid), dim3(256), 0, s, xp, gamma, beta, yp,
-                         (bf16_t*)nullptr, (float*)nullptr, rows, D, eps, pre_alpha);
+  if ((dt == DT_F32 || dt == DT_BF16) && D <= 128 && D % 4 == 0) {
+    const bool sv = xhat != nullptr, pre = pre_alpha >= 0.f;
+    if (dt == DT_F32) {
+      // fp32 (16-byte lanes): one row per half wave, one pass (4.4-5.3 TB/s; the bf16 form below measured
+      // 4.1-4.4 here, scripts/bench_ln.py)
+      const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 7) / 8, 1 << 30));
+      auto k = sv ? (pre ? layernorm_fwd_x4_kernel<float, true, true, 1> : layernorm_fwd_x4_kernel<float, true, false, 1>)
+                  : (pre ? layernorm_fwd_x4_kernel<float, false, true, 1> : layernorm_fwd_x4_kernel<float, false, false, 1>);
+      hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, s, (const float*)x, gamma, beta, (float*)y, (float*)xhat, rstd,
+                         rows, D, eps, pre_alpha);
+    } else {
+      // bf16 (8-byte lanes): two rows per half wave and pass on a grid of 8 workgroups per CU (-30 % without
+      // / -7 % with the saved xhat against one row per half wave and pass, 2.7 -> 3.9 TB/s)
+      const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 15) / 16, (int64_t)device_cu_count() * 8));
+      auto k = sv ? (pre ? layernorm_fwd_x4_kernel<bf16_t, true, true, 2> : layernorm_fwd_x4_kernel<bf16_t, true, false, 2>)
+                  : (pre ? layernorm_fwd_x4_kernel<bf16_t, false, true, 2> : layernorm_fwd_x4_kernel<bf16_t, false, false, 2>);
+      hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, gamma, beta, (bf16_t*)y, (bf16_t*)xhat, rstd,
+                         rows, D, eps, pre_alpha);
+    }
     return;
   }
   // one row per wave and no grid-stride loop: a wave's row is a dependent load -> reduce -> store

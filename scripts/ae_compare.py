@@ -1,46 +1,44 @@
-"""Per-k comparison of autoencoder sweeps across runs (device / dtype): mean and spread over seeds.
+"""Compare two AE study directories (scripts/ae_study.py outputs): per (panel, dtype, seed) sweep the largest
+absolute difference of every metric / Sharpe / turnover value, and the elapsed time of each run.
 
-usage: python scripts/ae_compare.py LABEL=glob [LABEL=glob ...] [--panel real|augmented] [--metric IS_r2]
-
-Each glob matches `ae_sweep` JSONs (scripts/ae_study.py / `hfrep replicate --method ae-sweep --out`);
-prints one markdown table: k, then per label `mean (sd)` of the metric over its seeds, and the number of
-epochs is not stored, so only the published metrics are compared.
+usage: python scripts/ae_compare.py NEW_DIR OLD_DIR [OLD_DIR2 ...]   (later dirs fill what earlier ones lack)
 """
 import glob
 import json
+import os
 import sys
 
-import numpy as np
+
+def flat(d, pre=""):
+    out = {}
+    for k, v in d.items():
+        if isinstance(v, dict):
+            out.update(flat(v, f"{pre}{k}/"))
+        elif isinstance(v, (int, float)):
+            out[pre + k] = float(v)
+    return out
 
 
-def load(pattern, metric):
-    runs = [json.load(open(p))["ae_sweep"] for p in sorted(glob.glob(pattern))]
-    if not runs:
-        raise SystemExit(f"no files match {pattern}")
-    ks = sorted(int(k) for k in runs[0]["metrics"])
-    vals = np.array([[r["metrics"][str(k)][metric] for k in ks] for r in runs], dtype=float)
-    return ks, vals
-
-
-def main(argv):
-    metric = "IS_r2"
-    specs = []
-    it = iter(argv)
-    for a in it:
-        if a == "--metric":
-            metric = next(it)
-        else:
-            lab, _, pat = a.partition("=")
-            specs.append((lab, pat))
-    cols = [(lab,) + load(pat, metric) for lab, pat in specs]
-    ks = cols[0][1]
-    head = "| k | " + " | ".join(f"{lab} ({v.shape[0]} seeds)" for lab, _, v in cols) + " |"
-    print(f"{metric}: mean (sd) over seeds\n")
-    print(head)
-    print("|---" * (len(cols) + 1) + "|")
-    for i, k in enumerate(ks):
-        print(f"| {k} | " + " | ".join(f"{v[:, i].mean():.3f} ({v[:, i].std():.3f})" for _, _, v in cols) + " |")
+def main():
+    new, olds = sys.argv[1], sys.argv[2:]
+    worst, n, exact, t_new, t_old = 0.0, 0, 0, 0.0, 0.0
+    for p in sorted(glob.glob(os.path.join(new, "sweep_*.json"))):
+        name = os.path.basename(p)
+        q = next((os.path.join(o, name) for o in olds if os.path.exists(os.path.join(o, name))), None)
+        if q is None:
+            continue
+        a, b = json.load(open(p))["ae_sweep"], json.load(open(q))["ae_sweep"]
+        t_new += a.get("elapsed_s", 0.0)
+        t_old += b.get("elapsed_s", 0.0)
+        fa, fb = flat({k: a[k] for k in ("metrics", "sharpe_ante", "sharpe_post", "turnover")}), \
+            flat({k: b[k] for k in ("metrics", "sharpe_ante", "sharpe_post", "turnover")})
+        d = max((abs(fa[k] - fb[k]) for k in fa if k in fb and fa[k] == fa[k] and fb[k] == fb[k]), default=0.0)
+        worst = max(worst, d)
+        n += 1
+        exact += d == 0.0
+    print(json.dumps({"sweeps_compared": n, "bitwise_equal_sweeps": exact, "max_abs_diff": worst,
+                      "elapsed_s_new_sum": round(t_new, 2), "elapsed_s_old_sum": round(t_old, 2)}))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    main()
