@@ -15,6 +15,8 @@ if [ "$2" = suite ]; then
 fi
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
+timeout -k 10 300 python -u scripts/bench_small.py --iters 300 > $OUT/small.jsonl 2>&1 || { tail -n 20 $OUT/small.jsonl; exit 1; }
+grep -h '"ms' $OUT/small.jsonl
 for dt in float32 bfloat16; do
   cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/prof_$dt" -o run -- python "$R/bench.py" --steps 3 --warmup 1 --dtype $dt > "$R/$OUT/prof_$dt.log" 2>&1 || { tail "$R/$OUT/prof_$dt.log"; exit 1; }
   cd "$R" && python scripts/prof_summary.py $(find $OUT/prof_$dt -name "*kernel_stats.csv" | head -1) 40 > $OUT/kernel_summary_$dt.txt 2>&1; head -8 $OUT/kernel_summary_$dt.txt
