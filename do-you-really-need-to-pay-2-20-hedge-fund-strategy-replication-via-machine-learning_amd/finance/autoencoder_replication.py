@@ -202,6 +202,7 @@ class AE:
 
     # -- training ------------------------------------------------------------------------------
     def _new_trainer(self) -> AETrainer:
+        self._oos_cache = None  # (predictions of the previous model)
         self.autoencoder = FactorAutoencoder(self._latent_dim, self._x_train.shape[1], seed=self.seed, dtype=torch.float32,
                                              device=self.device)
         return AETrainer(self.autoencoder, device=self.device)
@@ -271,13 +272,21 @@ class AE:
     def model_IS_RMSE(self):
         return rmse(self._x_train, self._predict(self._x_train))
 
+    def _oos_windows(self):
+        """(scaled window, prediction) for every expanding window xt[:i], i = 2 .. len - 1, each scaled by its
+        own refit MinMaxScaler (the reference's OOS loop).  The autoencoder is row-wise, so all windows'
+        rows go through ONE batched prediction (one launch chain instead of one per window and metric);
+        cached until the model is retrained."""
+        if getattr(self, "_oos_cache", None) is None:
+            xt = np.asarray(self._x_test, dtype=np.float64)
+            xrs = [MinMaxScaler().fit_transform(xt[:i]) for i in range(2, len(xt))]
+            pred = self._predict(np.concatenate(xrs, 0)) if xrs else np.zeros((0, xt.shape[1]))
+            cuts = np.cumsum([len(x) for x in xrs])[:-1]
+            self._oos_cache = list(zip(xrs, np.split(pred, cuts)))
+        return self._oos_cache
+
     def _oos(self, metric):
-        xt = np.asarray(self._x_test, dtype=np.float64)
-        seq = []
-        for i in range(2, len(xt)):
-            xr = MinMaxScaler().fit_transform(xt[:i])
-            seq.append(metric(xr, self._predict(xr)))
-        return seq
+        return [metric(xr, p) for xr, p in self._oos_windows()]
 
     def model_OOS_r2(self):
         return self._oos(r2_score)
