@@ -536,6 +536,9 @@ struct Tb4Geo {
   static constexpr size_t smem = (size_t)(4 * 32 * LG + 4 * 32 * LH) * 2;
 };
 
+#ifndef HFREP_BWD_PREFETCH
+#define HFREP_BWD_PREFETCH 1  // BPTT (TG = false): tape slots one step ahead (0: loaded at the top of their step)
+#endif
 template <int H, int ACT, bool DX, bool GEN = false, bool TG = true>
 __global__ void __launch_bounds__(512)
 lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd, const bf16_t* __restrict__ tape,
@@ -547,6 +550,7 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
   using Geo = Tb4Geo<H>;
   constexpr int G = Geo::G, NK = Geo::NK, KP = Geo::KP, LG = Geo::LG, LH = Geo::LH;
   constexpr bool TAIL = Geo::TAIL;
+  constexpr bool PF = !TG && HFREP_BWD_PREFETCH;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* zb = reinterpret_cast<bf16_t*>(smem);  // [2][32][LG]  dz_t
   bf16_t* zdb = zb + 2 * 32 * LG;                 // [2][32][LG]  dzdot_t
@@ -614,19 +618,37 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
       Slot8 cc = ld_slot8(rt, uok, lo8, tape_off(Tn - 1, wt32) + 4 * SLOT_ELEMS);
       Slot8 cdc = {};
       if constexpr (TG) cdc = ld_slot8(rtt, uok, lo8, tape_off(Tn - 1, wt32) + 4 * SLOT_ELEMS);
+      // BPTT (PF): the tape slots of step t - 1 are loaded during step t (registers free at TG = false),
+      // so their HBM latency hides under a whole step instead of under the step's MFMA chain only
+      Slot8 pg[PF ? 4 : 1], pcp = {};
+      if constexpr (PF) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) pg[s] = ld_slot8(rt, uok, lo8, tape_off(Tn - 1, wt32) + s * SLOT_ELEMS);
+        pcp = ld_slot8(rt, uok && Tn > 1, lo8, tape_off(max(Tn - 2, 0), wt32) + 4 * SLOT_ELEMS);
+      }
       __syncthreads();  // (A) LDS free (previous row block stored)
       __syncthreads();  // (B) dH_{T-1} / dHd_{T-1} staged
       for (int t = Tn - 1; t >= 0; --t) {
         const int cb = t & 1, nb = (t + 1) & 1;
         const bool pv = t > 0, live = t < Tn - 1;
         Slot8 tg[4], zd[TG ? 4 : 1], cp, cdp = {};
+        if constexpr (PF) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          tg[s] = ld_slot8(rt, uok, lo8, tape_off(t, wt32) + s * SLOT_ELEMS);
-          if constexpr (TG) zd[s] = ld_slot8(rtt, uok, lo8, tape_off(t, wt32) + s * SLOT_ELEMS);
+          for (int s = 0; s < 4; ++s) {
+            tg[s] = pg[s];
+            pg[s] = ld_slot8(rt, uok && pv, lo8, tape_off(max(t - 1, 0), wt32) + s * SLOT_ELEMS);
+          }
+          cp = pcp;
+          pcp = ld_slot8(rt, uok && t > 1, lo8, tape_off(max(t - 2, 0), wt32) + 4 * SLOT_ELEMS);
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            tg[s] = ld_slot8(rt, uok, lo8, tape_off(t, wt32) + s * SLOT_ELEMS);
+            if constexpr (TG) zd[s] = ld_slot8(rtt, uok, lo8, tape_off(t, wt32) + s * SLOT_ELEMS);
+          }
+          cp = ld_slot8(rt, uok && pv, lo8, tape_off(max(t - 1, 0), wt32) + 4 * SLOT_ELEMS);
+          if constexpr (TG) cdp = ld_slot8(rtt, uok && pv, lo8, tape_off(max(t - 1, 0), wt32) + 4 * SLOT_ELEMS);
         }
-        cp = ld_slot8(rt, uok && pv, lo8, tape_off(max(t - 1, 0), wt32) + 4 * SLOT_ELEMS);
-        if constexpr (TG) cdp = ld_slot8(rtt, uok && pv, lo8, tape_off(max(t - 1, 0), wt32) + 4 * SLOT_ELEMS);
         f32x4 ah[2], ahd[2], ax[2], axd[2];
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
