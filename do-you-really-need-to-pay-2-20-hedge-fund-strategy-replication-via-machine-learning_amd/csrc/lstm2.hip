@@ -964,6 +964,15 @@ struct XPart {
 #ifndef HFREP_FWD4_TAILNOP
 #define HFREP_FWD4_TAILNOP 0
 #endif
+// HFREP_FWD4_TRACE=1 (diagnosis only): every compute lane of the TAN forward writes, per row block, step
+// and wave, a fingerprint of what its row-half-1 cells of rows 4 g + {2, 3} used -- the xor of the five
+// primal-tape words, the accumulator registers 2 and 3 of the four gates, and the resulting h tangent --
+// to a host-given buffer [rb][t][wave][lane] x uint4, so two runs can be compared value by value
+#ifndef HFREP_FWD4_TRACE
+#define HFREP_FWD4_TRACE 0
+#endif
+__device__ uint4* g_fwd4_trace;
+__device__ __forceinline__ uint32_t rotl32(uint32_t v, int r) { return (v << r) | (v >> (32 - r)); }
 #if HFREP_FWD4_DIAG
 __device__ unsigned int g_fwd4_diag[4];  // cells checked, accumulator mismatches, tape mismatches, printed
 __device__ __forceinline__ float late_read(float v) {  // a fresh VALU read of v's register, here
@@ -1189,6 +1198,22 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
               }
               v0 = a0; v1 = a1; v2 = a2; v3 = a3; v4 = cd2; hv = hd2;
             }
+#if HFREP_FWD4_TRACE
+            if constexpr (TAN) {
+              if (m == 1 && p == 1 && g_fwd4_trace) {
+                uint32_t tx = 0, ta = 0, tb = 0;
+#pragma unroll
+                for (int s = 0; s < TAPE_SLOTS; ++s) tx ^= rotl32(tg[s].m1.y, 5 * s);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  ta ^= rotl32(__float_as_uint(acc[q][1][2]), 7 * q);
+                  tb ^= rotl32(__float_as_uint(acc[q][1][3]), 7 * q);
+                }
+                g_fwd4_trace[(((size_t)rb * Tn + t) * NCW + wave) * 64 + lane] =
+                    make_uint4(tx, ta, tb, pk2bf(hv[0], hv[1]));
+              }
+            }
+#endif
             // unconditional: padded unit columns (c in [H, 112)) receive the zeros they must hold
             hnext[rr * LH + c] = f2bf(hv[0]);
             hnext[(rr + 1) * LH + c] = f2bf(hv[1]);
@@ -1250,6 +1275,11 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 // ==========================================================================================
 // host side
 // ==========================================================================================
+// the HFREP_FWD4_TRACE build's fingerprint buffer (nullptr: off)
+void lstm2_fwd4_trace(void* buf) {
+  uint4* p = reinterpret_cast<uint4*>(buf);
+  HFREP_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_fwd4_trace), &p, sizeof(p)));
+}
 // counters of the HFREP_FWD4_DIAG build (zeros otherwise): cells checked, accumulator / tape mismatches
 void lstm2_fwd4_diag(unsigned int out[4], bool reset) {
 #if HFREP_FWD4_DIAG
