@@ -971,6 +971,9 @@ struct XPart {
 #ifndef HFREP_FWD4_TRACE
 #define HFREP_FWD4_TRACE 0
 #endif
+#ifndef HFREP_FWD4_PROBE
+#define HFREP_FWD4_PROBE 0
+#endif
 __device__ uint4* g_fwd4_trace;
 __device__ __forceinline__ uint32_t rotl32(uint32_t v, int r) { return (v << r) | (v >> (32 - r)); }
 #if HFREP_FWD4_DIAG
@@ -1198,6 +1201,20 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
               }
               v0 = a0; v1 = a1; v2 = a2; v3 = a3; v4 = cd2; hv = hd2;
             }
+#if HFREP_FWD4_PROBE
+            // (race A/B: a perturbation at the trace point -- 1: wait for every outstanding load, 2: a
+            // dummy LDS write + lgkmcnt(0), 3: an s_nop block)
+            if constexpr (TAN) {
+              if (m == 1 && p == 1) {
+                if constexpr (HFREP_FWD4_PROBE == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if constexpr (HFREP_FWD4_PROBE == 2) {
+                  *reinterpret_cast<volatile uint32_t*>(trash) = __float_as_uint(hv[0]);
+                  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                }
+                if constexpr (HFREP_FWD4_PROBE == 3) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+              }
+            }
+#endif
 #if HFREP_FWD4_TRACE
             if constexpr (TAN) {
               if (m == 1 && p == 1 && g_fwd4_trace) {
