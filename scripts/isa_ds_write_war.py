@@ -1,5 +1,11 @@
-import re,sys
-sys.path.insert(0,'/root/repo/scripts')
+"""LDS-write data WAR census of gfx950 assembly (hipcc -S output): every ds_write whose DATA register a
+following instruction overwrites within N wait states (before an lgkmcnt(0) wait).  Written for the
+act = sigmoid tangent-forward drift (profiles/r05_race: the hypothesis was refuted).
+usage: python scripts/isa_ds_write_war.py FILE.s [N]"""
+import os
+import re
+import sys
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from isa_mfma_war import regs, written
 def ops_of(t):
     q=t.split(None,1); return q[0], ([o.strip() for o in re.split(r",\s*(?![^\[]*\])", q[1])] if len(q)>1 else [])
