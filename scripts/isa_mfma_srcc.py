@@ -78,8 +78,49 @@ def scan(files):
     return tab, hits
 
 
+def scan_cfg(files, horizon=8):
+    """The same hand-over reached through control flow (a loop back-edge, a wave-uniform branch), which
+    scan() stops at: for every MFMA walk fall-through and branch targets (isa_mfma_hazard's parser) until
+    `horizon` wait states and report a later MFMA of the other bf16 opcode that reads the writer's
+    destination as ANY source below the measured need.  [(path, kernel, writer, reader, ws, crossed)]"""
+    from isa_mfma_hazard import parse, succ, ws_of, operands, allregs
+
+    hits = []
+    for path in files:
+        for kern, (ins, labels) in parse(path).items():
+            for i, l in enumerate(ins):
+                if not l.startswith("v_mfma"):
+                    continue
+                opw = l.split()[0]
+                dst = frozenset(allregs(operands(l)[0]))
+                stack = [(j, 0, False) for j in succ(ins, labels, i)]
+                seen = {}
+                while stack:
+                    j, ws, br = stack.pop()
+                    if j >= len(ins) or ws >= horizon or seen.get((j, br), horizon + 1) <= ws:
+                        continue
+                    seen[(j, br)] = ws
+                    lj = ins[j]
+                    op = lj.split()[0]
+                    ops = operands(lj)
+                    if op.startswith("v_mfma"):
+                        if op != opw and allregs(",".join(ops[1:])) & dst and ws < NEED.get((opw, op), 0):
+                            hits.append((path, kern, l, lj, ws, br))
+                        if allregs(ops[0]) & dst:
+                            continue
+                    elif op.startswith(("v_", "ds_read", "ds_load", "buffer_load", "global_load")) and ops \
+                            and allregs(ops[0]) & dst:
+                        continue  # destination rewritten on this path
+                    crossed = br or op.startswith(("s_branch", "s_cbranch"))
+                    stack += [(q, ws + ws_of(lj), crossed) for q in succ(ins, labels, j)]
+    return hits
+
+
 def main(argv):
     tab, hits = scan(argv)
+    for path, kern, a, b, ws, br in scan_cfg(argv):
+        print(f"{path}: {kern[:80]}: {b} reads {a} after {ws} wait states (through a branch: {br})")
+        hits.append((path, 0, kern, a, b, ws, 5))
     for k in sorted(tab):
         v = tab[k]
         print(f"{k[0]:28s} -> {k[1]:28s} {k[2]:7s} n={len(v):5d} min={min(v):3d} max={max(v):3d}")

@@ -76,6 +76,38 @@ def test_no_cross_opcode_mfma_srcc_hazard(asm_files):
                                for p, ln, fn, a, b, ws, need in hits)
 
 
+def test_no_cross_opcode_mfma_handover_through_branches(asm_files):
+    """isa_mfma_srcc.scan_cfg: the same hand-over reached through a loop back-edge or a wave-uniform branch
+    (which the straight-line scan stops at), any source operand.  Also holds for the diagnosis-only act =
+    sigmoid lstm_fwd4<TAN> build (profiles/r05_race/README.md), so that drift is not this hazard."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import isa_mfma_srcc
+
+    hits = isa_mfma_srcc.scan_cfg(asm_files)
+    assert not hits, "\n".join(f"{k[:60]}: {a} -> {b} ({ws} wait states, branch {br})"
+                               for _, k, a, b, ws, br in hits)
+
+
+def test_cfg_scan_finds_a_back_edge_handover(tmp_path):
+    """The checker itself: a 16-wide tail at the end of a loop body chained into the loop head's 16x16x32
+    through the back-edge is found (2 wait states), the straight-line pair with s_nop 4 is not."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import isa_mfma_srcc
+
+    s = tmp_path / "k.s"
+    s.write_text("_Z1kv:\n"
+                 ".LBB0_1:\n"
+                 "\tv_mfma_f32_16x16x32_bf16 v[0:3], v[8:11], v[12:15], v[0:3]\n"
+                 "\ts_nop 4\n"
+                 "\tv_mfma_f32_16x16x16_bf16 v[0:3], v[16:17], v[18:19], v[0:3]\n"
+                 "\ts_add_u32 s0, s0, 1\n"
+                 "\ts_cbranch_scc1 .LBB0_1\n"
+                 "\ts_endpgm\n"
+                 ".Lfunc_end0:\n")
+    hits = isa_mfma_srcc.scan_cfg([str(s)])
+    assert len(hits) == 1 and hits[0][4] == 2 and hits[0][5] and "16x16x16" in hits[0][2]
+
+
 def test_no_bit_cast_of_vector_elements():
     """Source lint: clang (ROCm 7.2) compiles ``__builtin_bit_cast(T, v[i])`` / ``(T, v.y)`` on an
     ext_vector element as a cast of element 0 (a round-4 split helper written that way gave the fp32
