@@ -108,6 +108,13 @@ __device__ __forceinline__ float act_dy(int act, float y) {
     default: return 1.f;
   }
 }
+// act_dy on a pair, compile-time act (packed-fp32 cell math)
+template <int ACT>
+__device__ __forceinline__ f2_t act_dy2(f2_t y) {
+  if constexpr (ACT == ACT_TANH) return 1.f - y * y;
+  else if constexpr (ACT == ACT_SIGMOID) return y - y * y;
+  else return f2_t{act_dy(ACT, y[0]), act_dy(ACT, y[1])};
+}
 // second derivative expressed through y: needed by the tangent (double-backward) LSTM
 __device__ __forceinline__ float act_d2y(int act, float y) {
   switch (act) {

@@ -445,6 +445,10 @@ struct Slot8 {  // 8 bf16 of one 16x16-layout lane: block m = 0, 1 (rows 16 m + 
     const uint32_t w = m == 0 ? ((i >> 1) ? m0.y : m0.x) : ((i >> 1) ? m1.y : m1.x);
     return (i & 1) ? hi_bf(w) : lo_bf(w);
   }
+  __device__ __forceinline__ f2_t get2(int m, int p) const {  // rows 2 p, 2 p + 1 of block m
+    const uint32_t w = m == 0 ? (p ? m0.y : m0.x) : (p ? m1.y : m1.x);
+    return f2_t{lo_bf(w), hi_bf(w)};
+  }
 };
 #ifndef HFREP_SLOT8_AUX
 #define HFREP_SLOT8_AUX 0  // (race A/B knob: cache-policy bits of the primal-tape loads)
@@ -536,6 +540,15 @@ struct Tb4Geo {
   static constexpr size_t smem = (size_t)(4 * 32 * LG + 4 * 32 * LH) * 2;
 };
 
+#ifndef HFREP_BWD_PK
+#define HFREP_BWD_PK 1  // BPTT (TG = false): packed-fp32 cell math (0: the scalar form)
+#endif
+// a lane's two vertically adjacent bf16 tile values (rows r, r + 1; row stride ld) from one conversion
+__device__ __forceinline__ void st_bf_pair(bf16_t* p, int ld, f2_t v) {
+  const uint32_t w = pk2bf(v[0], v[1]);
+  p[0] = (bf16_t)(w & 0xffffu);
+  p[ld] = (bf16_t)(w >> 16);
+}
 #ifndef HFREP_BWD_PREFETCH
 #define HFREP_BWD_PREFETCH 1  // BPTT (TG = false): tape slots one step ahead (0: loaded at the top of their step)
 #endif
@@ -706,8 +719,37 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
         }
         const bf16_t* dh_t = dhb + cb * 32 * LH;
         const bf16_t* dhd_t = dhdb + cb * 32 * LH;
-        if constexpr (!TG) {
-          // BPTT only (the former lstm_bwd3's contract): dz from the output adjoint and the carried cell adjoint
+        if constexpr (!TG && HFREP_BWD_PK) {
+          // BPTT only (the former lstm_bwd3's contract): dz from the output adjoint and the carried cell adjoint.
+          // Packed: rows 2 p, 2 p + 1 of a lane's four go through v_pk_mul / v_pk_add / v_pk_fma_f32 together,
+          // act(c) as exp2 + rcp without abs / copysign, and the two rows' dz share one v_cvt_pk_bf16_f32
+          // (low half -> row rr, high half -> row rr + 1).  The scalar form issued ~17 VALU per MFMA.
+          constexpr float CS = act_prescale<ACT>();
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+              const int e = 4 * m + 2 * p, rr = 16 * m + 4 * g4 + 2 * p;
+              const f2_t ig = tg[0].get2(m, p), fg = tg[1].get2(m, p), gg = tg[2].get2(m, p), og = tg[3].get2(m, p);
+              const f2_t cv = cc.get2(m, p), cpv = cp.get2(m, p);
+              const f2_t dh = uok ? f2_t{bf2f(dh_t[rr * LH + c]), bf2f(dh_t[(rr + 1) * LH + c])} : f2_t{0.f, 0.f};
+              const f2_t a_h = dh + f2_t{ah[m][2 * p], ah[m][2 * p + 1]};
+              const f2_t ca = act_s2<ACT>(CS * cv);
+              const f2_t dov = a_h * ca;
+              const f2_t dct = f2_t{ac[e], ac[e + 1]} + a_h * og * act_dy2<ACT>(ca);
+              const f2_t an = dct * fg;
+              ac[e] = uok ? an[0] : 0.f;
+              ac[e + 1] = uok ? an[1] : 0.f;
+              if (uok) {
+                bf16_t* zr = zb + cb * 32 * LG + rr * LG + c;
+                st_bf_pair(zr, LG, dct * gg * (ig - ig * ig));
+                st_bf_pair(zr + H, LG, dct * cpv * (fg - fg * fg));
+                st_bf_pair(zr + 2 * H, LG, dct * ig * act_dy2<ACT>(gg));
+                st_bf_pair(zr + 3 * H, LG, dov * (og - og * og));
+              }
+            }
+        } else if constexpr (!TG) {
+          // (scalar form, HFREP_BWD_PK=0)
 #pragma unroll
           for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -896,9 +938,19 @@ __device__ __forceinline__ void tape_image_store(const bf16_t* img, rsrc_t rt, i
   }
 }
 
+// x / h tile row stride (bf16 elements) of the forward: the smallest L >= KP with L % 32 == 16, i.e. a
+// row stride of 8 mod 16 dwords, makes the MFMA A-operand ds_read_b128 (lane l: row l & 15, k-group l >> 4)
+// conflict-free in all four CDNA4 lane groups (4 LDS cycles instead of 8); the 16-wide tail's ds_read_b64
+// becomes 2-way (4 instead of 2), a net 104 -> 64 LDS cycles per wave and step at K = H = 100.  KP + 8
+// (120 at K = 100) was 2-way on every b128 read (PMC: 1.5-1.9 conflict cycles per LDS-active cycle,
+// profiles/r05_pmc).  HFREP_FW4_STRIDE=0 restores KP + 8 for A/B.
+#ifndef HFREP_FW4_STRIDE
+#define HFREP_FW4_STRIDE 1
+#endif
+__host__ __device__ constexpr int fw4_stride(int kp) { return HFREP_FW4_STRIDE ? kp + ((16 - kp % 32) + 32) % 32 : kp + 8; }
 template <int H, int KX>
 struct Fw4Geo {
-  static constexpr int G = 4 * H, KPH = KSplit<H>::KP, LH = KPH + 8;
+  static constexpr int G = 4 * H, KPH = KSplit<H>::KP, LH = fw4_stride(KPH);
 };
 // x tile loader, split over the NP compute waves: part p moves chunks j = p, p + NP, ... of the
 // tile (8-byte chunks if K % 4 == 0, else 2-byte), i.e. one to three loads per lane per step.
@@ -997,7 +1049,7 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
   constexpr int NCW = (H + 15) / 16;
   static_assert(NCW <= 7, "fwd4: H <= 112");
   const int K = KX ? KX : K_rt;
-  const int KP = KX ? KS::KP : (K + 31) & ~31, LX = KP + 8, NKX = KX ? KS::NF : KP / 32;
+  const int KP = KX ? KS::KP : (K + 31) & ~31, LX = fw4_stride(KP), NKX = KX ? KS::NF : KP / 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* xb = reinterpret_cast<bf16_t*>(smem);  // [2][32][LX]
   bf16_t* hb = xb + 2 * 32 * LX;                  // [2][32][LH]
@@ -1336,7 +1388,7 @@ static int persistent_grid(int B) {
 }
 
 static size_t fwd4_smem(int H, int K, bool tape) {  // generous: the 32-rounded extents (>= the tail-split ones)
-  const int LX = ((K + 31) & ~31) + 8, LH = ((H + 31) / 32) * 32 + 8;
+  const int LX = fw4_stride((K + 31) & ~31), LH = fw4_stride(((H + 31) / 32) * 32);  // (>= fw4_stride of the split KP)
   return (size_t)(2 * 32 * LX + 2 * 32 * LH + (tape ? 2 * FW4_STAGE : 0) + 8) * 2;  // + trash
 }
 

@@ -10,7 +10,7 @@ def main(d):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "")[:48]
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")[:72]
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, cs in acc.items():
         print(k)

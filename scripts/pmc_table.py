@@ -21,15 +21,15 @@ def parse(path):
 
 
 def main(paths):
-    print("# kernel                                              MFMA busy  VALU/MFMA  LDS conflict/LDS-active")
+    print("# kernel                                                            MFMA busy  VALU/MFMA  LDS conflict/LDS-active")
     for p in paths:
         for name, d in parse(p).items():
-            if not name.startswith("hfrep::lstmf") or not d.get("SQ_INSTS_MFMA"):
+            if not name.startswith("hfrep::") or not d.get("SQ_INSTS_MFMA"):
                 continue
             busy = d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (1024 * d.get("GRBM_GUI_ACTIVE", 1) / 8)
             vm = d.get("SQ_INSTS_VALU", 0) / d["SQ_INSTS_MFMA"]
             lc = d.get("SQ_LDS_BANK_CONFLICT", 0) / max(d.get("SQ_ACTIVE_INST_LDS", 1), 1)
-            print(f"{name[:52]:52s} {100 * busy:8.1f}%  {vm:9.2f}  {lc:8.2f}")
+            print(f"{name[:66]:66s} {100 * busy:8.1f}%  {vm:9.2f}  {lc:8.2f}")
 
 
 if __name__ == "__main__":
