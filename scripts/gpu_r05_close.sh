@@ -14,3 +14,5 @@ for M in gan wgan_gp; do
 done
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
 python -c "import json; d=json.load(open('$OUT/bench.json')); print(d['value'], d['ms_per_step'], d['bf16']['value'], d['bf16']['ms_per_step'])"
+timeout -k 10 300 python -u scripts/bench_small.py --iters 300 > $OUT/small.jsonl 2>&1 || { tail -n 20 $OUT/small.jsonl; exit 1; }
+grep -h '"ms' $OUT/small.jsonl
