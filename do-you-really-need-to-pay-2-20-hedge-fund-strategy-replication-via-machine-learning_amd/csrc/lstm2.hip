@@ -941,9 +941,10 @@ __device__ __forceinline__ void tape_image_store(const bf16_t* img, rsrc_t rt, i
 // x / h tile row stride (bf16 elements) of the forward: the smallest L >= KP with L % 32 == 16, i.e. a
 // row stride of 8 mod 16 dwords, makes the MFMA A-operand ds_read_b128 (lane l: row l & 15, k-group l >> 4)
 // conflict-free in all four CDNA4 lane groups (4 LDS cycles instead of 8); the 16-wide tail's ds_read_b64
-// becomes 2-way (4 instead of 2), a net 104 -> 64 LDS cycles per wave and step at K = H = 100.  KP + 8
-// (120 at K = 100) was 2-way on every b128 read (PMC: 1.5-1.9 conflict cycles per LDS-active cycle,
-// profiles/r05_pmc).  HFREP_FW4_STRIDE=0 restores KP + 8 for A/B.
+// becomes 2-way (4 instead of 2), a net 104 -> 64 modelled LDS cycles per wave and step at K = H = 100
+// (KP + 8 = 120 was 2-way on every b128 read).  Measured: op times unchanged, and the PMC conflict metric
+// (1.5-1.9 cycles per LDS-active cycle) did not move either -- the counted conflicts are in the other LDS
+// traffic (profiles/r05_pmc/README.md).  HFREP_FW4_STRIDE=0 restores KP + 8 for A/B.
 #ifndef HFREP_FW4_STRIDE
 #define HFREP_FW4_STRIDE 1
 #endif
