@@ -540,6 +540,13 @@ struct Tb4Geo {
   static constexpr size_t smem = (size_t)(4 * 32 * LG + 4 * 32 * LH) * 2;
 };
 
+// BPTT wave priority.  The compute waves 4-6 share a SIMD with waves 0-2 and, being dispatched second,
+// lose VALU arbitration to them on every segment; one s_setprio 1 for them before the loop (no flips
+// inside) measured bwd_dx -3.0 % at K = 100 (2.93 -> 2.84 ms, twice), the other BPTT ops unchanged;
+// flips around each step's MFMA chain (2): unchanged (profiles/r05_bwdpk/prio).  0: off.
+#ifndef HFREP_BWD_PRIO
+#define HFREP_BWD_PRIO 1
+#endif
 #ifndef HFREP_BWD_PK
 #define HFREP_BWD_PK 1  // BPTT (TG = false): packed-fp32 cell math (0: the scalar form)
 #endif
@@ -620,6 +627,10 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
         wt4[j] = (short)f2bf((TAIL && c < K && k < G) ? W[(size_t)min(c, K - 1) * G + min(k, G - 1)] : 0.f);
       }
     }
+    // (HFREP_BWD_PRIO, BPTT only: 1 = the younger compute waves 4-6 at priority 1 for the whole kernel,
+    // 2 = priority 1 around each step's MFMA chain; readfirstlane keeps the guard a scalar branch)
+    if constexpr (!TG && HFREP_BWD_PRIO == 1)
+      if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
     for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
       const int row0 = rb * 32, nr = min(32, B - row0);
       const rsrc_t rt = tape_rsrc(tape, rb, nrb, Tn), rtt = tape_rsrc(ttape, rb, nrb, Tn);
@@ -667,6 +678,7 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
         for (int m = 0; m < 2; ++m) {
           ah[m] = f32x4{0.f, 0.f, 0.f, 0.f}; ahd[m] = ah[m]; ax[m] = ah[m]; axd[m] = ah[m];
         }
+        if constexpr (!TG && HFREP_BWD_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         if (live) {
 #pragma unroll
           for (int m = 0; m < 2; ++m) {
@@ -713,6 +725,7 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
             }
           }
         }
+        if constexpr (!TG && HFREP_BWD_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         if constexpr (DX) {
           store_dx16(ax, rdx, Tn, t + 1, xw && live, nr, K, c, g4);
           if constexpr (TG) store_dx16(axd, rdxd, Tn, t + 1, xw && live, nr, K, c, g4);
