@@ -20,6 +20,7 @@ import concurrent.futures as cf
 import hashlib
 import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -88,8 +89,27 @@ def _digest(paths, extra: str) -> str:
     return h.hexdigest()[:20]
 
 
+_INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _local_headers(src: str) -> list[str]:
+    """The csrc headers ``src`` includes, transitively (``#include "x.h"`` lines): a TU's stamp depends
+    on exactly these, so a new header only rebuilds the TUs that include it."""
+    seen, todo = [], [src]
+    while todo:
+        with open(todo.pop(), encoding="utf-8", errors="replace") as fh:
+            text = fh.read()
+        for name in _INC.findall(text):
+            p = os.path.join(CSRC, name)
+            if os.path.exists(p) and p not in seen:
+                seen.append(p)
+                todo.append(p)
+    return sorted(seen)
+
+
 def _compile(src, obj, flags, headers):
     stamp = obj + ".stamp"
+    headers = [h for h in headers if h in set(_local_headers(src))]
     dig = _digest([src] + headers, " ".join(flags))
     if os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == dig:
         return obj, False

@@ -1,0 +1,63 @@
+// Fused MLP-GAN passes (csrc/mlp.hip): host launchers for BASELINE configs 3 / 4 (the vanilla GAN of
+// GAN/GAN.py and the MLP WGAN-GP of GAN/WGAN_GP.py).  Included only by mlp.hip and bindings.cpp.
+//
+// Every launcher takes the fp32 master weights (Keras layout: kernel (in, out), row-major) and
+// activations of dtype `dt` (DT_F32 / DT_BF16) as row-major (M, features) matrices, M = B * T rows.
+// F is the feature count of the data windows, H the hidden width; supported: (F, H) in
+// {(32, 100), (36, 100)} (mlp_supported).  `slab` arguments are per-wave partial sums
+// (mlp_slab_rows(M) rows) reduced by launch_mlp_finish in a fixed order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hfrep {
+
+bool mlp_supported(int F, int H);
+// rows of every per-wave partial-sum slab a launch over M rows writes (grid x waves per block)
+int mlp_slab_rows(int64_t M);
+
+// G(noise): Dense(H, sigmoid) -> LReLU -> LN -> Dense(H, sigmoid) -> LReLU -> LN -> Dense(F)
+struct MlpGen {
+  const float *W1, *b1, *g1, *be1, *W2, *b2, *g2, *be2, *W3, *b3;
+};
+// critic / discriminator: Dense(H) -> Dense(H) -> head; head 0 = Flatten -> Dense(1) over T rows
+// (w3: T*H), head 1 = per-row Dense(1, sigmoid) (w3: H)
+struct MlpCritic {
+  const float *W1, *b1, *W2, *b2, *w3, *b3;
+};
+
+void launch_mlp_gen_fwd(int dt, const void* noise, const MlpGen& g, void* out, int64_t M, int F, int H,
+                        hipStream_t s);
+// per-row squared norm of the linear critic's input gradient dD/dx (head 0): gsq (M) fp32
+void launch_mlp_wgp_norm(int dt, const MlpCritic& c, float* gsq, int64_t M, int Tn, int F, int H, hipStream_t s);
+// per-sample GP coefficient c_b = -(2 lam / B)(1 - |g_b|) / |g_b| and (1 - |g_b|)^2
+void launch_mlp_wgp_coef(const float* gsq, int Tn, int64_t B, float lam, float* c, float* e, hipStream_t s);
+// the WGAN-GP critic step of the linear critic on one row tile: W terms on real / fake and the
+// reverse-over-tangent GP term, as combined wgrad operands (see mlp.hip)
+void launch_mlp_wgp_critic(int dt, const void* real, const void* fake, const float* c, const MlpCritic& cr,
+                           void* X2c, void* dY2, void* X1c, void* dY1, void* Y3c, float* slab, int64_t M, int Tn,
+                           int F, int H, hipStream_t s);
+// critic input gradient for the generator step: dx = dL/dx with the Wasserstein (head 0, label -1)
+// or BCE (head 1, label `label`) loss; slab: loss partials
+void launch_mlp_critic_dx(int dt, int head, const void* x, const MlpCritic& cr, float label, void* dx, float* slab,
+                          int64_t M, int Tn, int F, int H, hipStream_t s);
+// discriminator update of the vanilla GAN (head 1, BCE with label `label`): wgrad operands
+// h1 (X of W2), dh2 (dY of W2), dh1 (dY of W1), h2 (X of w3), dz3 (dY of w3); slab: loss partials
+void launch_mlp_gan_critic(int dt, const void* x, const MlpCritic& cr, float label, void* h1, void* dh2, void* dh1,
+                           void* h2, void* dz3, float* slab, int64_t M, int F, int H, hipStream_t s);
+// generator reverse pass from dfake: wgrad operands dz1 (dY of W1), u1 (X of W2), dz2 (dY of W2),
+// u2 (X of W3); LayerNorm parameter partials lnslab (mlp_slab_rows(M) x 4H: dgamma1, dbeta1,
+// dgamma2, dbeta2)
+void launch_mlp_gen_bwd(int dt, const void* noise, const void* dfake, const MlpGen& g, void* dz1, void* u1,
+                        void* dz2, void* u2, float* lnslab, int64_t M, int F, int H, hipStream_t s);
+// fixed-order reduction of a loss slab (P rows x 2) and optional per-sample e (n_e values) into
+// out[4]: mode 0 = WGAN-GP critic pack [w_real + w_fake + lam pen, w_real, w_fake, pen];
+// mode 1 = generator loss [loss, 0, 0, 0] (W: -mean score; BCE: mean); mode 2 = BCE segment loss [loss, 0, 0, 0]
+void launch_mlp_finish(const float* slab, int P, const float* e, int64_t n_e, int mode, float invB, const float* b3,
+                       float lam, float* out, hipStream_t s);
+// fixed-order column sums of a (P, L) slab added into out[L]; the 4-segment form adds segment k of
+// every (P, 4 L) slab row into o_k (nullptr: skipped)
+void launch_mlp_slab_sum(const float* slab, int P, int L, float* out, hipStream_t s);
+void launch_mlp_slab_sum4(const float* slab, int P, int L, float* o0, float* o1, float* o2, float* o3, hipStream_t s);
+
+}  // namespace hfrep

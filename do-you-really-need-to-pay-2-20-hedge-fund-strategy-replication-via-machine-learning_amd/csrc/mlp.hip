@@ -1,0 +1,1033 @@
+// Fused MLP-GAN passes for gfx950: BASELINE configs 3 / 4 (vanilla GAN, GAN/GAN.py:127-204, and the
+// MLP WGAN-GP, GAN/WGAN_GP.py:221-288) as one kernel per pass instead of one kernel per layer.
+//
+// The layer-by-layer engine (models/layers.py) round-tripped every (B*T, 100) activation and adjoint
+// through HBM: 607 GB per bf16 WGAN-GP iteration at 2.3 TB/s (profiles/r06_mlp/baseline).  Here a
+// wave owns 32 rows and carries them through every layer of the pass in registers:
+//
+//  * transposed orientation: a layer output is held as Y^T (features x rows) in f32x16 accumulators,
+//    32 features per tile, row = lane & 31; register q of lane half h is feature 8(q>>2) + 4h + (q&3).
+//    The next layer sums over that feature index, so the accumulator IS its B operand (CDNA4 guide
+//    §3 "An accumulator tile as the next MFMA's operand"): bf16 packs registers 8s..8s+7 into the
+//    k-step s fragment of v_mfma_f32_32x32x16_bf16, fp32 feeds register r straight into k-step r of the
+//    exact v_mfma_f32_32x32x2_f32.  No LDS round trip between layers.
+//  * the weights live in LDS as pre-permuted A-fragment images (one ds_read_b128 / b32 per MFMA, lane
+//    linear, conflict free), built per workgroup from the fp32 master weights in the prologue: a
+//    forward image A[o][k = i] and, where the pass goes backwards, a dgrad image A[i][k = o], both with
+//    the k order of the accumulator map above.
+//  * LayerNorm, bias, sigmoid / LeakyReLU and the per-row head dot are register epilogues: a row's
+//    features sit in one lane's registers plus its lane ^ 32 partner, so every row reduction is 16
+//    in-lane adds and one cross-half swap.
+//  * only the pass's inputs and outputs touch HBM: noise / windows in, fake windows, the weight-
+//    gradient operands (consumed by the streaming wgrad kernels) and per-wave loss partials out.
+//
+// The WGAN-GP critic of WGAN_GP.py (Dense(100) -> Dense(100) -> Flatten -> Dense(1), all linear) gets a
+// specialised step kernel (mlp_wgp_*): for an affine critic the W-terms on real / fake and the
+// reverse-over-tangent of the gradient penalty all have adjoints along the same head vector w3_t, so
+// their weight-gradient operands are summed per row before they leave the kernel (X2c, X1c, Y3c
+// below) and each weight gets ONE streaming wgrad instead of three.
+#include "common.h"
+#include "kernels.h"
+#include "mfma.h"
+#include "mlp.h"
+
+#include <algorithm>
+
+namespace hfrep {
+
+namespace {
+
+constexpr int MLP_WAVES = 4;  // waves per workgroup (one per SIMD; up to 512 registers per wave)
+constexpr int MLP_THREADS = 64 * MLP_WAVES;
+constexpr int VEC = 128;      // padded length of every per-feature vector in LDS
+constexpr float LN_EPS_F = 1e-3f, LRELU_ALPHA_F = 0.2f, KERAS_EPS_F = 1e-7f;
+
+__device__ __forceinline__ int featq(int q, int h) { return 8 * (q >> 2) + 4 * h + (q & 3); }
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------------------------
+// precision policies: k-step structure of the two MFMA forms over the accumulator feature map
+// ---------------------------------------------------------------------------------------------------
+template <typename T> struct MP;
+
+template <> struct MP<bf16_t> {
+  typedef bf16x8 frag;
+  static constexpr int steps(int K) { return (K + 15) / 16; }
+  // input feature of element e (0..7) of k-step s, lane half h
+  __device__ __forceinline__ static int feat(int s, int e, int h) { return 32 * (s >> 1) + featq(8 * (s & 1) + e, h); }
+  __device__ __forceinline__ static frag bop(const f32x16* a, int s) {
+    const f32x16& t = a[s >> 1];
+    const int o = 8 * (s & 1);
+    const u32x4_t u = {pk2bf(t[o], t[o + 1]), pk2bf(t[o + 2], t[o + 3]), pk2bf(t[o + 4], t[o + 5]),
+                       pk2bf(t[o + 6], t[o + 7])};
+    return __builtin_bit_cast(frag, u);
+  }
+  template <class G> __device__ __forceinline__ static frag make(G get) {
+    const u32x4_t u = {pk2bf(get(0), get(1)), pk2bf(get(2), get(3)), pk2bf(get(4), get(5)), pk2bf(get(6), get(7))};
+    return __builtin_bit_cast(frag, u);
+  }
+};
+
+template <> struct MP<float> {
+  typedef float frag;
+  // k-steps over K features: whole 32-feature tiles take 16, the last partial tile the prefix of
+  // registers whose lane-half-0 feature is < K (featq(r, 0) increases with r)
+  static constexpr int steps(int K) {
+    int n = 16 * (K / 32);
+    const int rem = K % 32;
+    for (int r = 0; r < 16; ++r)
+      if (rem && 8 * (r >> 2) + (r & 3) < rem) ++n;
+    return n;
+  }
+  __device__ __forceinline__ static int feat(int s, int /*e*/, int h) { return 32 * (s >> 4) + featq(s & 15, h); }
+  __device__ __forceinline__ static frag bop(const f32x16* a, int s) { return a[s >> 4][s & 15]; }
+  template <class G> __device__ __forceinline__ static frag make(G get) { return get(0); }
+};
+
+// ---------------------------------------------------------------------------------------------------
+// LDS images (built by the whole workgroup in the prologue)
+// ---------------------------------------------------------------------------------------------------
+// forward image of W (K x N, row-major fp32): entry (t, s) = A fragment rows o = 32 t .. +31, k-step s
+template <typename T, int K, int N>
+__device__ void build_fwd(typename MP<T>::frag* img, const float* __restrict__ W) {
+  constexpr int S = MP<T>::steps(K), NT = (N + 31) / 32;
+  for (int e = threadIdx.x; e < NT * S * 64; e += blockDim.x) {
+    const int lane = e & 63, idx = e >> 6, t = idx / S, s = idx - t * S;
+    const int o = 32 * t + (lane & 31), h = lane >> 5;
+    img[e] = MP<T>::make([&](int j) {
+      const int i = MP<T>::feat(s, j, h);
+      return (i < K && o < N) ? W[i * N + o] : 0.f;
+    });
+  }
+}
+// dgrad image of W (K x N): entry (t, s) = A fragment rows i = 32 t .. +31 (input features), k-step s
+// over the N output features
+template <typename T, int K, int N>
+__device__ void build_dgrad(typename MP<T>::frag* img, const float* __restrict__ W) {
+  constexpr int S = MP<T>::steps(N), NT = (K + 31) / 32;
+  for (int e = threadIdx.x; e < NT * S * 64; e += blockDim.x) {
+    const int lane = e & 63, idx = e >> 6, t = idx / S, s = idx - t * S;
+    const int i = 32 * t + (lane & 31), h = lane >> 5;
+    img[e] = MP<T>::make([&](int j) {
+      const int o = MP<T>::feat(s, j, h);
+      return (i < K && o < N) ? W[i * N + o] : 0.f;
+    });
+  }
+}
+template <typename T, int K, int N> constexpr int fwd_entries() { return ((N + 31) / 32) * MP<T>::steps(K); }
+template <typename T, int K, int N> constexpr int dgrad_entries() { return ((K + 31) / 32) * MP<T>::steps(N); }
+template <typename T> constexpr int frag_bytes() { return 64 * (int)sizeof(typename MP<T>::frag); }
+
+__device__ void load_vec(float* dst, const float* __restrict__ src, int n) {
+  for (int i = threadIdx.x; i < VEC; i += blockDim.x) dst[i] = (src && i < n) ? src[i] : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// register-level building blocks
+// ---------------------------------------------------------------------------------------------------
+// out[t] = sum over the KIN input features of img (t, s) x in: one output tile per 32 features of NOUT
+// The A fragments of step s + 1 are read while step s's MFMAs issue; the scheduling barrier per step
+// keeps hipcc from hoisting the whole image into registers (it did: 208 VGPRs for the fp32 100 x 100
+// layer, and spills everywhere).
+template <typename T, int KIN, int NOUT>
+__device__ __forceinline__ void dense(const f32x16* in, f32x16* out, const typename MP<T>::frag* img, int lane) {
+  constexpr int S = MP<T>::steps(KIN), NT = (NOUT + 31) / 32;
+  typedef typename MP<T>::frag Fr;
+  Fr cur[NT], nxt[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    out[t] = zero16();
+    cur[t] = img[(t * S) * 64 + lane];
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (s + 1 < S) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) nxt[t] = img[(t * S + s + 1) * 64 + lane];
+    }
+    const Fr b = MP<T>::bop(in, s);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) out[t] = MF<T>::mma(cur[t], b, out[t]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) cur[t] = nxt[t];
+  }
+}
+
+// 4 consecutive elements of a row (feature f0 .. f0 + 3), as floats
+template <typename T> struct Q4;
+template <> struct Q4<bf16_t> {
+  __device__ __forceinline__ static float4 ld(const bf16_t* p) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
+                       __uint_as_float(v.y & 0xffff0000u));
+  }
+  __device__ __forceinline__ static void st(bf16_t* p, float a, float b, float c, float d) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pk2bf(a, b), pk2bf(c, d));
+  }
+};
+template <> struct Q4<float> {
+  __device__ __forceinline__ static float4 ld(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  __device__ __forceinline__ static void st(float* p, float a, float b, float c, float d) {
+    *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+  }
+};
+
+// rows (M x K row-major) -> accumulator layout (zeros past M / K)
+template <typename T, int K>
+__device__ __forceinline__ void load_rows(f32x16* a, const T* __restrict__ x, int64_t row, int64_t M, int h) {
+  constexpr int NT = (K + 31) / 32;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * t + 8 * g + 4 * h;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < M && f0 < K) v = Q4<T>::ld(x + row * K + f0);
+      a[t][4 * g] = v.x; a[t][4 * g + 1] = v.y; a[t][4 * g + 2] = v.z; a[t][4 * g + 3] = v.w;
+    }
+}
+template <typename T, int N>
+__device__ __forceinline__ void store_rows(T* __restrict__ y, int64_t row, int64_t M, const f32x16* a, int h) {
+  constexpr int NT = (N + 31) / 32;
+  if (row >= M) return;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * t + 8 * g + 4 * h;
+      if (f0 < N) Q4<T>::st(y + row * N + f0, a[t][4 * g], a[t][4 * g + 1], a[t][4 * g + 2], a[t][4 * g + 3]);
+    }
+}
+// a per-row head vector (w: this row's N weights, fp32) scaled by `sc`, in accumulator layout
+template <int N>
+__device__ __forceinline__ void head_rows(f32x16* a, const float* __restrict__ w, float sc, bool ok, int h) {
+  constexpr int NT = (N + 31) / 32;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * t + 8 * g + 4 * h;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok && f0 < N) v = *reinterpret_cast<const float4*>(w + f0);
+      a[t][4 * g] = sc * v.x; a[t][4 * g + 1] = sc * v.y; a[t][4 * g + 2] = sc * v.z; a[t][4 * g + 3] = sc * v.w;
+    }
+}
+// sum_f a[row, f] * w[f] for this lane's row (both lane halves get the total)
+template <int N>
+__device__ __forceinline__ float rowdot(const f32x16* a, const float* __restrict__ w, bool ok, int h) {
+  constexpr int NT = (N + 31) / 32;
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * t + 8 * g + 4 * h;
+      if (ok && f0 < N) {
+        const float4 v = *reinterpret_cast<const float4*>(w + f0);
+        s = fmaf(a[t][4 * g], v.x, s); s = fmaf(a[t][4 * g + 1], v.y, s);
+        s = fmaf(a[t][4 * g + 2], v.z, s); s = fmaf(a[t][4 * g + 3], v.w, s);
+      }
+    }
+  return s + __shfl_xor(s, 32, 64);
+}
+// a = act(a + b) on features < N, 0 past N (b: LDS vector)
+template <int N>
+__device__ __forceinline__ void bias_act(f32x16* a, const float* b, int act, int h) {
+  constexpr int NT = (N + 31) / 32;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * t + 8 * g + 4 * h;
+      const float4 bv = *reinterpret_cast<const float4*>(b + f0);
+      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = a[t][4 * g + e] + bb[e];
+        v = act == ACT_SIGMOID ? sigmoidf_(v) : v;
+        a[t][4 * g + e] = f0 + e < N ? v : 0.f;
+      }
+    }
+}
+template <int N>
+__device__ __forceinline__ void axpy(f32x16* y, float s, const f32x16* x) {
+#pragma unroll
+  for (int t = 0; t < (N + 31) / 32; ++t) y[t] += s * x[t];
+}
+__device__ __forceinline__ float lrelu(float v) { return v >= 0.f ? v : LRELU_ALPHA_F * v; }
+
+// LeakyReLU then LayerNorm (eps 1e-3, biased variance) of this lane's row, in place; a holds the
+// activation outputs with zeros past N.  Returns the row statistics.
+template <int N>
+__device__ __forceinline__ void lrelu_ln(f32x16* a, const float* gam, const float* bet, int h, float& mean,
+                                         float& rstd) {
+  constexpr int NT = (N + 31) / 32;
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      a[t][q] = lrelu(a[t][q]);
+      s += a[t][q];
+    }
+  s += __shfl_xor(s, 32, 64);
+  mean = s * (1.f / N);
+  float v = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float d = 32 * t + featq(q, h) < N ? a[t][q] - mean : 0.f;
+      v = fmaf(d, d, v);
+    }
+  v += __shfl_xor(v, 32, 64);
+  rstd = 1.f / sqrtf(v * (1.f / N) + LN_EPS_F);
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * t + 8 * g + 4 * h;
+      const float4 gv = *reinterpret_cast<const float4*>(gam + f0), bv = *reinterpret_cast<const float4*>(bet + f0);
+      const float gg[4] = {gv.x, gv.y, gv.z, gv.w}, bb[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float u = (a[t][4 * g + e] - mean) * rstd * gg[e] + bb[e];
+        a[t][4 * g + e] = f0 + e < N ? u : 0.f;
+      }
+    }
+}
+
+// Sum over the 32 rows of one lane half of every feature of tile v (transpose-reduce butterfly: 16
+// shuffles instead of 80).  Lane l ends with the column sum of register q(l) = 8 b4 + 4 b3 + 2 b2 + b1
+// (bk = bit k of l), i.e. feature featq(q(l), h); lanes l and l ^ 1 hold the same value.
+__device__ __forceinline__ float colsum(const f32x16& v, int lane) {
+  float a8[8], a4[4], a2[2];
+  bool b = lane & 16;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a8[i] = (b ? v[8 + i] : v[i]) + __shfl_xor(b ? v[i] : v[8 + i], 16, 64);
+  b = lane & 8;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a4[i] = (b ? a8[4 + i] : a8[i]) + __shfl_xor(b ? a8[i] : a8[4 + i], 8, 64);
+  b = lane & 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) a2[i] = (b ? a4[2 + i] : a4[i]) + __shfl_xor(b ? a4[i] : a4[2 + i], 4, 64);
+  b = lane & 2;
+  float a1 = (b ? a2[1] : a2[0]) + __shfl_xor(b ? a2[0] : a2[1], 2, 64);
+  return a1 + __shfl_xor(a1, 1, 64);
+}
+__device__ __forceinline__ int colsum_q(int lane) {
+  return (((lane >> 4) & 1) << 3) | (((lane >> 3) & 1) << 2) | (((lane >> 2) & 1) << 1) | ((lane >> 1) & 1);
+}
+
+// per-wave partial sums -> slab row of this wave
+__device__ __forceinline__ void slab_put(float* slab, int L, int k, float v) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) slab[((int64_t)blockIdx.x * MLP_WAVES + (threadIdx.x >> 6)) * L + k] = v;
+}
+
+// Keras binary cross-entropy on a probability p with label y, its p-gradient scaled by inv
+// (zero where the [eps, 1 - eps] clip is active): the gan_loss kind-1 contract (ops/reference.py)
+__device__ __forceinline__ void bce(float p, float y, float inv, float& lo, float& g) {
+  const float o = fminf(fmaxf(p, KERAS_EPS_F), 1.f - KERAS_EPS_F);
+  lo = -(y * __logf(o + KERAS_EPS_F) + (1.f - y) * __logf(1.f - o + KERAS_EPS_F));
+  const bool inside = p > KERAS_EPS_F && p < 1.f - KERAS_EPS_F;
+  g = inside ? -(y / (o + KERAS_EPS_F) - (1.f - y) / (1.f - o + KERAS_EPS_F)) * inv : 0.f;
+}
+
+#define MLP_LOOP                                                                                               \
+  const int lane = threadIdx.x & 63, h = lane >> 5;                                                            \
+  const int64_t ntile = (M + 31) / 32;                                                                         \
+  for (int64_t tile = (int64_t)blockIdx.x * MLP_WAVES + (threadIdx.x >> 6); tile < ntile;                      \
+       tile += (int64_t)gridDim.x * MLP_WAVES)
+
+}  // namespace
+
+// ===================================================================================================
+// generator forward: noise -> fake (GAN/WGAN_GP.py:221-236 build_generator)
+// ===================================================================================================
+template <typename T, int F, int H>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_gen_fwd_kernel(const T* __restrict__ z, MlpGen g,
+                                                                  T* __restrict__ out, int64_t M) {
+  using Fr = typename MP<T>::frag;
+  constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  Fr* i1 = reinterpret_cast<Fr*>(lds);
+  Fr* i2 = i1 + fwd_entries<T, F, H>() * 64;
+  Fr* i3 = i2 + fwd_entries<T, H, H>() * 64;
+  float* vec = reinterpret_cast<float*>(i3 + fwd_entries<T, H, F>() * 64);
+  build_fwd<T, F, H>(i1, g.W1);
+  build_fwd<T, H, H>(i2, g.W2);
+  build_fwd<T, H, F>(i3, g.W3);
+  load_vec(vec + 0 * VEC, g.b1, H); load_vec(vec + 1 * VEC, g.g1, H); load_vec(vec + 2 * VEC, g.be1, H);
+  load_vec(vec + 3 * VEC, g.b2, H); load_vec(vec + 4 * VEC, g.g2, H); load_vec(vec + 5 * VEC, g.be2, H);
+  load_vec(vec + 6 * VEC, g.b3, F);
+  __syncthreads();
+  MLP_LOOP {
+    const int64_t row = tile * 32 + (lane & 31);
+    f32x16 x[NTF], a[NTH], b[NTH];
+    float mean, rstd;
+    load_rows<T, F>(x, z, row, M, h);
+    dense<T, F, H>(x, a, i1, lane);
+    bias_act<H>(a, vec + 0 * VEC, ACT_SIGMOID, h);
+    lrelu_ln<H>(a, vec + 1 * VEC, vec + 2 * VEC, h, mean, rstd);
+    dense<T, H, H>(a, b, i2, lane);
+    bias_act<H>(b, vec + 3 * VEC, ACT_SIGMOID, h);
+    lrelu_ln<H>(b, vec + 4 * VEC, vec + 5 * VEC, h, mean, rstd);
+    dense<T, H, F>(b, x, i3, lane);
+    bias_act<F>(x, vec + 6 * VEC, ACT_LINEAR, h);
+    store_rows<T, F>(out, row, M, x, h);
+  }
+}
+
+// ===================================================================================================
+// WGAN-GP critic (GAN/WGAN_GP.py:238-253): D(x) = sum_t ((x_t W1 + b1) W2 + b2) . w3_t + b3
+// ===================================================================================================
+// First-order GP pass: g = dD/dx at every row (for an affine critic it does not depend on x:
+// dh2 = w3_t, dh1 = W2 dh2, g = W1 dh1) and its squared norm per row.
+template <typename T, int F, int H>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_wgp_norm_kernel(MlpCritic c, float* __restrict__ gsq, int64_t M,
+                                                                   int Tn) {
+  using Fr = typename MP<T>::frag;
+  constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  Fr* d2 = reinterpret_cast<Fr*>(lds);
+  Fr* d1 = d2 + dgrad_entries<T, H, H>() * 64;
+  build_dgrad<T, H, H>(d2, c.W2);
+  build_dgrad<T, F, H>(d1, c.W1);
+  __syncthreads();
+  MLP_LOOP {
+    const int64_t row = tile * 32 + (lane & 31);
+    const bool ok = row < M;
+    const int tr = ok ? (int)(row % Tn) : 0;
+    f32x16 a[NTH], b[NTH], gg[NTF];
+    head_rows<H>(a, c.w3 + (int64_t)tr * H, 1.f, ok, h);
+    dense<T, H, H>(a, b, d2, lane);
+    dense<T, H, F>(b, gg, d1, lane);
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTF; ++t)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s = fmaf(gg[t][q], gg[t][q], s);
+    s += __shfl_xor(s, 32, 64);
+    if (ok && h == 0) gsq[row] = s;
+  }
+}
+
+// per sample: |g_b| from the T row norms, c_b = -(2 lam / B)(1 - |g_b|) / |g_b| (the gp_coef adjoint,
+// ops/reference.py) and e_b = (1 - |g_b|)^2
+__global__ void __launch_bounds__(256) mlp_wgp_coef_kernel(const float* __restrict__ gsq, int Tn, int64_t B, float lam,
+                                                           float* __restrict__ c, float* __restrict__ e) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  float s = 0.f;
+  for (int t = 0; t < Tn; ++t) s += gsq[b * Tn + t];
+  const float n = sqrtf(s);
+  c[b] = -(2.f * lam / (float)B) * (1.f - n) / fmaxf(n, 1e-30f);
+  e[b] = (1.f - n) * (1.f - n);
+}
+
+// One GP critic update's device work per row (b, t):
+//   W terms: dL/ds_b = -1/B (real), +1/B (fake)  ->  dh2 = +-w3_t / B, dh1 = +-W2 w3_t / B
+//   GP term (reverse over the tangent along v = c_b g): zd1 = v W1, zd2 = zd1 W2; seeds dzd2 = w3_t,
+//   dzd1 = W2 w3_t
+// Every adjoint of layer 2 is along w3_t and every adjoint of layer 1 along dh1' = W2 w3_t, so each
+// weight needs one product with a per-row combined operand:
+//   gW2 += X2c^T dY2,  X2c = (h1_fake - h1_real) / B + zd1,  dY2 = w3_t
+//   gW1 += X1c^T dY1,  X1c = (x_fake - x_real) / B + v,      dY1 = dh1' = W2 w3_t
+//   gw3_t += sum_b Y3c,  Y3c = (h2_fake - h2_real) / B + zd2 = X2c W2   (the b2 terms cancel)
+// The bias gradients cancel exactly (-1/B and +1/B per row pair; the tangent has none).  slab: per-wave
+// sums of h2 . w3_t over the real and the fake rows (the two W losses).
+template <typename T, int F, int H>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_wgp_critic_kernel(
+    const T* __restrict__ real, const T* __restrict__ fake, const float* __restrict__ cvec, MlpCritic c,
+    T* __restrict__ X2c, T* __restrict__ dY2, T* __restrict__ X1c, T* __restrict__ dY1, T* __restrict__ Y3c,
+    float* __restrict__ slab, int64_t M, int Tn, float invB) {
+  using Fr = typename MP<T>::frag;
+  constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  Fr* f1 = reinterpret_cast<Fr*>(lds);
+  Fr* f2 = f1 + fwd_entries<T, F, H>() * 64;
+  Fr* d2 = f2 + fwd_entries<T, H, H>() * 64;
+  Fr* d1 = d2 + dgrad_entries<T, H, H>() * 64;
+  float* vec = reinterpret_cast<float*>(d1 + dgrad_entries<T, F, H>() * 64);
+  build_fwd<T, F, H>(f1, c.W1);
+  build_fwd<T, H, H>(f2, c.W2);
+  build_dgrad<T, H, H>(d2, c.W2);
+  build_dgrad<T, F, H>(d1, c.W1);
+  load_vec(vec, c.b1, H);
+  load_vec(vec + VEC, c.b2, H);
+  __syncthreads();
+  float sr = 0.f, sf = 0.f;
+  MLP_LOOP {
+    const int64_t row = tile * 32 + (lane & 31);
+    const bool ok = row < M;
+    const int64_t bidx = ok ? row / Tn : 0;
+    const float* w3t = c.w3 + (int64_t)(ok ? row - bidx * Tn : 0) * H;
+    f32x16 A[NTH], Bv[NTH], X2[NTH], X1[NTF], x[NTF];
+    // ---- GP tangent stream
+    head_rows<H>(A, w3t, 1.f, ok, h);
+    store_rows<T, H>(dY2, row, M, A, h);
+    dense<T, H, H>(A, Bv, d2, lane);           // dh1' = W2 w3_t
+    store_rows<T, H>(dY1, row, M, Bv, h);
+    dense<T, H, F>(Bv, X1, d1, lane);          // g = W1 dh1'
+    const float cb = ok ? cvec[bidx] : 0.f;
+#pragma unroll
+    for (int t = 0; t < NTF; ++t) X1[t] *= cb;  // v
+    dense<T, F, H>(X1, X2, f1, lane);          // zd1 = v W1
+    // ---- W terms: real (-1/B) then fake (+1/B)
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const float sg = pass ? invB : -invB;
+      load_rows<T, F>(x, pass ? fake : real, row, M, h);
+      axpy<F>(X1, sg, x);
+      dense<T, F, H>(x, A, f1, lane);
+      bias_act<H>(A, vec, ACT_LINEAR, h);      // h1
+      axpy<H>(X2, sg, A);
+      dense<T, H, H>(A, Bv, f2, lane);
+      bias_act<H>(Bv, vec + VEC, ACT_LINEAR, h);  // h2
+      const float sc = rowdot<H>(Bv, w3t, ok, h);
+      if (ok && h == 0) {
+        if (pass) sf += sc;
+        else sr += sc;
+      }
+    }
+    store_rows<T, F>(X1c, row, M, X1, h);
+    store_rows<T, H>(X2c, row, M, X2, h);
+    dense<T, H, H>(X2, A, f2, lane);           // Y3c = X2c W2
+    store_rows<T, H>(Y3c, row, M, A, h);
+  }
+  slab_put(slab, 2, 0, sr);
+  slab_put(slab, 2, 1, sf);
+}
+
+// ===================================================================================================
+// critic input gradient for the generator step (and its loss): head 0 = the linear WGAN-GP critic
+// with W(fake, -1) (GAN/WGAN_GP.py:178-189), head 1 = the GAN discriminator Dense -> Dense ->
+// Dense(1, sigmoid) per row with BCE(label) (GAN/GAN.py:144-158, 195-198)
+// ===================================================================================================
+template <typename T, int F, int H, int HEAD>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_critic_dx_kernel(const T* __restrict__ x, MlpCritic c, float label,
+                                                                    T* __restrict__ dx, float* __restrict__ slab,
+                                                                    int64_t M, int Tn, float inv) {
+  using Fr = typename MP<T>::frag;
+  constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  Fr* f1 = reinterpret_cast<Fr*>(lds);
+  Fr* f2 = f1 + fwd_entries<T, F, H>() * 64;
+  Fr* d2 = f2 + fwd_entries<T, H, H>() * 64;
+  Fr* d1 = d2 + dgrad_entries<T, H, H>() * 64;
+  float* vec = reinterpret_cast<float*>(d1 + dgrad_entries<T, F, H>() * 64);
+  build_fwd<T, F, H>(f1, c.W1);
+  build_fwd<T, H, H>(f2, c.W2);
+  build_dgrad<T, H, H>(d2, c.W2);
+  build_dgrad<T, F, H>(d1, c.W1);
+  load_vec(vec, c.b1, H);
+  load_vec(vec + VEC, c.b2, H);
+  __syncthreads();
+  const float b3 = c.b3 ? c.b3[0] : 0.f;
+  float acc = 0.f;
+  MLP_LOOP {
+    const int64_t row = tile * 32 + (lane & 31);
+    const bool ok = row < M;
+    const float* w3t = HEAD == 0 ? c.w3 + (int64_t)(ok ? row % Tn : 0) * H : c.w3;
+    f32x16 A[NTH], Bv[NTH], X[NTF];
+    load_rows<T, F>(X, x, row, M, h);
+    dense<T, F, H>(X, A, f1, lane);
+    bias_act<H>(A, vec, ACT_LINEAR, h);
+    dense<T, H, H>(A, Bv, f2, lane);
+    bias_act<H>(Bv, vec + VEC, ACT_LINEAR, h);
+    const float sc = rowdot<H>(Bv, w3t, ok, h);
+    float dz;
+    if (HEAD == 0) {
+      if (ok && h == 0) acc += sc;
+      dz = -inv;  // d W(fake, -1) / d s_b = -1 / B
+    } else {
+      const float p = sigmoidf_(sc + b3);
+      float lo, gp;
+      bce(p, label, inv, lo, gp);
+      if (ok && h == 0) acc += lo;
+      dz = gp * p * (1.f - p);
+    }
+    head_rows<H>(A, w3t, dz, ok, h);  // dh2
+    dense<T, H, H>(A, Bv, d2, lane);  // dh1
+    dense<T, H, F>(Bv, X, d1, lane);  // dx
+    store_rows<T, F>(dx, row, M, X, h);
+  }
+  slab_put(slab, 2, 0, acc);
+  slab_put(slab, 2, 1, 0.f);
+}
+
+// ===================================================================================================
+// vanilla GAN discriminator update (GAN/GAN.py:187-189): forward, BCE(label) per row, reverse to the
+// weight-gradient operands
+// ===================================================================================================
+template <typename T, int F, int H>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_gan_critic_kernel(const T* __restrict__ x, MlpCritic c, float label,
+                                                                     T* __restrict__ h1o, T* __restrict__ dh2o,
+                                                                     T* __restrict__ dh1o, T* __restrict__ h2o,
+                                                                     T* __restrict__ dz3o, float* __restrict__ slab,
+                                                                     int64_t M, float inv) {
+  using Fr = typename MP<T>::frag;
+  constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  Fr* f1 = reinterpret_cast<Fr*>(lds);
+  Fr* f2 = f1 + fwd_entries<T, F, H>() * 64;
+  Fr* d2 = f2 + fwd_entries<T, H, H>() * 64;
+  float* vec = reinterpret_cast<float*>(d2 + dgrad_entries<T, H, H>() * 64);
+  build_fwd<T, F, H>(f1, c.W1);
+  build_fwd<T, H, H>(f2, c.W2);
+  build_dgrad<T, H, H>(d2, c.W2);
+  load_vec(vec, c.b1, H);
+  load_vec(vec + VEC, c.b2, H);
+  __syncthreads();
+  const float b3 = c.b3 ? c.b3[0] : 0.f;
+  float acc = 0.f;
+  MLP_LOOP {
+    const int64_t row = tile * 32 + (lane & 31);
+    const bool ok = row < M;
+    f32x16 A[NTH], Bv[NTH], X[NTF];
+    load_rows<T, F>(X, x, row, M, h);
+    dense<T, F, H>(X, A, f1, lane);
+    bias_act<H>(A, vec, ACT_LINEAR, h);
+    store_rows<T, H>(h1o, row, M, A, h);
+    dense<T, H, H>(A, Bv, f2, lane);
+    bias_act<H>(Bv, vec + VEC, ACT_LINEAR, h);
+    store_rows<T, H>(h2o, row, M, Bv, h);
+    const float p = sigmoidf_(rowdot<H>(Bv, c.w3, ok, h) + b3);
+    float lo, gp;
+    bce(p, label, inv, lo, gp);
+    const float dz = gp * p * (1.f - p);
+    if (ok && h == 0) {
+      acc += lo;
+      dz3o[row] = Cvt<T>::from_f(dz);
+    }
+    head_rows<H>(A, c.w3, dz, ok, h);
+    store_rows<T, H>(dh2o, row, M, A, h);
+    dense<T, H, H>(A, Bv, d2, lane);
+    store_rows<T, H>(dh1o, row, M, Bv, h);
+  }
+  slab_put(slab, 2, 0, acc);
+  slab_put(slab, 2, 1, 0.f);
+}
+
+// ===================================================================================================
+// generator reverse pass (GAN/WGAN_GP.py:178-189 / GAN/GAN.py:195-198: the combined model's update)
+// from dfake = dL/dG(z): recomputes the forward in registers and writes the weight-gradient operands
+// ===================================================================================================
+template <typename T, int F, int H>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_gen_bwd_kernel(const T* __restrict__ z, const T* __restrict__ dfake,
+                                                                  MlpGen g, T* __restrict__ dz1o, T* __restrict__ u1o,
+                                                                  T* __restrict__ dz2o, T* __restrict__ u2o,
+                                                                  float* __restrict__ lnslab, int64_t M) {
+  using Fr = typename MP<T>::frag;
+  constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  Fr* f1 = reinterpret_cast<Fr*>(lds);
+  Fr* f2 = f1 + fwd_entries<T, F, H>() * 64;
+  Fr* d3 = f2 + fwd_entries<T, H, H>() * 64;
+  Fr* d2 = d3 + dgrad_entries<T, H, F>() * 64;
+  float* vec = reinterpret_cast<float*>(d2 + dgrad_entries<T, H, H>() * 64);
+  build_fwd<T, F, H>(f1, g.W1);
+  build_fwd<T, H, H>(f2, g.W2);
+  build_dgrad<T, H, F>(d3, g.W3);
+  build_dgrad<T, H, H>(d2, g.W2);
+  load_vec(vec + 0 * VEC, g.b1, H); load_vec(vec + 1 * VEC, g.g1, H); load_vec(vec + 2 * VEC, g.be1, H);
+  load_vec(vec + 3 * VEC, g.b2, H); load_vec(vec + 4 * VEC, g.g2, H); load_vec(vec + 5 * VEC, g.be2, H);
+  __syncthreads();
+  const float* gam1 = vec + 1 * VEC;
+  const float* gam2 = vec + 4 * VEC;
+  float pg1[NTH], pb1[NTH], pg2[NTH], pb2[NTH];  // per-lane column sums (see colsum)
+#pragma unroll
+  for (int t = 0; t < NTH; ++t) pg1[t] = pb1[t] = pg2[t] = pb2[t] = 0.f;
+
+
+  MLP_LOOP {
+    const int64_t row = tile * 32 + (lane & 31);
+    f32x16 x[NTF], a[NTH], y2[NTH], d[NTH];
+    float mean1, rstd1, mean2, rstd2;
+    // ---- forward (u1, u2 out; y2 and the row statistics kept)
+    load_rows<T, F>(x, z, row, M, h);
+    dense<T, F, H>(x, a, f1, lane);
+    bias_act<H>(a, vec + 0 * VEC, ACT_SIGMOID, h);
+    lrelu_ln<H>(a, vec + 1 * VEC, vec + 2 * VEC, h, mean1, rstd1);
+    store_rows<T, H>(u1o, row, M, a, h);
+    dense<T, H, H>(a, y2, f2, lane);
+    bias_act<H>(y2, vec + 3 * VEC, ACT_SIGMOID, h);
+#pragma unroll
+    for (int t = 0; t < NTH; ++t) a[t] = y2[t];
+    lrelu_ln<H>(a, vec + 4 * VEC, vec + 5 * VEC, h, mean2, rstd2);
+    store_rows<T, H>(u2o, row, M, a, h);
+    // ---- reverse: du2 = dfake W3^T, LN2 / LReLU / sigmoid reverse -> dz2
+    load_rows<T, F>(x, dfake, row, M, h);
+    dense<T, F, H>(x, d, d3, lane);
+#pragma unroll
+    for (int t = 0; t < NTH; ++t) pb2[t] += colsum(d[t], lane);
+    {
+      float m1 = 0.f, m2 = 0.f;
+#pragma unroll
+      for (int t = 0; t < NTH; ++t)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int f0 = 32 * t + 8 * gq + 4 * h;
+          const float4 gv = *reinterpret_cast<const float4*>(gam2 + f0);
+          const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int q = 4 * gq + e;
+            const bool in = f0 + e < H;
+            const float xh = in ? (lrelu(y2[t][q]) - mean2) * rstd2 : 0.f;
+            const float gd = in ? d[t][q] * gg[e] : 0.f;
+            m1 += gd;
+            m2 = fmaf(gd, xh, m2);
+          }
+        }
+      m1 += __shfl_xor(m1, 32, 64);
+      m2 += __shfl_xor(m2, 32, 64);
+      m1 *= 1.f / H;
+      m2 *= 1.f / H;
+#pragma unroll
+      for (int t = 0; t < NTH; ++t) {
+        f32x16 px;
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int f0 = 32 * t + 8 * gq + 4 * h;
+          const float4 gv = *reinterpret_cast<const float4*>(gam2 + f0);
+          const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int q = 4 * gq + e;
+            const bool in = f0 + e < H;
+            const float yv = y2[t][q];
+            const float xh = in ? (lrelu(yv) - mean2) * rstd2 : 0.f;
+            const float dv = in ? d[t][q] : 0.f;
+            px[q] = dv * xh;
+            float dl = rstd2 * (dv * gg[e] - m1 - xh * m2);
+            dl *= yv >= 0.f ? 1.f : LRELU_ALPHA_F;
+            d[t][q] = in ? dl * yv * (1.f - yv) : 0.f;
+          }
+        }
+        pg2[t] += colsum(px, lane);
+      }
+    }
+    store_rows<T, H>(dz2o, row, M, d, h);
+    // ---- du1 = dz2 W2^T; recompute y1; LN1 / LReLU / sigmoid reverse -> dz1
+    dense<T, H, H>(d, y2, d2, lane);  // y2 now holds du1
+#pragma unroll
+    for (int t = 0; t < NTH; ++t) pb1[t] += colsum(y2[t], lane);
+    load_rows<T, F>(x, z, row, M, h);
+    dense<T, F, H>(x, a, f1, lane);
+    bias_act<H>(a, vec + 0 * VEC, ACT_SIGMOID, h);  // y1
+    {
+      float m1 = 0.f, m2 = 0.f;
+#pragma unroll
+      for (int t = 0; t < NTH; ++t)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int f0 = 32 * t + 8 * gq + 4 * h;
+          const float4 gv = *reinterpret_cast<const float4*>(gam1 + f0);
+          const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int q = 4 * gq + e;
+            const bool in = f0 + e < H;
+            const float xh = in ? (lrelu(a[t][q]) - mean1) * rstd1 : 0.f;
+            const float gd = in ? y2[t][q] * gg[e] : 0.f;
+            m1 += gd;
+            m2 = fmaf(gd, xh, m2);
+          }
+        }
+      m1 += __shfl_xor(m1, 32, 64);
+      m2 += __shfl_xor(m2, 32, 64);
+      m1 *= 1.f / H;
+      m2 *= 1.f / H;
+#pragma unroll
+      for (int t = 0; t < NTH; ++t) {
+        f32x16 px;
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int f0 = 32 * t + 8 * gq + 4 * h;
+          const float4 gv = *reinterpret_cast<const float4*>(gam1 + f0);
+          const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int q = 4 * gq + e;
+            const bool in = f0 + e < H;
+            const float yv = a[t][q];
+            const float xh = in ? (lrelu(yv) - mean1) * rstd1 : 0.f;
+            const float dv = in ? y2[t][q] : 0.f;
+            px[q] = dv * xh;
+            float dl = rstd1 * (dv * gg[e] - m1 - xh * m2);
+            dl *= yv >= 0.f ? 1.f : LRELU_ALPHA_F;
+            a[t][q] = in ? dl * yv * (1.f - yv) : 0.f;
+          }
+        }
+        pg1[t] += colsum(px, lane);
+      }
+    }
+    store_rows<T, H>(dz1o, row, M, a, h);
+  }
+  // per-wave LN partials: lanes with bit 0 clear own feature featq(colsum_q(lane), h) of every tile
+  float* out = lnslab + ((int64_t)blockIdx.x * MLP_WAVES + (threadIdx.x >> 6)) * 4 * H;
+  if ((lane & 1) == 0) {
+#pragma unroll
+    for (int t = 0; t < NTH; ++t) {
+      const int f = 32 * t + featq(colsum_q(lane), h);
+      if (f < H) {
+        out[f] = pg1[t];
+        out[H + f] = pb1[t];
+        out[2 * H + f] = pg2[t];
+        out[3 * H + f] = pb2[t];
+      }
+    }
+  }
+}
+
+// ===================================================================================================
+// fixed-order reductions
+// ===================================================================================================
+__global__ void __launch_bounds__(256) mlp_finish_kernel(const float* __restrict__ slab, int P,
+                                                         const float* __restrict__ e, int64_t ne, int mode, float invB,
+                                                         const float* __restrict__ b3p, float lam,
+                                                         float* __restrict__ out) {
+  __shared__ float red[3][4];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < P; i += 256) {
+    s0 += slab[2 * i];
+    s1 += slab[2 * i + 1];
+  }
+  for (int64_t i = threadIdx.x; i < ne; i += 256) s2 += e[i];
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = s0;
+    red[1][w] = s1;
+    red[2][w] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float b3 = b3p ? b3p[0] : 0.f;
+    const float a = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    const float b = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    const float c = (red[2][0] + red[2][1]) + (red[2][2] + red[2][3]);
+    if (mode == 0) {
+      const float wr = -(a * invB + b3), wf = b * invB + b3, pen = c * invB;
+      out[0] = wr + wf + lam * pen;
+      out[1] = wr;
+      out[2] = wf;
+      out[3] = pen;
+    } else if (mode == 1) {  // generator W loss on the fake rows: W(fake, -1) = -mean s
+      out[0] = -(a * invB + b3);
+      out[1] = out[2] = out[3] = 0.f;
+    } else {  // BCE: the slab holds the per-row losses; invB = 1 / rows gives their mean
+      out[0] = a * invB;
+      out[1] = out[2] = out[3] = 0.f;
+    }
+  }
+}
+
+// out[k][j] += sum_p slab[p][k L + j] for the nseg segments (fixed order: one thread per element)
+__global__ void __launch_bounds__(256) mlp_slab_sum_kernel(const float* __restrict__ slab, int P, int L, int nseg,
+                                                           float* __restrict__ o0, float* __restrict__ o1,
+                                                           float* __restrict__ o2, float* __restrict__ o3) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= nseg * L) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += slab[(int64_t)p * nseg * L + i];
+  const int k = i / L, j = i - k * L;
+  float* o = k == 0 ? o0 : k == 1 ? o1 : k == 2 ? o2 : o3;
+  if (o) o[j] += s;
+}
+
+// ===================================================================================================
+// host launchers
+// ===================================================================================================
+bool mlp_supported(int F, int H) { return H == 100 && (F == 32 || F == 36); }
+
+namespace {
+
+template <typename KER>
+int mlp_grid(KER kern, size_t lds, int64_t M) {
+  static_assert(sizeof(KER) > 0, "");
+  int per_cu = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), MLP_THREADS, lds) !=
+          hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const int64_t ntile = (M + 31) / 32;
+  const int64_t want = (ntile + MLP_WAVES - 1) / MLP_WAVES;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)device_cu_count() * std::min(per_cu, 2)));
+}
+
+template <typename KER>
+void set_lds(KER kern, size_t lds) {
+  if (lds > 64 * 1024)
+    HFREP_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds));
+}
+
+template <typename T, int F, int H> constexpr size_t lds_gen_fwd() {
+  return (size_t)(fwd_entries<T, F, H>() + fwd_entries<T, H, H>() + fwd_entries<T, H, F>()) * frag_bytes<T>() +
+         7 * VEC * 4;
+}
+template <typename T, int F, int H> constexpr size_t lds_wgp_norm() {
+  return (size_t)(dgrad_entries<T, H, H>() + dgrad_entries<T, F, H>()) * frag_bytes<T>();
+}
+template <typename T, int F, int H> constexpr size_t lds_critic4() {
+  return (size_t)(fwd_entries<T, F, H>() + fwd_entries<T, H, H>() + dgrad_entries<T, H, H>() +
+                  dgrad_entries<T, F, H>()) *
+             frag_bytes<T>() +
+         2 * VEC * 4;
+}
+template <typename T, int F, int H> constexpr size_t lds_gan_critic() {
+  return (size_t)(fwd_entries<T, F, H>() + fwd_entries<T, H, H>() + dgrad_entries<T, H, H>()) * frag_bytes<T>() +
+         2 * VEC * 4;
+}
+template <typename T, int F, int H> constexpr size_t lds_gen_bwd() {
+  return (size_t)(fwd_entries<T, F, H>() + fwd_entries<T, H, H>() + dgrad_entries<T, H, F>() +
+                  dgrad_entries<T, H, H>()) *
+             frag_bytes<T>() +
+         6 * VEC * 4;
+}
+static_assert(lds_critic4<float, 36, 100>() <= 160 * 1024, "fp32 critic images exceed LDS");
+static_assert(lds_gen_bwd<float, 36, 100>() <= 160 * 1024, "fp32 generator reverse images exceed LDS");
+
+// dispatch over (dtype, F) with H = 100
+#define MLP_DISPATCH(dt, F, ...)                      \
+  do {                                                 \
+    if (dt == DT_BF16) {                               \
+      using T = bf16_t;                                \
+      if (F == 32) { constexpr int FF = 32; __VA_ARGS__ }     \
+      else { constexpr int FF = 36; __VA_ARGS__ }             \
+    } else {                                           \
+      using T = float;                                 \
+      if (F == 32) { constexpr int FF = 32; __VA_ARGS__ }     \
+      else { constexpr int FF = 36; __VA_ARGS__ }             \
+    }                                                  \
+  } while (0)
+
+}  // namespace
+
+int mlp_slab_rows(int64_t M) {
+  const int64_t ntile = (M + 31) / 32;
+  const int64_t want = (ntile + MLP_WAVES - 1) / MLP_WAVES;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)device_cu_count() * 2)) * MLP_WAVES;
+}
+
+void launch_mlp_gen_fwd(int dt, const void* noise, const MlpGen& g, void* out, int64_t M, int F, int H,
+                        hipStream_t s) {
+  if (M <= 0) return;
+  MLP_DISPATCH(dt, F, {
+    auto k = mlp_gen_fwd_kernel<T, FF, 100>;
+    constexpr size_t lds = lds_gen_fwd<T, FF, 100>();
+    set_lds(k, lds);
+    hipLaunchKernelGGL(k, dim3(mlp_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, (const T*)noise, g, (T*)out, M);
+  });
+  (void)H;
+}
+
+void launch_mlp_wgp_norm(int dt, const MlpCritic& c, float* gsq, int64_t M, int Tn, int F, int H, hipStream_t s) {
+  if (M <= 0) return;
+  MLP_DISPATCH(dt, F, {
+    auto k = mlp_wgp_norm_kernel<T, FF, 100>;
+    constexpr size_t lds = lds_wgp_norm<T, FF, 100>();
+    set_lds(k, lds);
+    hipLaunchKernelGGL(k, dim3(mlp_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, c, gsq, M, Tn);
+  });
+  (void)H;
+}
+
+void launch_mlp_wgp_coef(const float* gsq, int Tn, int64_t B, float lam, float* c, float* e, hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(mlp_wgp_coef_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, gsq, Tn, B, lam, c, e);
+}
+
+// the slab-writing launchers must use exactly mlp_slab_rows(M) / MLP_WAVES workgroups
+template <typename KER>
+static int slab_grid(KER kern, size_t lds, int64_t M) {
+  (void)kern;
+  (void)lds;
+  return mlp_slab_rows(M) / MLP_WAVES;
+}
+
+void launch_mlp_wgp_critic(int dt, const void* real, const void* fake, const float* c, const MlpCritic& cr,
+                           void* X2c, void* dY2, void* X1c, void* dY1, void* Y3c, float* slab, int64_t M, int Tn,
+                           int F, int H, hipStream_t s) {
+  if (M <= 0) return;
+  const float invB = (float)Tn / (float)M;
+  MLP_DISPATCH(dt, F, {
+    auto k = mlp_wgp_critic_kernel<T, FF, 100>;
+    constexpr size_t lds = lds_critic4<T, FF, 100>();
+    set_lds(k, lds);
+    hipLaunchKernelGGL(k, dim3(slab_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, (const T*)real, (const T*)fake, c, cr,
+                       (T*)X2c, (T*)dY2, (T*)X1c, (T*)dY1, (T*)Y3c, slab, M, Tn, invB);
+  });
+  (void)H;
+}
+
+void launch_mlp_critic_dx(int dt, int head, const void* x, const MlpCritic& cr, float label, void* dx, float* slab,
+                          int64_t M, int Tn, int F, int H, hipStream_t s) {
+  if (M <= 0) return;
+  // head 0: d/ds_b of the W loss = -1/B (B = M / T samples); head 1: BCE mean over the M rows
+  const float inv = head == 0 ? (float)Tn / (float)M : 1.f / (float)M;
+  MLP_DISPATCH(dt, F, {
+    constexpr size_t lds = lds_critic4<T, FF, 100>();
+    if (head == 0) {
+      auto k = mlp_critic_dx_kernel<T, FF, 100, 0>;
+      set_lds(k, lds);
+      hipLaunchKernelGGL(k, dim3(slab_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, (const T*)x, cr, label, (T*)dx, slab,
+                         M, Tn, inv);
+    } else {
+      auto k = mlp_critic_dx_kernel<T, FF, 100, 1>;
+      set_lds(k, lds);
+      hipLaunchKernelGGL(k, dim3(slab_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, (const T*)x, cr, label, (T*)dx, slab,
+                         M, Tn, inv);
+    }
+  });
+  (void)H;
+}
+
+void launch_mlp_gan_critic(int dt, const void* x, const MlpCritic& cr, float label, void* h1, void* dh2, void* dh1,
+                           void* h2, void* dz3, float* slab, int64_t M, int F, int H, hipStream_t s) {
+  if (M <= 0) return;
+  MLP_DISPATCH(dt, F, {
+    auto k = mlp_gan_critic_kernel<T, FF, 100>;
+    constexpr size_t lds = lds_gan_critic<T, FF, 100>();
+    set_lds(k, lds);
+    hipLaunchKernelGGL(k, dim3(slab_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, (const T*)x, cr, label, (T*)h1,
+                       (T*)dh2, (T*)dh1, (T*)h2, (T*)dz3, slab, M, 1.f / (float)M);
+  });
+  (void)H;
+}
+
+void launch_mlp_gen_bwd(int dt, const void* noise, const void* dfake, const MlpGen& g, void* dz1, void* u1,
+                        void* dz2, void* u2, float* lnslab, int64_t M, int F, int H, hipStream_t s) {
+  if (M <= 0) return;
+  MLP_DISPATCH(dt, F, {
+    auto k = mlp_gen_bwd_kernel<T, FF, 100>;
+    constexpr size_t lds = lds_gen_bwd<T, FF, 100>();
+    set_lds(k, lds);
+    hipLaunchKernelGGL(k, dim3(slab_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, (const T*)noise, (const T*)dfake, g,
+                       (T*)dz1, (T*)u1, (T*)dz2, (T*)u2, lnslab, M);
+  });
+  (void)H;
+}
+
+void launch_mlp_finish(const float* slab, int P, const float* e, int64_t n_e, int mode, float invB, const float* b3,
+                       float lam, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(mlp_finish_kernel, dim3(1), dim3(256), 0, s, slab, P, e, n_e, mode, invB, b3, lam, out);
+}
+
+void launch_mlp_slab_sum(const float* slab, int P, int L, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((L + 255) / 256), dim3(256), 0, s, slab, P, L, 1, out, nullptr, nullptr,
+                     nullptr);
+}
+
+void launch_mlp_slab_sum4(const float* slab, int P, int L, float* o0, float* o1, float* o2, float* o3, hipStream_t s) {
+  hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((4 * L + 255) / 256), dim3(256), 0, s, slab, P, L, 4, o0, o1, o2, o3);
+}
+
+}  // namespace hfrep

@@ -117,6 +117,14 @@ class GANTrainer:
 
             self.grad_sync = GradSync(process_group, world)
             self.grad_sync.broadcast_params([self.generator, self.critic])
+        # BASELINE configs 3 / 4 (MLP GAN, MLP WGAN-GP): one fused kernel per pass instead of the
+        # layer-by-layer engine (train/mlp_fused.py; HFREP_MLP_FUSED=0 keeps the engine)
+        self._fused = None
+        if self.device.type == "cuda":
+            from .mlp_fused import FusedMLP
+
+            if FusedMLP.supported(self):
+                self._fused = FusedMLP(self)
 
     # ------------------------------------------------------------------------------------
     def _want_concurrent(self, cfg) -> bool:
@@ -345,7 +353,9 @@ class GANTrainer:
     @torch.no_grad()
     def train_step(self):
         cfg, B = self.cfg, self.cfg.batch_size
-        if cfg.loss == "gan":
+        if self._fused is not None:
+            self._fused.train_step()
+        elif cfg.loss == "gan":
             real, noise = self._batch(B)
             fake = self.generator.predict(noise)
             lr_ = self._bce_step(real, 1.0)

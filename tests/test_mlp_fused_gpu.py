@@ -1,0 +1,154 @@
+"""Fused MLP-GAN kernels (csrc/mlp.hip, train/mlp_fused.py) vs the CPU fp64 explicit engine.
+
+BASELINE configs 3 / 4: the vanilla GAN (GAN/GAN.py) and the MLP WGAN-GP (GAN/WGAN_GP.py).  Every
+fused pass is checked against the layer-by-layer fp64 reference of the same quantity: the generator
+forward, the WGAN-GP critic gradient (W terms + reverse-over-tangent penalty), the GAN discriminator
+gradient, the generator gradient through the frozen critic and the loss values; plus run-to-run
+bitwise determinism and whole training steps against the GPU engine path (HFREP_MLP_FUSED=0).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"float32": 2e-4, "bfloat16": 3e-2}
+
+
+def _rel(got, ref):
+    got, ref = got.double().cpu(), ref.double().cpu()
+    return ((got - ref).norm() / max(ref.norm().item(), 1e-30)).item()
+
+
+def _pair(cuda, loss, dtype, B, T=24, F=32):
+    from hfrep.train.gan_trainer import GANConfig, GANTrainer
+
+    ds = np.random.RandomState(0).rand(64, T, F).astype(np.float32)
+    kw = dict(arch="mlp", loss=loss, window=T, features=F, batch_size=B)
+    tg = GANTrainer(GANConfig(dtype=dtype, **kw), ds, device=cuda)
+    assert tg._fused is not None, "the fused MLP path must be selected on the GPU"
+    tc = GANTrainer(GANConfig(dtype="float64", **kw), ds, param_dtype=torch.float64)
+    with torch.no_grad():
+        tc.generator.flat.copy_(tg.generator.flat.double().cpu())
+        tc.critic.flat.copy_(tg.critic.flat.double().cpu())
+    return tg, tc
+
+
+def _inputs(B, T, F, seed=11):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(B, T, F, generator=g), torch.randn(B, T, F, generator=g), torch.rand(B, generator=g)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("B,T,F", [(48, 24, 32), (37, 24, 32), (20, 48, 36)])
+def test_mlp_wgan_gp_fused_grads(cuda, dtype, B, T, F):
+    """Config 4: generator forward, the critic update's gradient and loss pack, and the generator
+    gradient, fused kernels vs the fp64 engine (same weights, same batch)."""
+    tg, tc = _pair(cuda, "wgan_gp", dtype, B, T, F)
+    fz = tg._fused
+    ops = torch.ops.hfrep
+    dt = tg.dtype
+    real, noise, alpha = _inputs(B, T, F)
+    with torch.no_grad():
+        fake = ops.mlp_gen_fwd(noise.to(cuda, dt), fz.gw)
+        fc = tc.generator.predict(noise.double())
+        assert _rel(fake, fc) < TOL[dtype], f"G(z) rel err {_rel(fake, fc):.2e}"
+        pack_g = fz._wgp_critic_grads(real.to(cuda, dt), fake)
+        pack_c = tc.critic_gp_grads(real.double(), fake.double().cpu(), alpha.double())
+        rel = _rel(tg.critic.flat.grad, tc.critic.flat.grad)
+        assert rel < TOL[dtype], f"critic grad rel err {rel:.2e}"
+        lt = 1e-4 if dtype == "float32" else 2e-2
+        for a, b in zip(pack_g.cpu().tolist(), pack_c.tolist()):
+            assert abs(a - b) <= lt * max(1.0, abs(b)), (pack_g, pack_c)
+        lg = fz._generator_grads(noise.to(cuda, dt), fake)
+        lc = tc.generator_grads(noise.double())
+        rel = _rel(tg.generator.flat.grad, tc.generator.flat.grad)
+        assert rel < TOL[dtype], f"generator grad rel err {rel:.2e}"
+        assert abs(lg.item() - lc.item()) <= lt * max(1.0, abs(lc.item()))
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("B", [48, 37])
+def test_mlp_gan_fused_grads(cuda, dtype, B):
+    """Config 3: the discriminator update on real (label 1) and fake (label 0) and the generator update
+    (label 1 through the frozen discriminator), fused vs the fp64 engine."""
+    from hfrep.ops import functional as Fn
+
+    T, F = 24, 32
+    tg, tc = _pair(cuda, "gan", dtype, B, T, F)
+    fz = tg._fused
+    dt = tg.dtype
+    real, noise, _ = _inputs(B, T, F)
+    lt = 1e-4 if dtype == "float32" else 2e-2
+    with torch.no_grad():
+        for x, label in ((real, 1.0), (torch.sigmoid(noise), 0.0)):
+            tg.critic.zero_grad()
+            tc.critic.zero_grad()
+            lg = fz._gan_d_grads(x.to(cuda, dt), label)
+            p, tape = tc.critic.efwd(x.double(), save=True)
+            out, dp = Fn.gan_loss(p, p.numel(), label, label, 1)
+            tc.critic.ebwd(tape, dp)
+            rel = _rel(tg.critic.flat.grad, tc.critic.flat.grad)
+            assert rel < TOL[dtype], f"D grad rel err {rel:.2e} (label {label})"
+            assert abs(lg.item() - out[0].item()) <= lt * max(1.0, abs(out[0].item()))
+        fake = torch.ops.hfrep.mlp_gen_fwd(noise.to(cuda, dt), fz.gw)
+        lg = fz._generator_grads(noise.to(cuda, dt), fake)
+        lc = tc.generator_grads(noise.double())
+        rel = _rel(tg.generator.flat.grad, tc.generator.flat.grad)
+        assert rel < TOL[dtype], f"generator grad rel err {rel:.2e}"
+        assert abs(lg.item() - lc.item()) <= lt * max(1.0, abs(lc.item()))
+
+
+@pytest.mark.parametrize("loss", ["wgan_gp", "gan"])
+def test_mlp_fused_bitwise_and_engine_parity(cuda, loss, monkeypatch):
+    """Three training iterations: two fused runs are bitwise identical (fixed-order reductions, no
+    atomics); the fused run tracks the GPU engine path (HFREP_MLP_FUSED=0) on the same RNG stream."""
+    from hfrep.train.gan_trainer import GANConfig, GANTrainer
+
+    T, F, B = 24, 32, 96
+    ds = np.random.RandomState(1).rand(256, T, F).astype(np.float32)
+    cfg = GANConfig(arch="mlp", loss=loss, window=T, features=F, batch_size=B, dtype="float32")
+
+    def run(fused):
+        monkeypatch.setenv("HFREP_MLP_FUSED", "1" if fused else "0")
+        tr = GANTrainer(cfg, ds, device=cuda)
+        assert (tr._fused is not None) == fused
+        for _ in range(3):
+            tr.train_step()
+        torch.cuda.synchronize()
+        return tr
+
+    a, b, e = run(True), run(True), run(False)
+    assert torch.equal(a.critic.flat, b.critic.flat) and torch.equal(a.generator.flat, b.generator.flat)
+    assert torch.equal(a._d_acc, b._d_acc) and torch.equal(a._g_acc, b._g_acc)
+    for m in ("critic", "generator"):
+        pa, pe = getattr(a, m).flat, getattr(e, m).flat
+        assert _rel(pa, pe) < 1e-4, f"{m} params drift from the engine path: {_rel(pa, pe):.2e}"
+    la, le = a.losses(), e.losses()
+    for k in ("d_loss", "g_loss"):
+        assert abs(la[k] - le[k]) <= 1e-3 * max(1.0, abs(le[k])), (la, le)
+
+
+def test_mlp_fused_large_batch_slices(cuda):
+    """At a batch spanning many persistent-grid rounds the fused critic gradient is the average of
+    the gradients of its four quarter batches (bf16 and fp32)."""
+    T, F = 24, 32
+    for dtype in ("float32", "bfloat16"):
+        B = 4 * 8192
+        tg, _ = _pair(cuda, "wgan_gp", dtype, B, T, F)
+        fz, dt = tg._fused, tg.dtype
+        real, noise, _ = _inputs(B, T, F, seed=3)
+        with torch.no_grad():
+            fake = torch.ops.hfrep.mlp_gen_fwd(noise.to(cuda, dt), fz.gw)
+            tg.critic.zero_grad()
+            fz._wgp_critic_grads(real.to(cuda, dt), fake)
+            full = tg.critic.flat.grad.clone()
+            acc = torch.zeros_like(full)
+            r = real.to(cuda, dt)
+            for q in range(4):
+                tg.critic.zero_grad()
+                sl = slice(q * B // 4, (q + 1) * B // 4)
+                fz._wgp_critic_grads(r[sl].contiguous(), fake[sl].contiguous())
+                acc += tg.critic.flat.grad / 4
+        rel = _rel(full, acc)
+        assert rel < (1e-5 if dtype == "float32" else 2e-2), f"{dtype}: full vs slice-average rel {rel:.2e}"
