@@ -62,7 +62,8 @@ inline int64_t hidden_of(const std::vector<Tensor>& p, int64_t F) {
   return H;
 }
 inline Tensor slab_new(const Tensor& like, int64_t M, int64_t L) {
-  return at::zeros({(int64_t)hfrep::mlp_slab_rows(M), L}, like.options().dtype(at::kFloat));
+  // every wave of the launch writes its whole row (also waves without a tile): no fill needed
+  return at::empty({(int64_t)hfrep::mlp_slab_rows(M), L}, like.options().dtype(at::kFloat));
 }
 
 bool mlp_supported_op(int64_t F, int64_t H) { return hfrep::mlp_supported((int)F, (int)H); }
@@ -96,7 +97,7 @@ std::tuple<Tensor, Tensor> mlp_wgp_coef(Tensor gsq, double lam) {
               "mlp_wgp_coef: gsq (B, T) fp32");
   GUARD(gsq);
   const int64_t B = gsq.size(0), T = gsq.size(1);
-  Tensor c = at::empty({B}, gsq.options()), e = at::empty({B}, gsq.options());
+  Tensor c = at::empty({B}, gsq.options()), e = at::empty({hfrep::mlp_wgp_coef_parts(B)}, gsq.options());
   hfrep::launch_mlp_wgp_coef(gsq.data_ptr<float>(), (int)T, B, (float)lam, c.data_ptr<float>(), e.data_ptr<float>(),
                              cur_stream(gsq));
   return {c, e};

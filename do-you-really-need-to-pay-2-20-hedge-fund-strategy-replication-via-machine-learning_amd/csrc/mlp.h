@@ -30,7 +30,9 @@ void launch_mlp_gen_fwd(int dt, const void* noise, const MlpGen& g, void* out, i
                         hipStream_t s);
 // per-row squared norm of the linear critic's input gradient dD/dx (head 0): gsq (M) fp32
 void launch_mlp_wgp_norm(int dt, const MlpCritic& c, float* gsq, int64_t M, int Tn, int F, int H, hipStream_t s);
-// per-sample GP coefficient c_b = -(2 lam / B)(1 - |g_b|) / |g_b| and (1 - |g_b|)^2
+// per-sample GP coefficient c_b = -(2 lam / B)(1 - |g_b|) / |g_b|, and e = per-block sums of (1 - |g_b|)^2
+// (mlp_wgp_coef_parts(B) values)
+int mlp_wgp_coef_parts(int64_t B);
 void launch_mlp_wgp_coef(const float* gsq, int Tn, int64_t B, float lam, float* c, float* e, hipStream_t s);
 // the WGAN-GP critic step of the linear critic on one row tile: W terms on real / fake and the
 // reverse-over-tangent GP term, as combined wgrad operands (see mlp.hip)

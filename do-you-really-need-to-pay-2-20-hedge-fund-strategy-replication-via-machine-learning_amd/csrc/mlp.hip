@@ -416,16 +416,23 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_wgp_norm_kernel(MlpCritic c, 
 }
 
 // per sample: |g_b| from the T row norms, c_b = -(2 lam / B)(1 - |g_b|) / |g_b| (the gp_coef adjoint,
-// ops/reference.py) and e_b = (1 - |g_b|)^2
+// ops/reference.py); epart[block] = sum over the block's samples of (1 - |g_b|)^2 (fixed order)
 __global__ void __launch_bounds__(256) mlp_wgp_coef_kernel(const float* __restrict__ gsq, int Tn, int64_t B, float lam,
-                                                           float* __restrict__ c, float* __restrict__ e) {
+                                                           float* __restrict__ c, float* __restrict__ epart) {
+  __shared__ float red[4];
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (b >= B) return;
-  float s = 0.f;
-  for (int t = 0; t < Tn; ++t) s += gsq[b * Tn + t];
-  const float n = sqrtf(s);
-  c[b] = -(2.f * lam / (float)B) * (1.f - n) / fmaxf(n, 1e-30f);
-  e[b] = (1.f - n) * (1.f - n);
+  float e = 0.f;
+  if (b < B) {
+    float s = 0.f;
+    for (int t = 0; t < Tn; ++t) s += gsq[b * Tn + t];
+    const float n = sqrtf(s);
+    c[b] = -(2.f * lam / (float)B) * (1.f - n) / fmaxf(n, 1e-30f);
+    e = (1.f - n) * (1.f - n);
+  }
+  e = wave_sum(e);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = e;
+  __syncthreads();
+  if (threadIdx.x == 0) epart[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // One GP critic update's device work per row (b, t):
@@ -829,17 +836,35 @@ __global__ void __launch_bounds__(256) mlp_finish_kernel(const float* __restrict
   }
 }
 
-// out[k][j] += sum_p slab[p][k L + j] for the nseg segments (fixed order: one thread per element)
-__global__ void __launch_bounds__(256) mlp_slab_sum_kernel(const float* __restrict__ slab, int P, int L, int nseg,
-                                                           float* __restrict__ o0, float* __restrict__ o1,
-                                                           float* __restrict__ o2, float* __restrict__ o3) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= nseg * L) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += slab[(int64_t)p * nseg * L + i];
-  const int k = i / L, j = i - k * L;
-  float* o = k == 0 ? o0 : k == 1 ? o1 : k == 2 ? o2 : o3;
-  if (o) o[j] += s;
+// out[k][j] += sum_p slab[p][k L + j] for the nseg segments: 64 elements per workgroup, the 16 waves
+// split the P rows (4 partial sums each so loads overlap), combined in a fixed order (deterministic)
+__global__ void __launch_bounds__(1024) mlp_slab_sum_kernel(const float* __restrict__ slab, int P, int L, int nseg,
+                                                            float* __restrict__ o0, float* __restrict__ o1,
+                                                            float* __restrict__ o2, float* __restrict__ o3) {
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane, n = nseg * L;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (i < n) {
+    int p = wv;
+    for (; p + 48 < P; p += 64) {
+      s0 += slab[(int64_t)p * n + i];
+      s1 += slab[(int64_t)(p + 16) * n + i];
+      s2 += slab[(int64_t)(p + 32) * n + i];
+      s3 += slab[(int64_t)(p + 48) * n + i];
+    }
+    for (; p < P; p += 16) s0 += slab[(int64_t)p * n + i];
+  }
+  part[wv][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (wv == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += part[w][lane];
+    const int k = i / L, j = i - k * L;
+    float* o = k == 0 ? o0 : k == 1 ? o1 : k == 2 ? o2 : o3;
+    if (o) o[j] += t;
+  }
 }
 
 // ===================================================================================================
@@ -940,6 +965,8 @@ void launch_mlp_wgp_norm(int dt, const MlpCritic& c, float* gsq, int64_t M, int 
   (void)H;
 }
 
+int mlp_wgp_coef_parts(int64_t B) { return (int)((B + 255) / 256); }
+
 void launch_mlp_wgp_coef(const float* gsq, int Tn, int64_t B, float lam, float* c, float* e, hipStream_t s) {
   if (B <= 0) return;
   hipLaunchKernelGGL(mlp_wgp_coef_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, gsq, Tn, B, lam, c, e);
@@ -1022,12 +1049,12 @@ void launch_mlp_finish(const float* slab, int P, const float* e, int64_t n_e, in
 }
 
 void launch_mlp_slab_sum(const float* slab, int P, int L, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((L + 255) / 256), dim3(256), 0, s, slab, P, L, 1, out, nullptr, nullptr,
+  hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((L + 63) / 64), dim3(1024), 0, s, slab, P, L, 1, out, nullptr, nullptr,
                      nullptr);
 }
 
 void launch_mlp_slab_sum4(const float* slab, int P, int L, float* o0, float* o1, float* o2, float* o3, hipStream_t s) {
-  hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((4 * L + 255) / 256), dim3(256), 0, s, slab, P, L, 4, o0, o1, o2, o3);
+  hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((4 * L + 63) / 64), dim3(1024), 0, s, slab, P, L, 4, o0, o1, o2, o3);
 }
 
 }  // namespace hfrep
