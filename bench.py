@@ -58,6 +58,18 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
+def _device_id(dev) -> str:
+    """This rank's device as the record names it: index, plus the PCI bus / UUID where the runtime exposes
+    them (so an N-GPU record shows N distinct devices)."""
+    import torch
+
+    if dev.type != "cuda":
+        return str(dev)
+    p = torch.cuda.get_device_properties(dev)
+    tags = [f"{k}={getattr(p, k)}" for k in ("pci_bus_id", "pci_device_id", "uuid") if getattr(p, k, None) is not None]
+    return f"cuda:{dev.index} {p.name}" + (f" ({', '.join(str(t) for t in tags)})" if tags else "")
+
+
 def _measure(args, dtype, rank, world, pg, dev):
     """Warm up, then time exactly args.steps training iterations at one compute dtype.
 
@@ -126,6 +138,12 @@ def _measure(args, dtype, rank, world, pg, dev):
     _sync(dev)
     losses = tr.losses()
     per_rank = tr.windows_per_iteration()
+    # the job as the process group sees it: its size and every rank's device
+    world_pg = dist.get_world_size(pg) if world > 1 else 1
+    devices = [_device_id(dev)]
+    if world > 1:
+        devices = [None] * world
+        dist.all_gather_object(devices, _device_id(dev), group=pg)
     out = {
         "value": round(per_rank * world * args.steps / elapsed, 2),
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -137,6 +155,10 @@ def _measure(args, dtype, rank, world, pg, dev):
         "allreduce": "none" if gs is None else ("p2p" if gs.use_p2p else "rccl" if gs.backend == "nccl" else gs.backend),
         "buckets": 0 if gs is None else gs.buckets,
         "allreduce_exposed_ms_per_step": exposed,
+        "world_pg": world_pg,
+        "rank_devices": devices,
+        # fp32 gradient bytes each rank all-reduces per step (0 on one GPU: nothing is reduced)
+        "allreduce_bytes_per_step": 4 * tr.allreduce_floats_per_step() if world > 1 else 0,
     }
     tr.close()
     del tr, ds
@@ -181,8 +203,11 @@ def main():
               f"torch.distributed.run --nproc-per-node N)", file=sys.stderr)
         sys.exit(2)
     rank, local_rank, world, pg = init_distributed()
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+    else:  # CPU (gloo) rehearsal of the multi-rank record: tests/test_distributed.py
+        dev = torch.device("cpu")
 
     primary = "float32" if args.dtype in ("both", "float32") else "bfloat16"
     res = _measure(args, primary, rank, world, pg, dev)
@@ -223,6 +248,9 @@ def main():
             "allreduce": res["allreduce"],
             "buckets": res["buckets"],
             "allreduce_exposed_ms_per_step": res["allreduce_exposed_ms_per_step"],
+            "world_pg": res["world_pg"],
+            "rank_devices": res["rank_devices"],
+            "allreduce_bytes_per_step": res["allreduce_bytes_per_step"],
         }
         if sub is not None:
             # same config, same step count, timed after the fp32 run: bf16 MFMA with fp32 accumulation,

@@ -79,10 +79,13 @@ class _LegacyGAN:
     discriminator = critic
 
     def build_generator(self):
-        e = self._entry
+        """A fresh generator of this model's architecture, honouring the ``hidden`` and (LSTM
+        generators) ``lrelu_after_first`` overrides the instance was built with."""
+        cfg = self._trainer.cfg
         if self.KEY[0] == "mlp":
-            return e.generator(self.ts_length, self.ts_feature)
-        return e.generator(self.ts_length, self.ts_feature)
+            return self._entry.generator(self.ts_length, self.ts_feature, cfg.hidden)
+        return self._entry.generator(self.ts_length, self.ts_feature, cfg.hidden,
+                                     lrelu_after_first=cfg.lrelu_after_first)
 
     def build_critic(self):
         return self._entry.critic(self.ts_length, self.ts_feature)
@@ -105,7 +108,10 @@ class _LegacyGAN:
         if save_dir:
             os.makedirs(save_dir, exist_ok=True)
             stem = os.path.join(save_dir, f"{self._entry.save_prefix}{checkpoint.timestamp()}")
-            cfg = dict(self._cfg_kw, hidden=100, lrelu_after_first=False)
+            # the trainer's real architecture: a Q2-variant generator (LReLU after the first LSTM) or
+            # a non-default width must be rebuilt as such by checkpoint.load_generator
+            tc = self._trainer.cfg
+            cfg = dict(self._cfg_kw, hidden=tc.hidden, lrelu_after_first=tc.lrelu_after_first)
             checkpoint.save_generator(stem + ".pkl", self.generator, cfg)
             checkpoint.save_generator(stem + ".npz", self.generator, cfg)
             self.saved_path = stem + ".pkl"

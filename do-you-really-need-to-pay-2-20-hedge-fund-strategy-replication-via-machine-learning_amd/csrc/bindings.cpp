@@ -157,6 +157,8 @@ void lstm_wgrad_(Tensor x, Tensor hs, Tensor dZ, Tensor gW, Tensor gU, optional<
   if (tangent) {
     TORCH_CHECK(hds.has_value() && dZd.has_value(), "tangent segment needs xd, hds, dZd");
     CHECK_GPU(*xd); CHECK_GPU(*hds); CHECK_GPU(*dZd);
+    // the fp32 launcher takes untyped pointers: a bf16 tangent beside an fp32 primal would be read as fp32
+    same_dt(*xd, x); same_dt(*hds, hs); same_dt(*dZd, dZ);
     TORCH_CHECK(xd->sizes() == x.sizes() && hds->sizes() == hs.sizes() && dZd->sizes() == dZ.sizes(), "tangent shapes");
   }
   GUARD(x);

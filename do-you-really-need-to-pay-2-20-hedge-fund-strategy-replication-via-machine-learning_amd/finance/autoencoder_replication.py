@@ -240,6 +240,9 @@ class AE:
         batched = (all(a.device.type == "cuda" and a.device == a0.device and a.dtype == a0.dtype
                        and a._x_train.shape[1] == A for a in aes)
                    and a0.dtype in (torch.float32, torch.bfloat16)
+                   # use_native_for first: with HFREP_ALLOW_TORCH_FALLBACK=1 and no library it is False (the
+                   # one-by-one fallback below), where native() would raise
+                   and _native.use_native_for(a0.autoencoder.parts()[0].flat)
                    and all(bool(_native.native().ae_fit_supported(A, a._latent_dim, 48)) for a in aes))
         if batched:
             jobs = []

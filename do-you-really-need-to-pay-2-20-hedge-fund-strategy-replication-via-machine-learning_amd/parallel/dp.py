@@ -92,6 +92,10 @@ class GradSync:
         self.p2p_cap = int(os.environ.get("HFREP_DP_P2P_CAP", str(1 << 21)))
         self.p2p = None
         self._p2p_stream = None
+        # the collective kinds the buckets actually took ("p2p", "rccl", "gloo"): a bucket over the P2P cap,
+        # or not a CUDA fp32 tensor, falls back to the group's collective even with HFREP_DP_P2P on, which
+        # decides what a hipGraph capture may contain (use_graph_group_, graph_capturable)
+        self.routes: set = set()
         # exposed-wait timing (bench.py): per finish_ an event pair on the compute stream around the join
         self.timing = False
         self._events = []
@@ -111,6 +115,7 @@ class GradSync:
         if self.world <= 1:
             return
         p2p = self._p2p_for(flat_grad)
+        self.routes.add("p2p" if p2p is not None else "rccl" if self.backend == "nccl" else "gloo")
         if p2p is not None:
             p2p.all_reduce_(flat_grad, average=True)
         elif self.backend == "nccl":
@@ -131,6 +136,7 @@ class GradSync:
         if self.world <= 1:
             return
         p2p = self._p2p_for(grad_slice)
+        self.routes.add("p2p" if p2p is not None else "rccl" if self.backend == "nccl" else "gloo")
         if p2p is not None:
             # the side stream joins the compute stream here and is joined back in finish_
             s = self._p2p_stream
@@ -184,8 +190,13 @@ class GradSync:
     def graph_capturable(self) -> bool:
         """Whether a step's bucket all-reduces can be captured into a hipGraph at all: RCCL collectives, or
         every bucket on the one-shot P2P kernel (device-side epochs; the group only carried the IPC
-        handles).  gloo collectives cannot be captured."""
-        return self.world <= 1 or self.backend == "nccl" or self.use_p2p
+        handles).  gloo collectives cannot be captured -- also not a bucket that fell back to gloo from
+        the P2P route during the eager steps (``routes``)."""
+        if self.world <= 1:
+            return True
+        if "gloo" in self.routes:
+            return False
+        return self.backend == "nccl" or self.use_p2p
 
     def check_errors(self, blocking: bool = False) -> None:
         """Surface a failed one-shot all-reduce (P2PTimeout).  Non-blocking by default (pinned-host
@@ -223,6 +234,15 @@ class GradSync:
             time.sleep(0.0005)
         return True
 
+    def needs_graph_group(self) -> bool:
+        """Whether a capture needs the capture-only communicator (:meth:`use_graph_group_`): any RCCL
+        bucket would be captured.  Not when every bucket of the eager steps went through the P2P kernel
+        (no RCCL work inside the capture); a bucket over HFREP_DP_P2P_CAP (or not CUDA fp32) went to
+        RCCL instead and would be captured on the eager communicator, so it does."""
+        if self.backend != "nccl" or self.world <= 1 or self.group is None:
+            return False
+        return not (self.use_p2p and self.routes and self.routes <= {"p2p"})
+
     def use_graph_group_(self) -> bool:
         """Route the bucket all-reduces through a communicator reserved for hipGraph captures.
 
@@ -235,10 +255,8 @@ class GradSync:
         eagerly and used ONLY inside captures, has no eager work for its watchdog to query, and the
         first group's stream never joins a capture: no timing assumption left.  Collective call (every
         rank, same point); nccl only.  Returns whether the switch happened."""
-        if self.backend != "nccl" or self.world <= 1 or self.group is None:
+        if not self.needs_graph_group():
             return False
-        if self.use_p2p:
-            return False  # the buckets go through the P2P kernel: no RCCL work inside the capture
         if self._graph_group is None:
             ranks = dist.get_process_group_ranks(self.group)
             dev = torch.device("cuda", torch.cuda.current_device())

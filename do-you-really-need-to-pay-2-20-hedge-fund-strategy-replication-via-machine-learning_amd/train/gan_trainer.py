@@ -403,6 +403,14 @@ class GANTrainer:
         return {"iteration": self.iteration, "d_loss": float(d[0]), "d_real": float(d[1]), "d_fake": float(d[2]),
                 "gp": float(d[3]), "g_loss": float(self._g_acc.detach().float().cpu()[0])}
 
+    def allreduce_floats_per_step(self) -> int:
+        """Gradient floats one rank all-reduces per iteration under data parallelism: the critic's flat
+        buffer once per critic update (2 for the BCE GAN, 2 n_critic for the clipped WGAN, n_critic
+        with the gradient penalty) plus the generator's once."""
+        loss = self.cfg.loss
+        updates = 2 if loss == "gan" else 2 * self.n_critic if loss == "wgan" else self.n_critic
+        return updates * self.critic.flat.numel() + self.generator.flat.numel()
+
     def windows_per_iteration(self) -> int:
         """Windows consumed per iteration on this rank (SURVEY §6 seq/s definition)."""
         B = self.cfg.batch_size

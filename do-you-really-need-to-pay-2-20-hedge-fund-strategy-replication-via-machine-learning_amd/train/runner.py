@@ -114,6 +114,9 @@ class GraphedStep:
             t.grad_sync.finish_()
         torch.cuda.synchronize()
         if t.grad_sync is not None:
+            if not t.grad_sync.graph_capturable():  # a warmup bucket took gloo (P2P cap / dtype fallback)
+                raise RuntimeError(f"graph capture: a gradient bucket went through {sorted(t.grad_sync.routes)}; "
+                                   "gloo collectives cannot be captured (raise HFREP_DP_P2P_CAP or use RCCL)")
             t.grad_sync.drain_()
             t.grad_sync.use_graph_group_()
             torch.cuda.synchronize()

@@ -113,6 +113,35 @@ def test_legacy_gan_classes_api(tmp_path):
         assert m.generate(5).shape == (5, 6, 3)
 
 
+@pytest.mark.parametrize("kw", [dict(lrelu_after_first=True), dict(hidden=24), dict(lrelu_after_first=True, hidden=16)])
+def test_legacy_checkpoint_roundtrip_keeps_architecture(tmp_path, kw):
+    """A Q2-variant (LeakyReLU after the first LSTM, the production checkpoint's generator)
+    or non-default-width generator trained through the legacy class API saves its real architecture:
+    load_generator rebuilds it and predicts bitwise-identically; build_generator honours the flags."""
+    sys.path.insert(0, ROOT)
+    import torch
+
+    from GAN.MTSS_WGAN_GP import WGAN_GP
+    from hfrep.models.layers import LeakyReLU
+    from hfrep.utils import checkpoint
+
+    ds = np.random.RandomState(0).rand(20, 6, 3).astype(np.float32)
+    m = WGAN_GP(ds, device="cpu", **kw)
+    m.train(epochs=2, batch_size=4, save_dir=str(tmp_path), verbose=False)
+    lrelu = kw.get("lrelu_after_first", False)
+    assert isinstance(m.generator.layers[1], LeakyReLU) == lrelu
+    fresh = m.build_generator()
+    assert [type(l) for l in fresh.layers] == [type(l) for l in m.generator.layers]
+    assert fresh.count_params() == m.generator.count_params()
+    z = torch.randn(5, 6, 3, generator=torch.Generator().manual_seed(3))
+    want = m.generator.predict(z)
+    for path in (m.saved_path, m.saved_path[:-4] + ".npz"):
+        g, cfg = checkpoint.load_generator(path)
+        assert cfg["lrelu_after_first"] == lrelu and cfg["hidden"] == kw.get("hidden", 100)
+        assert [type(l) for l in g.layers] == [type(l) for l in m.generator.layers]
+        assert torch.equal(g.predict(z), want)
+
+
 def test_autoencoder_compat(cleaned):
     sys.path.insert(0, ROOT)
     from Autoencoder_encapsulate import AE

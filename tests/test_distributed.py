@@ -271,6 +271,58 @@ def test_bench_aggregate_uses_max_elapsed_over_ranks():
         # the DP fields of the record: gloo buckets (no GPU events: zero exposed wait), one entry per rank
         assert res[r]["allreduce"] == "gloo" and res[r]["buckets"] == 2
         assert res[r]["allreduce_exposed_ms_per_step"] == [0.0] * world
+        # the job as the process group saw it, and the bytes each rank reduces per step
+        assert res[r]["world_pg"] == world and res[r]["rank_devices"] == ["cpu"] * world
+        assert res[r]["allreduce_bytes_per_step"] > 0 and res[r]["allreduce_bytes_per_step"] % 4 == 0
+
+
+def test_bench_torchrun_world8_record_shape():
+    """``torchrun --nproc-per-node 8 bench.py --gpus 8`` as the driver launches it (gloo on the CPU):
+    rank 0 prints ONE JSON line naming the 8-rank job -- n_gpus, world_pg, 8 rank devices, dp8, the
+    aggregate over all ranks and the all-reduce bytes of the MTSS-WGAN-GP step."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"), "--gpus", "8", "--steps", "1",
+           "--warmup", "0", "--batch-per-gpu", "4", "--window", "6", "--features", "3", "--dataset-windows", "16",
+           "--dtype", "float32"]
+    p = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8 and rec["world_pg"] == 8 and len(rec["rank_devices"]) == 8
+    assert rec["config"]["parallelism"] == "dp8" and rec["config"]["global_batch"] == 32
+    assert rec["config"]["windows_per_step"] == 8 * (5 * 4 + 4) and rec["steps"] == 1 and rec["warmup"] == 0
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0 and rec["allreduce"] == "gloo"
+    # critic buffer 5 times + generator once, fp32
+    assert rec["allreduce_bytes_per_step"] > 0 and len(rec["allreduce_exposed_ms_per_step"]) == 8
+
+
+def test_gradsync_graph_routes():
+    """What a hipGraph capture may contain follows the routes the eager buckets took: a bucket
+    that fell back from P2P to gloo makes the step uncapturable; one that fell back to RCCL needs the
+    capture-only communicator; all-P2P needs neither."""
+    from hfrep.parallel.dp import GradSync
+
+    gs = GradSync(None, 2)
+    gs.use_p2p, gs.backend, gs.group = True, "nccl", object()
+    assert gs.needs_graph_group()  # no eager step seen yet: switch (safe)
+    gs.routes = {"p2p"}
+    assert not gs.needs_graph_group() and gs.graph_capturable()
+    gs.routes = {"p2p", "rccl"}  # a bucket over HFREP_DP_P2P_CAP went to RCCL
+    assert gs.needs_graph_group() and gs.graph_capturable()
+    gs.backend = "gloo"
+    gs.routes = {"p2p", "gloo"}  # forced P2P on a gloo group, an oversize bucket took gloo
+    assert not gs.graph_capturable() and not gs.needs_graph_group()
+    gs.routes = {"p2p"}
+    assert gs.graph_capturable()
+    assert GradSync(None, 1).graph_capturable()
 
 
 def test_bench_refuses_gpus_world_mismatch():
