@@ -330,7 +330,21 @@ def cmd_replicate(a) -> int:
                      "sharpe_ex_post": {k: analytics.annualized_sharpe_ratio(post[k], rf_ae) for k in post.columns},
                      "turnover": dict(zip(post.columns, map(float, ae.turnover(c.get("hfd_fullname", {k: k for k in
                                                                                    post.columns}))["Turnover"])))}
-    if a.method == "ae-sweep":
+    if a.method == "ae-sweep" and a.freq == "daily":
+        from .data.io import load_daily_etf
+        from .finance.experiment import daily_factor_study
+
+        lo, _, hi = a.latents.partition("-")
+        latents = list(range(int(lo), int(hi or lo) + 1))
+        daily, _ = load_daily_etf()
+        t0 = time.perf_counter()
+        st = daily_factor_study(daily, latents=latents, seeds=[a.seed], device=dev, dtype=dt)
+        res["ae_sweep_daily"] = {"device": str(dev), "dtype": a.dtype, "seed": a.seed, "rows": int(len(daily)),
+                                 "period": [str(daily.index[0].date()), str(daily.index[-1].date())],
+                                 "elapsed_s": round(time.perf_counter() - t0, 3),
+                                 "fit_s": round(float(st["fit_s"].iloc[0]), 3),
+                                 "metrics": st.set_index("latent").drop(columns=["seed", "fit_s"]).to_dict(orient="index")}
+    elif a.method == "ae-sweep":
         from .finance.experiment import generated_augmentation, latent_sweep
 
         lo, _, hi = a.latents.partition("-")
@@ -401,6 +415,9 @@ def main(argv=None) -> int:
     r = sub.add_parser("replicate", help="hedge-fund clone benchmarks")
     r.add_argument("--method", default="all", choices=["linear", "ae", "all", "ae-sweep"])
     r.add_argument("--latents", default="1-21", help="ae-sweep latent sizes, e.g. 1-21")
+    r.add_argument("--freq", default="monthly", choices=["monthly", "daily"],
+                   help="ae-sweep panel: the 337-month cleaned panel (reference) or the daily ETF excess-return "
+                        "matrix (BASELINE config 2, data.cleaning.build_factor_etf_daily)")
     r.add_argument("--augment", default=None, help="ae-sweep: generated windows .npy (F=36) to add to training")
     r.add_argument("--window", type=int, default=24)
     r.add_argument("--latent", type=int, default=12)

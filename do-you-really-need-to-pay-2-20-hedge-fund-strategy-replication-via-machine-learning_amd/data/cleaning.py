@@ -124,6 +124,71 @@ def build_factor_etf(etf_csv: str, rf: pd.DataFrame, tickers=ETF_TICKERS, overri
     return out
 
 
+def build_rf_daily(ff_daily_csv: str) -> pd.Series:
+    """Daily log risk-free rate log(1 + RF / 100) on the Fama-French trading days."""
+    ff = pd.read_csv(ff_daily_csv, usecols=["Date", "RF"])
+    idx = pd.to_datetime(ff["Date"].astype(str), format="%Y%m%d")
+    return pd.Series(np.log1p(ff["RF"].to_numpy(np.float64) / 100.0), index=pd.DatetimeIndex(idx), name="RF")
+
+
+def build_factor_etf_daily(etf_csv: str, ff_daily_csv: str, tickers=REPRODUCIBLE_ETF, overrides: dict | None = None,
+                           start: str = START, end: str = END):
+    """DAILY excess log returns of the ETF / index factors (BASELINE config 2: the factor autoencoder on a
+    daily ETF-return matrix).  Returns ``(excess, rf_daily)`` on one calendar.
+
+    The calendar is every Fama-French trading day plus every day any selected index has a price, from
+    the first day of ``start``'s month to ``end``.  For each index, L(d) = log of its last price on or
+    before d, and the day's return is L(d) - L(previous calendar day); the first day's return is taken
+    from the last price before the window (the month-end the monthly panel's first return starts from).
+    An index without a price that day returns 0 and its next price carries the whole move, so the
+    returns of a month always sum to log(P_last(m) / P_last(m - 1)), the monthly panel's price relative
+    (``aggregate_daily_to_monthly`` reproduces ``factor_etf_data``; tests/test_data.py).  ``rf_daily`` =
+    log(1 + RF / 100) on Fama-French days, 0 on the others.  Default tickers: the 14 columns the shipped
+    raw prices reproduce."""
+    prices = read_etf_prices(etf_csv)
+    if overrides:
+        prices.update(overrides)
+    rf = build_rf_daily(ff_daily_csv)
+    lo = pd.Timestamp(start).to_period("M").to_timestamp(how="start")
+    hi = pd.Timestamp(end)
+    days = set(rf.loc[lo:hi].index)
+    logp = {}
+    for t in tickers:
+        if t not in prices:
+            continue
+        s = prices[t]
+        s = s[~s.index.duplicated(keep="last")].sort_index()
+        s = s[s > 0]
+        logp[t] = np.log(s.astype(np.float64))
+        days |= set(s.loc[lo:hi].index)
+    cal = pd.DatetimeIndex(sorted(days))
+    cols = {}
+    for t, lp in logp.items():
+        before = lp[lp.index < lo]
+        if before.empty:
+            continue
+        L = lp.reindex(lp.index.union(cal)).ffill().reindex(cal)
+        rel = L.diff()
+        rel.iloc[0] = L.iloc[0] - before.iloc[-1]
+        cols[t] = rel
+    rf_cal = rf.reindex(cal).fillna(0.0)
+    excess = pd.DataFrame(cols, index=cal).sub(rf_cal, axis=0)
+    excess.index.name = "Date"
+    rf_cal.index.name = "Date"
+    return excess, rf_cal
+
+
+def aggregate_daily_to_monthly(excess: pd.DataFrame, rf_daily: pd.Series, rf_monthly: pd.DataFrame) -> pd.DataFrame:
+    """Monthly excess log returns from the daily panel: sum the day's price relatives (excess + daily rf)
+    over each month, minus the monthly rf of ``build_rf`` -- the construction of ``factor_etf_data``."""
+    rel = excess.add(rf_daily, axis=0)
+    m = rel.groupby(rel.index.to_period("M")).sum()
+    m.index = m.index.to_timestamp(how="end").normalize()
+    out = m.reindex(rf_monthly.index).sub(rf_monthly["RF"], axis=0)
+    out.index.name = "Date"
+    return out
+
+
 def build_all(raw_dir: str, out_dir: str | None = None) -> dict:
     """Run the whole pipeline on a reference-layout ``data/`` directory."""
     rf = build_rf(os.path.join(raw_dir, "F-F_Research_Data_Factors_daily.CSV"))

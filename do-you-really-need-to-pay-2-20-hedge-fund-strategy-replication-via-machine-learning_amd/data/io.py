@@ -294,3 +294,23 @@ def load_cleaned(root: str | None = None) -> dict:
             out[key] = {c: c for c in cols}
     out["all_data_name"] = {**out["factor_etf_name"], **out["hfd_fullname"]}
     return out
+
+
+def load_daily_etf(root: str | None = None, tickers=None):
+    """The DAILY ETF excess-return matrix and its daily rf (``cleaning.build_factor_etf_daily``), as
+    ``(excess, rf_daily)`` DataFrame / Series: from ``cleaned_data/factor_etf_daily.csv`` +
+    ``rf_daily.csv`` when staged there (GPU boxes: scripts/stage_reference_data.sh), otherwise built from
+    the raw ``data/ETF_data.csv`` and the Fama-French daily file.  Default: all 22 factor columns (the 8
+    CBOE option indices from the shipped raw prices)."""
+    from .cleaning import ETF_TICKERS, build_factor_etf_daily
+
+    tickers = list(tickers or ETF_TICKERS)
+    root = root or require_data_root()
+    cd = os.path.join(root, "cleaned_data")
+    fx, fr = os.path.join(cd, "factor_etf_daily.csv"), os.path.join(cd, "rf_daily.csv")
+    if os.path.exists(fx) and os.path.exists(fr):
+        ex = read_csv(fx)
+        return ex[[t for t in tickers if t in ex.columns]], read_csv(fr).iloc[:, 0]
+    raw = os.path.join(root, "data")
+    return build_factor_etf_daily(os.path.join(raw, "ETF_data.csv"), os.path.join(raw, "F-F_Research_Data_Factors_daily.CSV"),
+                                  tickers=tickers)

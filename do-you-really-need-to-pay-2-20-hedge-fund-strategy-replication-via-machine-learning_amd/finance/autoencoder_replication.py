@@ -186,7 +186,7 @@ class AE:
     """
 
     def __init__(self, x_train, y_train, x_test, y_test, latent_dim, device="cpu", dtype=torch.float32,
-                 seed: int = 123, scale_test: bool = False, beta_index: str = "first"):
+                 seed: int = 123, scale_test: bool = False, beta_index: str = "first", oos_stride: int = 1):
         assert len(x_train) == len(y_train) and len(y_test) == len(x_test)
         self.train_scale = MinMaxScaler()
         self._x_train = self.train_scale.fit_transform(np.asarray(x_train, dtype=np.float64))
@@ -196,6 +196,9 @@ class AE:
         self._latent_dim = latent_dim
         self.device, self.dtype, self.seed = torch.device(device), dtype, seed
         self.scale_test, self.beta_index = scale_test, beta_index
+        # expanding OOS windows xt[:i] for i = 2, 2 + stride, ... (1 = the reference's every window; the
+        # daily panel evaluates one window per ~month of trading days)
+        self.oos_stride = int(oos_stride)
         self.autoencoder = None
         self.history = None
         self._ante = self._post = None
@@ -282,7 +285,7 @@ class AE:
         cached until the model is retrained."""
         if getattr(self, "_oos_cache", None) is None:
             xt = np.asarray(self._x_test, dtype=np.float64)
-            xrs = [MinMaxScaler().fit_transform(xt[:i]) for i in range(2, len(xt))]
+            xrs = [MinMaxScaler().fit_transform(xt[:i]) for i in range(2, len(xt), self.oos_stride)]
             pred = self._predict(np.concatenate(xrs, 0)) if xrs else np.zeros((0, xt.shape[1]))
             cuts = np.cumsum([len(x) for x in xrs])[:-1]
             self._oos_cache = list(zip(xrs, np.split(pred, cuts)))

@@ -60,3 +60,19 @@ def cuda():
 
     _native.native()  # must load on a GPU box
     return torch.device("cuda")
+
+
+@pytest.fixture(scope="session")
+def daily():
+    """The daily ETF excess-return matrix (staged CSV on GPU boxes, else built from the raw data)."""
+    r = _first_root_with("cleaned_data")
+    if r is None:
+        pytest.skip("reference dataset not available")
+    staged = os.path.exists(os.path.join(r, "cleaned_data", "factor_etf_daily.csv"))
+    if not staged and not os.path.isdir(os.path.join(r, "data")):
+        r = _first_root_with("data")
+        if r is None:
+            pytest.skip("daily ETF prices not available")
+    from hfrep.data.io import load_daily_etf
+
+    return load_daily_etf(r)[0]

@@ -109,3 +109,40 @@ def test_ae_train_many_matches_one_by_one(cuda, cleaned, dt):
         assert a.history["loss"] == b.history["loss"] and a.history["val_loss"] == b.history["val_loss"]
         for pa, pb in zip(a.autoencoder.parts(), b.autoencoder.parts()):
             assert torch.equal(pa.flat, pb.flat)
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, 1e-3), (torch.bfloat16, 5e-2)])
+def test_ae_fit_daily_size_vs_cpu(cuda, daily, dt, tol):
+    """BASELINE config 2 at its stated size: the fused Keras fit (csrc/ae.hip) on the DAILY ETF panel's
+    training half (~3,660 days: ~57 batches per epoch, ~900 validation rows) tracks the CPU fp64 engine
+    over 3 epochs (same weights, same batch order)."""
+    from hfrep.data.scaler import MinMaxScaler
+
+    x = daily.to_numpy(np.float64)
+    x = MinMaxScaler().fit_transform(x[: len(x) // 2])
+    k = 7
+    mg = FactorAutoencoder(k, x.shape[1], seed=3, device=cuda)
+    mc = FactorAutoencoder(k, x.shape[1], seed=3, dtype=torch.float64)
+    with torch.no_grad():
+        for a, b in zip(mg.parts(), mc.parts()):
+            b.flat.copy_(a.flat.double().cpu())
+    hg = AETrainer(mg, device=cuda).fit(x, epochs=3, patience=100, seed=9, dtype=dt, fused=True)
+    hc = AETrainer(mc).fit(x, epochs=3, patience=100, seed=9, dtype=torch.float64)
+    np.testing.assert_allclose(hg["loss"], hc["loss"], rtol=tol * 10, atol=1e-7)
+    np.testing.assert_allclose(hg["val_loss"], hc["val_loss"], rtol=tol * 10, atol=1e-7)
+    for a, b in zip(mg.parts(), mc.parts()):
+        wa, wb = a.flat.detach().double().cpu(), b.flat.detach()
+        rel = ((wa - wb).norm() / wb.norm()).item()
+        assert rel < tol, f"{dt}: weight rel err {rel:.2e}"
+
+
+def test_ae_daily_study_on_gpu(cuda, daily):
+    """The daily factor study (finance.experiment.daily_factor_study): every (latent) fit of the daily
+    panel in one launch, finite reference-style metrics at fp32 and bf16."""
+    from hfrep.finance.experiment import daily_factor_study
+
+    for dt in (torch.float32, torch.bfloat16):
+        st = daily_factor_study(daily, latents=[1, 7, 21], device=cuda, dtype=dt)
+        assert len(st) == 3 and np.isfinite(st[["IS_r2", "IS_RMSE", "OOS_r2", "OOS_RMSE"]].to_numpy()).all()
+        assert (st["IS_r2"] <= 1).all() and st["IS_r2"].iloc[-1] > st["IS_r2"].iloc[0]
+        assert (st["epochs"] >= 1).all() and st["train_rows"].iloc[0] == len(daily) // 2
