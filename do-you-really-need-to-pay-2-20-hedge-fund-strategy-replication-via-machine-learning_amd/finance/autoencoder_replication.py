@@ -245,7 +245,7 @@ class AE:
                    and a0.dtype in (torch.float32, torch.bfloat16)
                    # use_native_for first: with HFREP_ALLOW_TORCH_FALLBACK=1 and no library it is False (the
                    # one-by-one fallback below), where native() would raise
-                   and _native.use_native_for(a0.autoencoder.parts()[0].flat)
+                   and _native.use_native_for(torch.empty(0, device=a0.device))
                    and all(bool(_native.native().ae_fit_supported(A, a._latent_dim, 48)) for a in aes))
         if batched:
             jobs = []
