@@ -931,19 +931,6 @@ void p2p_allreduce_(Tensor x, Tensor buf, std::vector<int64_t> peers, int64_t ra
                               cur_stream(x));
 }
 
-// diagnosis: the fingerprint buffer of an HFREP_FWD4_TRACE build (an empty tensor turns it off)
-void fwd4_trace(Tensor buf) {
-  TORCH_CHECK(buf.numel() == 0 || (buf.is_cuda() && buf.is_contiguous()), "fwd4_trace: contiguous GPU buffer");
-  if (buf.numel()) GUARD(buf);
-  hfrep::lstm2_fwd4_trace(buf.numel() ? buf.data_ptr() : nullptr);
-}
-
-std::vector<int64_t> fwd4_diag(bool reset) {
-  unsigned int c[4];
-  hfrep::lstm2_fwd4_diag(c, reset);
-  return {c[0], c[1], c[2], c[3]};
-}
-
 int64_t p2p_error(Tensor buf) {
   TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kByte, "p2p_error: a p2p_buffer tensor");
   GUARD(buf);
@@ -1014,8 +1001,6 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("p2p_close(int ptr) -> ()", &p2p_close);
   m.def("p2p_allreduce_(Tensor(a!) x, Tensor buf, int[] peers, int rank, int cap, float scale, float timeout_s) -> ()");
   m.def("p2p_error(Tensor buf) -> int");
-  m.def("fwd4_trace(Tensor buf) -> ()");  // diagnosis build only
-  m.def("fwd4_diag(bool reset=False) -> int[]", &fwd4_diag);  // no tensor inputs: catch-all kernel
 }
 
 TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
@@ -1060,7 +1045,6 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("philox_fill_", &philox_fill_);
   m.impl("sample_windows", &sample_windows);
   m.impl("ae_fit", &ae_fit);
-  m.impl("fwd4_trace", &fwd4_trace);
   m.impl("rmsprop_", &rmsprop_);
   m.impl("adam_", &adam_);
   m.impl("nadam_", &nadam_);

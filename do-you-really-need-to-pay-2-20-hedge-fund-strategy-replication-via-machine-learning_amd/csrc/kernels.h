@@ -201,8 +201,6 @@ void p2p_free(void* p);
 void p2p_ipc_handle(void* p, uint8_t out[64]);
 void* p2p_ipc_open(const uint8_t h[64], int device);
 void p2p_ipc_close(void* p);
-void lstm2_fwd4_trace(void* buf);  // HFREP_FWD4_TRACE build: fingerprint buffer (nullptr: off)
-void lstm2_fwd4_diag(unsigned int out[4], bool reset);  // HFREP_FWD4_DIAG build counters (else zeros)
 int p2p_read_error(void* own);  // the sticky error word: 0, or 1 + the rank that gave up first (synchronous)
 uint64_t p2p_timeout_ticks(double seconds, int device);  // seconds -> wall-clock (s_memrealtime) ticks
 int p2p_blocks(int64_t n);

@@ -450,14 +450,11 @@ struct Slot8 {  // 8 bf16 of one 16x16-layout lane: block m = 0, 1 (rows 16 m + 
     return f2_t{lo_bf(w), hi_bf(w)};
   }
 };
-#ifndef HFREP_SLOT8_AUX
-#define HFREP_SLOT8_AUX 0  // (race A/B knob: cache-policy bits of the primal-tape loads)
-#endif
 __device__ __forceinline__ Slot8 ld_slot8(rsrc_t rs, bool on, int lane_off, int uoff) {
   Slot8 s;
   const int v = on ? lane_off * 2 : kOOB;
-  s.m0 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, v, uoff * 2, HFREP_SLOT8_AUX));
-  s.m1 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, v, (uoff + SLOT_HALF) * 2, HFREP_SLOT8_AUX));
+  s.m0 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, v, uoff * 2, 0));
+  s.m1 = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, v, (uoff + SLOT_HALF) * 2, 0));
   return s;
 }
 __device__ __forceinline__ f32x4 mma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
@@ -920,12 +917,7 @@ lstm_tbwd4_kernel(const bf16_t* __restrict__ dH, const bf16_t* __restrict__ dHd,
 // worse, stalled the compute waves at issue, so tape traffic and the recurrence did not overlap.
 // Lanes of padded units (unit >= H) get the out-of-range offset: no bytes written for them.
 constexpr int FW4_STAGE = NW2 * TAPE_SLOTS * SLOT_ELEMS;
-#ifndef HFREP_TAPE_STORE_AUX
-#define HFREP_TAPE_STORE_AUX 2  // (race A/B knob: the cache-policy bits of the tape stream, 2 = nt)
-#endif
-#ifndef HFREP_FWD4_DATA_VMWAIT
-#define HFREP_FWD4_DATA_VMWAIT 0  // (race A/B knob: the data wave waits for its stores at every step)
-#endif
+constexpr int TAPE_STORE_AUX = 2;  // cache-policy bits of the tape stream: 2 = nt (non-temporal)
 template <int H>
 __device__ __forceinline__ void tape_image_store(const bf16_t* img, rsrc_t rt, int t, bool on, int lane) {
   constexpr int NCH = FW4_STAGE / 512, G = 5;  // 1 KiB chunks, stored in groups of G
@@ -946,7 +938,7 @@ __device__ __forceinline__ void tape_image_store(const bf16_t* img, rsrc_t rt, i
       // forward 2.72 -> 2.55 ms, tangent 3.33 -> 3.03 ms at B = 262144; sc1 / sc0 sc1: no gain;
       // nt on the reverse kernels' dZ stores: BPTT +8 %; nt tape loads: tangent reverse +3-4 %.  profiles/archive_scripts/gpu_store_policy.sh,
       // profiles/archive_scripts/gpu_ab_lstm.sh, profiles/r01_fwd5/store_policy.jsonl)
-      __builtin_amdgcn_raw_buffer_store_b128(d[j], rt, ok ? base + ch * 1024 : kOOB, 0, HFREP_TAPE_STORE_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128(d[j], rt, ok ? base + ch * 1024 : kOOB, 0, TAPE_STORE_AUX);
     }
   }
 }
@@ -1016,39 +1008,14 @@ struct XPart {
   }
 };
 
-// Diagnosis build of the act = sigmoid tangent-forward nondeterminism (profiles/r03_race/README.md):
-// HFREP_TFWD4_SIGMOID=1 routes act = sigmoid back to this kernel; HFREP_FWD4_DIAG=1 re-derives, in the
-// last row half, every cell's tangent from accumulator and tape values read again long after the step's
-// MFMAs / loads (inline-asm register reads behind s_nops; tape re-loaded after vmcnt(0)) and counts /
-// prints every cell whose normally scheduled result differs.  Neither is set in the shipped library.
+// HFREP_TFWD4_SIGMOID=1 (diagnosis builds only) routes act = sigmoid's tangent forward to this kernel
+// instead of lstm_tfwd2: on it act = sigmoid drifts run to run in rows 30 / 31 of a few row blocks, a
+// timing-shaped fault that tanh / linear never show, not even under the perturbations that multiply the
+// sigmoid drift (profiles/r05_race/README.md, round-6 section).  The round-5 diagnosis instrumentation of
+// this kernel (in-kernel re-check, fingerprint trace, perturbation probes, tail nops) is retired: its
+// results are recorded there and the builds live in git history (commit d3e5e5a).
 #ifndef HFREP_TFWD4_SIGMOID
 #define HFREP_TFWD4_SIGMOID 0
-#endif
-#ifndef HFREP_FWD4_DIAG
-#define HFREP_FWD4_DIAG 0
-#endif
-#ifndef HFREP_FWD4_TAILNOP
-#define HFREP_FWD4_TAILNOP 0
-#endif
-// HFREP_FWD4_TRACE=1 (diagnosis only): every compute lane of the TAN forward writes, per row block, step
-// and wave, a fingerprint of what its row-half-1 cells of rows 4 g + {2, 3} used -- the xor of the five
-// primal-tape words, the accumulator registers 2 and 3 of the four gates, and the resulting h tangent --
-// to a host-given buffer [rb][t][wave][lane] x uint4, so two runs can be compared value by value
-#ifndef HFREP_FWD4_TRACE
-#define HFREP_FWD4_TRACE 0
-#endif
-#ifndef HFREP_FWD4_PROBE
-#define HFREP_FWD4_PROBE 0
-#endif
-__device__ uint4* g_fwd4_trace;
-__device__ __forceinline__ uint32_t rotl32(uint32_t v, int r) { return (v << r) | (v >> (32 - r)); }
-#if HFREP_FWD4_DIAG
-__device__ unsigned int g_fwd4_diag[4];  // cells checked, accumulator mismatches, tape mismatches, printed
-__device__ __forceinline__ float late_read(float v) {  // a fresh VALU read of v's register, here
-  float r;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
-  return r;
-}
 #endif
 template <int H, int ACT, int KX, bool TAPE, bool TAN>
 __global__ void __launch_bounds__(512)
@@ -1188,13 +1155,6 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 #pragma unroll
               for (int q = 0; q < 4; ++q) acc[q][m] = mma16k16(ah4, uf4[q], acc[q][m]);
             }
-#if HFREP_FWD4_TAILNOP
-            // A/B of the act = sigmoid tangent-forward drift: nothing issues in the 8 wait states after
-            // the last tail MFMAs (the cell math overwrote their SrcC registers 3-4 instructions after issue)
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_nop 7" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-#endif
           }
         }
 #pragma unroll
@@ -1232,71 +1192,12 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
                 const float ca = act_f(act, cv);
                 float hd = odot * ca + og * act_dy(act, ca) * cdn;
                 if (!uok) { cdn = 0.f; hd = 0.f; }
-#if HFREP_FWD4_DIAG
-                if (m == 1) {
-                  const float cs0 = cs[e + u], cp0 = cprev[e + u];
-                  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-                  float al[4];
-#pragma unroll
-                  for (int q = 0; q < 4; ++q) al[q] = late_read(acc[q][m][i]);
-                  // the tape words again, from memory, after every load of this wave has landed
-                  const Slot8 re0 = ld_slot8(rp, uok, lo8, tape_off(t, wt32) + 0 * SLOT_ELEMS);
-                  const Slot8 re4 = ld_slot8(rp, uok, lo8, tape_off(t, wt32) + 4 * SLOT_ELEMS);
-                  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                  const float ig2 = late_read(ig), cv2 = late_read(cv);
-                  const bool tape_bad = uok && (re0.get(m, i) != ig2 || re4.get(m, i) != cv2);
-                  const float idot2 = ig * (1.f - ig) * al[0], fdot2 = fg * (1.f - fg) * al[1];
-                  const float gdot2 = act_dy(act, gg) * al[2], odot2 = og * (1.f - og) * al[3];
-                  float cdn2 = fdot2 * cp0 + fg * cs0 + idot2 * gg + ig * gdot2;
-                  float hd2 = odot2 * ca + og * act_dy(act, ca) * cdn2;
-                  if (!uok) { cdn2 = 0.f; hd2 = 0.f; }
-                  const bool acc_bad = fabsf(hd2 - hd) > 1e-3f * (fabsf(hd2) + 1e-3f) ||
-                                       fabsf(cdn2 - cdn) > 1e-3f * (fabsf(cdn2) + 1e-3f);
-                  atomicAdd(&g_fwd4_diag[0], 1u);
-                  if (acc_bad) atomicAdd(&g_fwd4_diag[1], 1u);
-                  if (tape_bad) atomicAdd(&g_fwd4_diag[2], 1u);
-                  if ((acc_bad || tape_bad) && atomicAdd(&g_fwd4_diag[3], 1u) < 24u)
-                    printf("fwd4-diag rb %d t %d wave %d lane %d row %d i %d acc_bad %d tape_bad %d hd %g/%g cdn %g/%g "
-                           "acc3 %g ig %g/%g\n", rb, t, wave, lane, 16 * m + 4 * g4 + i, i, (int)acc_bad, (int)tape_bad,
-                           hd, hd2, cdn, cdn2, al[3], ig, re0.get(m, i));
-                }
-#endif
                 cs[e + u] = cdn;
                 cprev[e + u] = cv;
                 cd2[u] = cdn; hd2[u] = hd;
               }
               v0 = a0; v1 = a1; v2 = a2; v3 = a3; v4 = cd2; hv = hd2;
             }
-#if HFREP_FWD4_PROBE
-            // (race A/B: a perturbation at the trace point -- 1: wait for every outstanding load, 2: a
-            // dummy LDS write + lgkmcnt(0), 3: an s_nop block)
-            if constexpr (TAN) {
-              if (m == 1 && p == 1) {
-                if constexpr (HFREP_FWD4_PROBE == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if constexpr (HFREP_FWD4_PROBE == 2) {
-                  *reinterpret_cast<volatile uint32_t*>(trash) = __float_as_uint(hv[0]);
-                  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                }
-                if constexpr (HFREP_FWD4_PROBE == 3) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-              }
-            }
-#endif
-#if HFREP_FWD4_TRACE
-            if constexpr (TAN) {
-              if (m == 1 && p == 1 && g_fwd4_trace) {
-                uint32_t tx = 0, ta = 0, tb = 0;
-#pragma unroll
-                for (int s = 0; s < TAPE_SLOTS; ++s) tx ^= rotl32(tg[s].m1.y, 5 * s);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                  ta ^= rotl32(__float_as_uint(acc[q][1][2]), 7 * q);
-                  tb ^= rotl32(__float_as_uint(acc[q][1][3]), 7 * q);
-                }
-                g_fwd4_trace[(((size_t)rb * Tn + t) * NCW + wave) * 64 + lane] =
-                    make_uint4(tx, ta, tb, pk2bf(hv[0], hv[1]));
-              }
-            }
-#endif
             // unconditional: padded unit columns (c in [H, 112)) receive the zeros they must hold
             hnext[rr * LH + c] = f2bf(hv[0]);
             hnext[(rr + 1) * LH + c] = f2bf(hv[1]);
@@ -1335,9 +1236,6 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
         tile8_store_w<H>(hb + (t & 1) * 32 * LH, LH, rh, Tn, t - 1, t > 0 && !(dbg & 2), lane);
         if constexpr (TAPE)
           tape_image_store<H>(tsg + ((t + 1) & 1) * FW4_STAGE, rt, (dbg & 256) ? 0 : t - 1, t > 0 && ton, lane);
-#if HFREP_FWD4_DATA_VMWAIT
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
         lds_barrier();
       }
       tile8_store_w<H>(hb + (Tn & 1) * 32 * LH, LH, rh, Tn, Tn - 1, true, lane);
@@ -1358,25 +1256,6 @@ lstm_fwd4_kernel(const bf16_t* __restrict__ x, const float* __restrict__ W, cons
 // ==========================================================================================
 // host side
 // ==========================================================================================
-// the HFREP_FWD4_TRACE build's fingerprint buffer (nullptr: off)
-void lstm2_fwd4_trace(void* buf) {
-  uint4* p = reinterpret_cast<uint4*>(buf);
-  HFREP_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_fwd4_trace), &p, sizeof(p)));
-}
-// counters of the HFREP_FWD4_DIAG build (zeros otherwise): cells checked, accumulator / tape mismatches
-void lstm2_fwd4_diag(unsigned int out[4], bool reset) {
-#if HFREP_FWD4_DIAG
-  HFREP_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd4_diag), 4 * sizeof(unsigned int)));
-  if (reset) {
-    const unsigned int z[4] = {0, 0, 0, 0};
-    HFREP_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_fwd4_diag), z, sizeof(z)));
-  }
-#else
-  (void)reset;
-  for (int i = 0; i < 4; ++i) out[i] = 0;
-#endif
-}
-
 size_t lstm2_tape_elems(int B, int Tn) { return (size_t)((B + 31) / 32) * Tn * NW2 * TAPE_SLOTS * SLOT_ELEMS; }
 
 static size_t tfwd2_smem(int H, int K) {
