@@ -123,6 +123,40 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> mlp_wgp_critic(Tensor
   return {X2c, dY2, X1c, dY1, Y3c, slab};
 }
 
+bool mlp_wgpw_supported_op(int64_t F, int64_t T) { return hfrep::mlp_wgpw_supported((int)F, (int)T); }
+
+// the GP critic update with in-kernel weight gradients (bf16): adds gW1, gW2, gw3 into the given fp32
+// gradient views (bias gradients cancel, as in mlp_wgp_critic) and returns the W-loss slab
+Tensor mlp_wgp_critic_w(Tensor real, Tensor fake, Tensor c, std::vector<Tensor> cp, Tensor gW1, Tensor gW2,
+                        Tensor gw3) {
+  TORCH_CHECK(act_dt(real) == hfrep::DT_BF16, "mlp_wgp_critic_w: bf16 activations");
+  TORCH_CHECK(fake.scalar_type() == real.scalar_type() && fake.sizes() == real.sizes(), "mlp_wgp_critic_w: fake like real");
+  act_dt(fake);
+  const int64_t F = real.size(-1), H = hidden_of(cp, F), M = rows_of(real, F, "real"), B = real.size(0), T = real.size(1);
+  TORCH_CHECK(hfrep::mlp_wgpw_supported((int)F, (int)T), "mlp_wgp_critic_w: (F, T) = (", F, ", ", T,
+              ") outside the in-kernel weight-gradient variant");
+  const auto cr = critic_of(cp, F, H, T * H);
+  TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kFloat && c.is_contiguous() && c.numel() == B,
+              "mlp_wgp_critic_w: c (B) fp32");
+  for (const Tensor* g : {&gW1, &gW2, &gw3})
+    TORCH_CHECK(g->device() == real.device(), "mlp_wgp_critic_w: gradients on the activations' device");
+  float* pW1 = const_cast<float*>(w(gW1, F * H, "gW1"));
+  float* pW2 = const_cast<float*>(w(gW2, H * H, "gW2"));
+  float* pw3 = const_cast<float*>(w(gw3, T * H, "gw3"));
+  GUARD(real);
+  const int P = hfrep::mlp_wgpw_blocks(M);
+  const int64_t L = (H + F + T) * H;
+  Tensor gslab = at::empty({P, L}, real.options().dtype(at::kFloat));
+  Tensor slab = at::empty({4 * (int64_t)P, 2}, real.options().dtype(at::kFloat));
+  const hipStream_t s = cur_stream(real);
+  hfrep::launch_mlp_wgp_critic_w(real.data_ptr(), fake.data_ptr(), c.data_ptr<float>(), cr, gslab.data_ptr<float>(),
+                                 slab.data_ptr<float>(), M, (int)T, (int)F, s);
+  hfrep::launch_mlp_slab_sum_cols(gslab.data_ptr<float>(), P, L, 0, (int)(H * H), pW2, s);
+  hfrep::launch_mlp_slab_sum_cols(gslab.data_ptr<float>(), P, L, (int)(H * H), (int)(F * H), pW1, s);
+  hfrep::launch_mlp_slab_sum_cols(gslab.data_ptr<float>(), P, L, (int)((H + F) * H), (int)(T * H), pw3, s);
+  return slab;
+}
+
 std::tuple<Tensor, Tensor> mlp_critic_dx(Tensor x, std::vector<Tensor> cp, int64_t head, double label) {
   const int dt = act_dt(x);
   TORCH_CHECK(head == 0 || head == 1, "mlp_critic_dx: head 0 (flatten, W loss) or 1 (per-row sigmoid, BCE)");
@@ -207,6 +241,9 @@ TORCH_LIBRARY_FRAGMENT(hfrep, m) {
   m.def("mlp_wgp_norm(Tensor like, Tensor[] cp) -> Tensor");
   m.def("mlp_wgp_coef(Tensor gsq, float lam) -> (Tensor, Tensor)");
   m.def("mlp_wgp_critic(Tensor real, Tensor fake, Tensor c, Tensor[] cp) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("mlp_wgpw_supported(int F, int T) -> bool", &mlp_wgpw_supported_op);
+  m.def("mlp_wgp_critic_w(Tensor real, Tensor fake, Tensor c, Tensor[] cp, Tensor(a!) gW1, Tensor(b!) gW2, "
+        "Tensor(c!) gw3) -> Tensor");
   m.def("mlp_critic_dx(Tensor x, Tensor[] cp, int head, float label) -> (Tensor, Tensor)");
   m.def("mlp_gan_critic(Tensor x, Tensor[] cp, float label) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("mlp_gen_bwd(Tensor noise, Tensor dfake, Tensor[] gp) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
@@ -217,6 +254,7 @@ TORCH_LIBRARY_FRAGMENT(hfrep, m) {
 
 TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("mlp_gen_fwd", &mlp_gen_fwd);
+  m.impl("mlp_wgp_critic_w", &mlp_wgp_critic_w);
   m.impl("mlp_wgp_norm", &mlp_wgp_norm);
   m.impl("mlp_wgp_coef", &mlp_wgp_coef);
   m.impl("mlp_wgp_critic", &mlp_wgp_critic);

@@ -61,5 +61,16 @@ void launch_mlp_finish(const float* slab, int P, const float* e, int64_t n_e, in
 // every (P, 4 L) slab row into o_k (nullptr: skipped)
 void launch_mlp_slab_sum(const float* slab, int P, int L, float* out, hipStream_t s);
 void launch_mlp_slab_sum4(const float* slab, int P, int L, float* o0, float* o1, float* o2, float* o3, hipStream_t s);
+// out[j] += sum_p slab[p * stride + col0 + j], j < L (fixed order)
+void launch_mlp_slab_sum_cols(const float* slab, int P, int64_t stride, int col0, int L, float* out, hipStream_t s);
+
+// The GP critic update with its three weight gradients accumulated in the kernel (bf16 only; T <= 64
+// and the LDS plan must fit: mlp_wgpw_supported).  Launches mlp_wgpw_blocks(M) workgroups; gslab
+// (blocks x (H + F + T) H fp32) gets each workgroup's partial [gW2 | gW1 | gw3], slab (4 blocks x 2)
+// the per-wave W-loss partials of mlp_wgp_critic.  Every slab element is written.
+bool mlp_wgpw_supported(int F, int Tn);
+int mlp_wgpw_blocks(int64_t M);
+void launch_mlp_wgp_critic_w(const void* real, const void* fake, const float* c, const MlpCritic& cr, float* gslab,
+                             float* slab, int64_t M, int Tn, int F, hipStream_t s);
 
 }  // namespace hfrep

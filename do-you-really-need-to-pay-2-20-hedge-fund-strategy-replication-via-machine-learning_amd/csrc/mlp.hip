@@ -32,6 +32,7 @@
 #include "mlp.h"
 
 #include <algorithm>
+#include <stdexcept>
 
 namespace hfrep {
 
@@ -509,6 +510,237 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_wgp_critic_kernel(
   slab_put(slab, 2, 1, sf);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// The same critic update with the three weight gradients accumulated in the kernel (bf16).
+//
+// mlp_wgp_critic writes 5 per-row operands (872 B a row at F = 36) that linear_wgrad_ reads back:
+// ~11 GB of HBM traffic per update at B*T = 6.3 M rows.  Here the 4 waves of a workgroup walk 128-row
+// block tiles together.  After the per-row chain (unchanged) each wave stages its 32 rows of X2c, X1c and
+// Y3c in LDS, TRANSPOSED (feature-major [f][row], bf16, pitch WQ), and the block's 128 rows become the
+// k dimension of three small GEMMs on v_mfma_f32_32x32x16_bf16, wave w owning output columns
+// o = 32 w .. 32 w + 31:
+//   gW2[i][o] += sum_r X2c[r][i] w3_{t(r)}[o]     A: one ds_read_b128 of img2 row i, B: gathered from
+//   gW1[i][o] += sum_r X1c[r][i] dh1'_{t(r)}[o]        the per-t tables (w3_t and dh1'_t = W2 w3_t are
+//   gw3[t][o] += sum_r [t(r) = t] Y3c[r][o]             functions of t only: built once per workgroup)
+// (A: the one-hot of t(r), built in registers; B: one ds_read_b128 of img3 row o.)  The 8-row runs the
+// fragments need are contiguous in the transposed images, so every MFMA operand is one 16-byte read;
+// WQ = 136 bf16 makes those reads conflict-free (272 B row stride = 68 dwords: 16 lanes hit 16 distinct
+// 4-bank groups).  The per-workgroup partial gradients go to one fp32 slab row per workgroup, summed in
+// a fixed order by mlp_slab_sum.  Two barriers per block tile: before the staging writes (the previous
+// tile's readers are done) and before the reads.
+// ---------------------------------------------------------------------------------------------------
+constexpr int WQ = 136;  // pitch (bf16) of a transposed staging row: 128 rows + 8
+
+template <int F, int H> constexpr size_t wgpw_images() {
+  return (size_t)(fwd_entries<bf16_t, F, H>() + fwd_entries<bf16_t, H, H>() + dgrad_entries<bf16_t, H, H>() +
+                  dgrad_entries<bf16_t, F, H>()) *
+             frag_bytes<bf16_t>() +
+         2 * VEC * 4;
+}
+// byte offsets: [images][img2: H x WQ][img3: H x WQ][img1: F x WQ][toff: 128 ints][w3 table][dh1' table]
+template <int F, int H> constexpr size_t wgpw_off_img2() { return wgpw_images<F, H>(); }
+template <int F, int H> constexpr size_t wgpw_off_img3() { return wgpw_off_img2<F, H>() + (size_t)H * WQ * 2; }
+template <int F, int H> constexpr size_t wgpw_off_img1() { return wgpw_off_img3<F, H>() + (size_t)H * WQ * 2; }
+template <int F, int H> constexpr size_t wgpw_off_toff() { return wgpw_off_img1<F, H>() + (size_t)F * WQ * 2; }
+template <int F, int H> constexpr size_t wgpw_off_tab() { return wgpw_off_toff<F, H>() + 128 * 4; }
+template <int F, int H> constexpr size_t wgpw_lds(int Tn) { return wgpw_off_tab<F, H>() + 2 * (size_t)Tn * 128 * 2; }
+static_assert(wgpw_off_img3<36, 100>() % 16 == 0 && wgpw_off_toff<36, 100>() % 16 == 0, "16-byte aligned images");
+static_assert(wgpw_off_img3<32, 100>() % 16 == 0 && wgpw_off_toff<32, 100>() % 16 == 0, "16-byte aligned images");
+
+__device__ __forceinline__ float dpp_xor1(float v) {
+  // quad_perm [1, 0, 3, 2]: the value of lane ^ 1
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+}
+// this lane's row rr (block-local, 0..127) of accumulator tiles a -> img[f][rr] for f < N; even lanes
+// write the (rr, rr + 1) pair as one dword
+template <int N>
+__device__ __forceinline__ void stage_t(unsigned short* img, const f32x16* a, int rr, int h) {
+#pragma unroll
+  for (int t = 0; t < (N + 31) / 32; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float v = a[t][q];
+      const float p = dpp_xor1(v);
+      const int f = 32 * t + featq(q, h);
+      if (f < N && !(rr & 1)) *reinterpret_cast<uint32_t*>(img + f * WQ + rr) = pk2bf(v, p);
+    }
+}
+// a per-t table row (bf16, 128 features) from accumulator tiles; zeros past N come from a
+template <int N>
+__device__ __forceinline__ void table_put(unsigned short* row, const f32x16* a, int h) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * t + 8 * g + 4 * h;
+      const float4 v = t < (N + 31) / 32 ? make_float4(a[t][4 * g], a[t][4 * g + 1], a[t][4 * g + 2], a[t][4 * g + 3])
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<uint2*>(row + f0) = make_uint2(pk2bf(v.x, v.y), pk2bf(v.z, v.w));
+    }
+}
+// B fragment gathered from a per-t table: element j = tab[ofs[j] + col]
+__device__ __forceinline__ bf16x8 gather8(const unsigned short* tab, const int* ofs, int col) {
+  u32x4_t u;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) u[e] = (uint32_t)tab[ofs[2 * e] + col] | ((uint32_t)tab[ofs[2 * e + 1] + col] << 16);
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+template <int F, int H, int NTT>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_wgp_critic_w_kernel(
+    const bf16_t* __restrict__ real, const bf16_t* __restrict__ fake, const float* __restrict__ cvec, MlpCritic c,
+    float* __restrict__ gslab, float* __restrict__ slab, int64_t M, int Tn, float invB) {
+  using T = bf16_t;
+  using Fr = bf16x8;
+  constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  Fr* f1 = reinterpret_cast<Fr*>(lds);
+  Fr* f2 = f1 + fwd_entries<T, F, H>() * 64;
+  Fr* d2 = f2 + fwd_entries<T, H, H>() * 64;
+  Fr* d1 = d2 + dgrad_entries<T, H, H>() * 64;
+  float* vec = reinterpret_cast<float*>(d1 + dgrad_entries<T, F, H>() * 64);
+  unsigned short* img2 = reinterpret_cast<unsigned short*>(lds + wgpw_off_img2<F, H>());
+  unsigned short* img3 = reinterpret_cast<unsigned short*>(lds + wgpw_off_img3<F, H>());
+  unsigned short* img1 = reinterpret_cast<unsigned short*>(lds + wgpw_off_img1<F, H>());
+  int* toff = reinterpret_cast<int*>(lds + wgpw_off_toff<F, H>());
+  unsigned short* tabw = reinterpret_cast<unsigned short*>(lds + wgpw_off_tab<F, H>());
+  unsigned short* tabd = tabw + Tn * 128;
+  build_fwd<T, F, H>(f1, c.W1);
+  build_fwd<T, H, H>(f2, c.W2);
+  build_dgrad<T, H, H>(d2, c.W2);
+  build_dgrad<T, F, H>(d1, c.W1);
+  load_vec(vec, c.b1, H);
+  load_vec(vec + VEC, c.b2, H);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, h = lane >> 5, w = threadIdx.x >> 6, cl = lane & 31;
+  // per-t tables: wave w < NTT computes t = 32 w + lane (the chain's own head_rows / dense, so the table
+  // holds exactly the bf16 values the operand path stored per row)
+  if (w < NTT) {
+    const int t = 32 * w + cl;
+    const bool ok = t < Tn;
+    f32x16 A[NTH], Bv[NTH];
+    head_rows<H>(A, c.w3 + (int64_t)(ok ? t : 0) * H, 1.f, ok, h);
+    dense<T, H, H>(A, Bv, d2, lane);
+    if (ok) {
+      table_put<H>(tabw + t * 128, A, h);
+      table_put<H>(tabd + t * 128, Bv, h);
+    }
+  }
+  f32x16 gW2[NTH], gW1[NTF], gw3[NTT];
+#pragma unroll
+  for (int i = 0; i < NTH; ++i) gW2[i] = zero16();
+#pragma unroll
+  for (int i = 0; i < NTF; ++i) gW1[i] = zero16();
+#pragma unroll
+  for (int i = 0; i < NTT; ++i) gw3[i] = zero16();
+  float sr = 0.f, sf = 0.f;
+  const int rr = 32 * w + cl;  // this lane's block-local row
+  const int64_t nbt = (M + 127) / 128;
+  for (int64_t bt = blockIdx.x; bt < nbt; bt += gridDim.x) {
+    const int64_t row = bt * 128 + rr;
+    const bool ok = row < M;
+    const int64_t bidx = ok ? row / Tn : 0;
+    const int tr = ok ? (int)(row - bidx * Tn) : 0;
+    const float* w3t = c.w3 + (int64_t)tr * H;
+    f32x16 A[NTH], Bv[NTH], X2[NTH], X1[NTF], x[NTF];
+    head_rows<H>(A, w3t, 1.f, ok, h);
+    dense<T, H, H>(A, Bv, d2, lane);            // dh1' = W2 w3_t
+    dense<T, H, F>(Bv, X1, d1, lane);           // g = W1 dh1'
+    const float cb = ok ? cvec[bidx] : 0.f;
+#pragma unroll
+    for (int t = 0; t < NTF; ++t) X1[t] *= cb;  // v
+    dense<T, F, H>(X1, X2, f1, lane);           // zd1 = v W1
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const float sg = pass ? invB : -invB;
+      load_rows<T, F>(x, pass ? fake : real, row, M, h);
+      axpy<F>(X1, sg, x);
+      dense<T, F, H>(x, A, f1, lane);
+      bias_act<H>(A, vec, ACT_LINEAR, h);       // h1
+      axpy<H>(X2, sg, A);
+      dense<T, H, H>(A, Bv, f2, lane);
+      bias_act<H>(Bv, vec + VEC, ACT_LINEAR, h);  // h2
+      const float sc = rowdot<H>(Bv, w3t, ok, h);
+      if (ok && h == 0) {
+        if (pass) sf += sc;
+        else sr += sc;
+      }
+    }
+    // rows past M contribute nothing (their operands are exactly what the zero inputs give, up to an
+    // fma residue of b1 / B - b1 / B: zeroed explicitly)
+    if (!ok) {
+#pragma unroll
+      for (int t = 0; t < NTH; ++t) X2[t] = zero16();
+#pragma unroll
+      for (int t = 0; t < NTF; ++t) X1[t] = zero16();
+    }
+    dense<T, H, H>(X2, A, f2, lane);            // Y3c = X2c W2
+    __syncthreads();  // the previous block tile's wgrad reads are done
+    stage_t<H>(img2, X2, rr, h);
+    stage_t<H>(img3, A, rr, h);
+    stage_t<F>(img1, X1, rr, h);
+    if (h == 0) toff[rr] = tr * 128;
+    __syncthreads();
+#pragma unroll 2
+    for (int ks = 0; ks < 8; ++ks) {
+      const int r0 = 16 * ks + 8 * h;
+      const int4 oa = *reinterpret_cast<const int4*>(toff + r0), ob = *reinterpret_cast<const int4*>(toff + r0 + 4);
+      const int ofs[8] = {oa.x, oa.y, oa.z, oa.w, ob.x, ob.y, ob.z, ob.w};
+      const int col = 32 * w + cl;
+      const Fr bw = gather8(tabw, ofs, col), bd = gather8(tabd, ofs, col);
+#pragma unroll
+      for (int it = 0; it < NTH; ++it) {
+        const int i = min(32 * it + cl, H - 1);
+        gW2[it] = MF<T>::mma(*reinterpret_cast<const Fr*>(img2 + i * WQ + r0), bw, gW2[it]);
+      }
+#pragma unroll
+      for (int it = 0; it < NTF; ++it) {
+        const int i = min(32 * it + cl, F - 1);
+        gW1[it] = MF<T>::mma(*reinterpret_cast<const Fr*>(img1 + i * WQ + r0), bd, gW1[it]);
+      }
+      const Fr b3 = *reinterpret_cast<const Fr*>(img3 + min(col, H - 1) * WQ + r0);
+#pragma unroll
+      for (int tt = 0; tt < NTT; ++tt) {
+        const int want = (32 * tt + cl) * 128;
+        u32x4_t u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          u[e] = (ofs[2 * e] == want ? 0x3F80u : 0u) | (ofs[2 * e + 1] == want ? 0x3F800000u : 0u);
+        gw3[tt] = MF<T>::mma(__builtin_bit_cast(Fr, u), b3, gw3[tt]);
+      }
+    }
+  }
+  // this workgroup's partial gradients: [gW2 H x H][gW1 F x H][gw3 Tn x H], wave w writes columns 32 w ..
+  const int64_t L = (int64_t)(H + F + Tn) * H;
+  float* g = gslab + (int64_t)blockIdx.x * L;
+  const int o = 32 * w + cl;
+  if (o < H) {
+#pragma unroll
+    for (int it = 0; it < NTH; ++it)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = 32 * it + featq(q, h);
+        if (i < H) g[i * H + o] = gW2[it][q];
+      }
+#pragma unroll
+    for (int it = 0; it < NTF; ++it)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = 32 * it + featq(q, h);
+        if (i < F) g[(H + i) * H + o] = gW1[it][q];
+      }
+#pragma unroll
+    for (int tt = 0; tt < NTT; ++tt)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int t = 32 * tt + featq(q, h);
+        if (t < Tn) g[(H + F + t) * H + o] = gw3[tt][q];
+      }
+  }
+  slab_put(slab, 2, 0, sr);
+  slab_put(slab, 2, 1, sf);
+}
+
 // ===================================================================================================
 // critic input gradient for the generator step (and its loss): head 0 = the linear WGAN-GP critic
 // with W(fake, -1) (GAN/WGAN_GP.py:178-189), head 1 = the GAN discriminator Dense -> Dense ->
@@ -838,22 +1070,25 @@ __global__ void __launch_bounds__(256) mlp_finish_kernel(const float* __restrict
 
 // out[k][j] += sum_p slab[p][k L + j] for the nseg segments: 64 elements per workgroup, the 16 waves
 // split the P rows (4 partial sums each so loads overlap), combined in a fixed order (deterministic)
-__global__ void __launch_bounds__(1024) mlp_slab_sum_kernel(const float* __restrict__ slab, int P, int L, int nseg,
-                                                            float* __restrict__ o0, float* __restrict__ o1,
-                                                            float* __restrict__ o2, float* __restrict__ o3) {
+// (slab rows have `stride` floats; the summed columns start at col0)
+__global__ void __launch_bounds__(1024) mlp_slab_sum_kernel(const float* __restrict__ slab, int P, int64_t stride,
+                                                            int col0, int L, int nseg, float* __restrict__ o0,
+                                                            float* __restrict__ o1, float* __restrict__ o2,
+                                                            float* __restrict__ o3) {
   __shared__ float part[16][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane, n = nseg * L;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (i < n) {
+    const float* col = slab + col0 + i;
     int p = wv;
     for (; p + 48 < P; p += 64) {
-      s0 += slab[(int64_t)p * n + i];
-      s1 += slab[(int64_t)(p + 16) * n + i];
-      s2 += slab[(int64_t)(p + 32) * n + i];
-      s3 += slab[(int64_t)(p + 48) * n + i];
+      s0 += col[(int64_t)p * stride];
+      s1 += col[(int64_t)(p + 16) * stride];
+      s2 += col[(int64_t)(p + 32) * stride];
+      s3 += col[(int64_t)(p + 48) * stride];
     }
-    for (; p < P; p += 16) s0 += slab[(int64_t)p * n + i];
+    for (; p < P; p += 16) s0 += col[(int64_t)p * stride];
   }
   part[wv][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
@@ -1049,12 +1284,50 @@ void launch_mlp_finish(const float* slab, int P, const float* e, int64_t n_e, in
 }
 
 void launch_mlp_slab_sum(const float* slab, int P, int L, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((L + 63) / 64), dim3(1024), 0, s, slab, P, L, 1, out, nullptr, nullptr,
-                     nullptr);
+  hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((L + 63) / 64), dim3(1024), 0, s, slab, P, (int64_t)L, 0, L, 1, out,
+                     nullptr, nullptr, nullptr);
 }
 
 void launch_mlp_slab_sum4(const float* slab, int P, int L, float* o0, float* o1, float* o2, float* o3, hipStream_t s) {
-  hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((4 * L + 63) / 64), dim3(1024), 0, s, slab, P, L, 4, o0, o1, o2, o3);
+  hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((4 * L + 63) / 64), dim3(1024), 0, s, slab, P, (int64_t)4 * L, 0, L, 4,
+                     o0, o1, o2, o3);
+}
+
+void launch_mlp_slab_sum_cols(const float* slab, int P, int64_t stride, int col0, int L, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((L + 63) / 64), dim3(1024), 0, s, slab, P, stride, col0, L, 1, out,
+                     nullptr, nullptr, nullptr);
+}
+
+// ---- GP critic update with in-kernel weight gradients (bf16) ----
+bool mlp_wgpw_supported(int F, int Tn) {
+  if (Tn < 1 || Tn > 64 || !(F == 32 || F == 36)) return false;
+  const size_t lds = F == 32 ? wgpw_lds<32, 100>(Tn) : wgpw_lds<36, 100>(Tn);
+  return lds <= 160 * 1024;
+}
+
+int mlp_wgpw_blocks(int64_t M) {
+  const int64_t nbt = (M + 127) / 128;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(nbt, (int64_t)device_cu_count()));
+}
+
+void launch_mlp_wgp_critic_w(const void* real, const void* fake, const float* c, const MlpCritic& cr, float* gslab,
+                             float* slab, int64_t M, int Tn, int F, hipStream_t s) {
+  if (M <= 0) return;
+  if (!mlp_wgpw_supported(F, Tn))
+    throw std::runtime_error("mlp_wgp_critic_w: (F, T) outside the in-kernel weight-gradient variant");
+  const float invB = (float)Tn / (float)M;
+  const int P = mlp_wgpw_blocks(M);
+  auto go = [&](auto kern, size_t lds) {
+    set_lds(kern, lds);
+    hipLaunchKernelGGL(kern, dim3(P), dim3(MLP_THREADS), lds, s, (const bf16_t*)real, (const bf16_t*)fake, c, cr, gslab,
+                       slab, M, Tn, invB);
+  };
+  if (F == 32) {
+    if (Tn <= 32) go(mlp_wgp_critic_w_kernel<32, 100, 1>, wgpw_lds<32, 100>(Tn));
+    else go(mlp_wgp_critic_w_kernel<32, 100, 2>, wgpw_lds<32, 100>(Tn));
+  } else {  // F = 36: the LDS plan leaves room for T <= 27 tables only (one t tile)
+    go(mlp_wgp_critic_w_kernel<36, 100, 1>, wgpw_lds<36, 100>(Tn));
+  }
 }
 
 }  // namespace hfrep

@@ -10,7 +10,8 @@ replaces it with one kernel per pass that carries a 32-row tile through every la
   sample and the adjoint coefficient c_b (GAN/WGAN_GP.py:201-216);
 * ``mlp_wgp_critic``  a whole WGAN-GP critic update of the linear critic (GAN/WGAN_GP.py:238-253):
   W terms on real / fake and the reverse-over-tangent of the penalty, as one combined weight-gradient
-  operand per weight (see the kernel's comment);
+  operand per weight (see the kernel's comment); in bf16 ``mlp_wgp_critic_w`` also accumulates the
+  three weight gradients in the kernel (128-row block tiles staged transposed in LDS);
 * ``mlp_gan_critic``  a vanilla-GAN discriminator update (GAN/GAN.py:144-158, 187-189);
 * ``mlp_critic_dx`` + ``mlp_gen_bwd``  the generator update through the frozen critic
   (GAN/WGAN_GP.py:178-189, GAN/GAN.py:195-198);
@@ -86,6 +87,13 @@ class FusedMLP:
         self.gw, self.gg = _gen_lists(tr.generator), _gen_lists(tr.generator, grad=True)
         self.cw, self.cg = _critic_lists(tr.critic, self.head), _critic_lists(tr.critic, self.head, grad=True)
         self._ones = {}
+        # bf16 GP critic update with the weight gradients accumulated inside the pass kernel
+        # (mlp_wgp_critic_w): no per-row operands in HBM.  HFREP_MLP_WGRAD_INKERNEL=0 keeps the operand
+        # path (mlp_wgp_critic + linear_wgrad_) for A/B; fp32 always uses it (its LDS images leave no room)
+        cfg = tr.cfg
+        self.wgrad_inkernel = (self.head == 0 and tr.dtype == torch.bfloat16
+                               and os.environ.get("HFREP_MLP_WGRAD_INKERNEL", "1") != "0"
+                               and bool(_ops().mlp_wgpw_supported(int(cfg.features), int(cfg.window))))
 
     @staticmethod
     def supported(tr) -> bool:
@@ -132,8 +140,11 @@ class FusedMLP:
         B, T = real.shape[0], real.shape[1]
         gsq = ops.mlp_wgp_norm(real, self.cw)
         c, e = ops.mlp_wgp_coef(gsq, float(tr.gp_weight))
-        X2c, dY2, X1c, dY1, Y3c, slab = ops.mlp_wgp_critic(real, fake, c, self.cw)
         gW1, _gb1, gW2, _gb2, gw3, _gb3 = self.cg
+        if self.wgrad_inkernel:
+            slab = ops.mlp_wgp_critic_w(real, fake, c, self.cw, gW1, gW2, gw3)
+            return ops.mlp_finish(slab, e, 0, 1.0 / B, self.cw[5], float(tr.gp_weight))
+        X2c, dY2, X1c, dY1, Y3c, slab = ops.mlp_wgp_critic(real, fake, c, self.cw)
         # the W terms' bias gradients cancel (-1/B and +1/B per row pair) and the tangent has none
         Fn.linear_wgrad_(X2c, dY2, gW2, None)
         Fn.linear_wgrad_(X1c, dY1, gW1, None)

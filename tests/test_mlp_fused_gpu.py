@@ -152,3 +152,32 @@ def test_mlp_fused_large_batch_slices(cuda):
                 acc += tg.critic.flat.grad / 4
         rel = _rel(full, acc)
         assert rel < (1e-5 if dtype == "float32" else 2e-2), f"{dtype}: full vs slice-average rel {rel:.2e}"
+
+
+@pytest.mark.parametrize("B,T,F", [(37, 24, 32), (300, 40, 32), (45, 24, 36), (6000, 24, 32)])
+def test_mlp_wgp_inkernel_wgrad_matches_operand_path(cuda, B, T, F):
+    """bf16 config 4: the GP critic update with the weight gradients accumulated in the kernel
+    (mlp_wgp_critic_w: 128-row block tiles staged transposed in LDS, per-t tables for w3_t and
+    W2 w3_t, one-hot MFMA for gw3) vs the operand path (mlp_wgp_critic + linear_wgrad_) on the same
+    batch.  Both round the same operands to bf16 and differ only in the fp32 summation order; two
+    in-kernel runs are bitwise identical.  Shapes: partial block tile, two t tiles (T = 40), F = 36,
+    and a batch that takes several grid rounds."""
+    ops = torch.ops.hfrep
+    assert not ops.mlp_wgpw_supported(36, 48)  # the LDS plan: F = 36 takes T <= 27
+    tg, _ = _pair(cuda, "wgan_gp", "bfloat16", B, T, F)
+    fz, dt = tg._fused, tg.dtype
+    assert fz.wgrad_inkernel
+    real, noise, _ = _inputs(B, T, F, seed=5)
+    grads, packs = [], []
+    with torch.no_grad():
+        fake = ops.mlp_gen_fwd(noise.to(cuda, dt), fz.gw)
+        r = real.to(cuda, dt)
+        for inkernel in (True, True, False):
+            fz.wgrad_inkernel = inkernel
+            tg.critic.zero_grad()
+            packs.append(fz._wgp_critic_grads(r, fake).clone())
+            grads.append(tg.critic.flat.grad.clone())
+    assert torch.equal(grads[0], grads[1]) and torch.equal(packs[0], packs[1])
+    rel = _rel(grads[0], grads[2])
+    assert rel < 1e-4, f"in-kernel vs operand-path critic gradient rel {rel:.2e}"
+    torch.testing.assert_close(packs[0], packs[2], rtol=1e-5, atol=1e-6)
