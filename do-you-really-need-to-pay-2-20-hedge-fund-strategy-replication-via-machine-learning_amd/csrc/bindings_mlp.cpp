@@ -157,6 +157,64 @@ Tensor mlp_wgp_critic_w(Tensor real, Tensor fake, Tensor c, std::vector<Tensor> 
   return slab;
 }
 
+// the generator reverse with in-kernel parameter gradients (bf16): adds the gradients of
+// [W1, b1, gamma1, beta1, W2, b2, gamma2, beta2, W3, b3] into the fp32 views gg
+void mlp_gen_bwd_w(Tensor noise, Tensor dfake, std::vector<Tensor> gp, std::vector<Tensor> gg) {
+  TORCH_CHECK(act_dt(noise) == hfrep::DT_BF16, "mlp_gen_bwd_w: bf16 activations");
+  act_dt(dfake);
+  TORCH_CHECK(dfake.scalar_type() == noise.scalar_type() && dfake.sizes() == noise.sizes(), "mlp_gen_bwd_w: dfake like noise");
+  const int64_t F = noise.size(-1), H = hidden_of(gp, F), M = rows_of(noise, F, "noise");
+  const auto g = gen_of(gp, F, H);
+  TORCH_CHECK(gg.size() == 10, "mlp_gen_bwd_w: 10 gradient views");
+  const int64_t n[10] = {F * H, H, H, H, H * H, H, H, H, H * F, F};
+  float* p[10];
+  for (int i = 0; i < 10; ++i) {
+    TORCH_CHECK(gg[i].device() == noise.device(), "mlp_gen_bwd_w: gradients on the activations' device");
+    p[i] = const_cast<float*>(w(gg[i], n[i], "generator gradient"));
+  }
+  GUARD(noise);
+  const int P = hfrep::mlp_gbw_blocks(M);
+  const int64_t L = F * H + H + H * H + H + H * F + F;
+  Tensor gslab = at::empty({P, L}, noise.options().dtype(at::kFloat));
+  Tensor lnslab = at::empty({4 * (int64_t)P, 4 * H}, noise.options().dtype(at::kFloat));
+  const hipStream_t s = cur_stream(noise);
+  hfrep::launch_mlp_gen_bwd_w(noise.data_ptr(), dfake.data_ptr(), g, gslab.data_ptr<float>(), lnslab.data_ptr<float>(), M,
+                              (int)F, s);
+  // slab segments in the order [W1][b1][W2][b2][W3][b3]
+  const int seg[6] = {0, 1, 4, 5, 8, 9};
+  int64_t col = 0;
+  for (int k : seg) {
+    hfrep::launch_mlp_slab_sum_cols(gslab.data_ptr<float>(), P, L, (int)col, (int)n[k], p[k], s);
+    col += n[k];
+  }
+  hfrep::launch_mlp_slab_sum4(lnslab.data_ptr<float>(), 4 * P, (int)H, p[2], p[3], p[6], p[7], s);
+}
+
+// the GAN discriminator update with its six gradients in the kernel (fp32 / bf16): adds them into the
+// fp32 views cg = [gW1, gb1, gW2, gb2, gw3, gb3] and returns the loss slab
+Tensor mlp_gan_critic_g(Tensor x, std::vector<Tensor> cp, double label, std::vector<Tensor> cg) {
+  const int dt = act_dt(x);
+  const int64_t F = x.size(-1), H = hidden_of(cp, F), M = rows_of(x, F, "x");
+  const auto cr = critic_of(cp, F, H, H);
+  TORCH_CHECK(cg.size() == 6, "mlp_gan_critic_g: 6 gradient views");
+  const int64_t n[6] = {F * H, H, H * H, H, H, 1};
+  float* p[6];
+  for (int i = 0; i < 6; ++i) {
+    TORCH_CHECK(cg[i].device() == x.device(), "mlp_gan_critic_g: gradients on the activations' device");
+    p[i] = const_cast<float*>(w(cg[i], n[i], "critic gradient"));
+  }
+  GUARD(x);
+  const int64_t L = F + 2 * H + 1;
+  Tensor gslab = slab_new(x, M, L), slab = slab_new(x, M, 2);
+  Tensor v = at::zeros({L}, x.options().dtype(at::kFloat));
+  const hipStream_t s = cur_stream(x);
+  hfrep::launch_mlp_gan_critic_g(dt, x.data_ptr(), cr, (float)label, gslab.data_ptr<float>(), slab.data_ptr<float>(), M,
+                                 (int)F, s);
+  hfrep::launch_mlp_slab_sum(gslab.data_ptr<float>(), (int)gslab.size(0), (int)L, v.data_ptr<float>(), s);
+  hfrep::launch_mlp_gan_grad_finish(v.data_ptr<float>(), cr, (int)F, (int)H, p[0], p[1], p[2], p[3], p[4], p[5], s);
+  return slab;
+}
+
 std::tuple<Tensor, Tensor> mlp_critic_dx(Tensor x, std::vector<Tensor> cp, int64_t head, double label) {
   const int dt = act_dt(x);
   TORCH_CHECK(head == 0 || head == 1, "mlp_critic_dx: head 0 (flatten, W loss) or 1 (per-row sigmoid, BCE)");
@@ -244,6 +302,8 @@ TORCH_LIBRARY_FRAGMENT(hfrep, m) {
   m.def("mlp_wgpw_supported(int F, int T) -> bool", &mlp_wgpw_supported_op);
   m.def("mlp_wgp_critic_w(Tensor real, Tensor fake, Tensor c, Tensor[] cp, Tensor(a!) gW1, Tensor(b!) gW2, "
         "Tensor(c!) gw3) -> Tensor");
+  m.def("mlp_gen_bwd_w(Tensor noise, Tensor dfake, Tensor[] gp, Tensor(a!)[] gg) -> ()");
+  m.def("mlp_gan_critic_g(Tensor x, Tensor[] cp, float label, Tensor(a!)[] cg) -> Tensor");
   m.def("mlp_critic_dx(Tensor x, Tensor[] cp, int head, float label) -> (Tensor, Tensor)");
   m.def("mlp_gan_critic(Tensor x, Tensor[] cp, float label) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("mlp_gen_bwd(Tensor noise, Tensor dfake, Tensor[] gp) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
@@ -255,6 +315,8 @@ TORCH_LIBRARY_FRAGMENT(hfrep, m) {
 TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("mlp_gen_fwd", &mlp_gen_fwd);
   m.impl("mlp_wgp_critic_w", &mlp_wgp_critic_w);
+  m.impl("mlp_gen_bwd_w", &mlp_gen_bwd_w);
+  m.impl("mlp_gan_critic_g", &mlp_gan_critic_g);
   m.impl("mlp_wgp_norm", &mlp_wgp_norm);
   m.impl("mlp_wgp_coef", &mlp_wgp_coef);
   m.impl("mlp_wgp_critic", &mlp_wgp_critic);

@@ -68,6 +68,22 @@ void launch_mlp_slab_sum_cols(const float* slab, int P, int64_t stride, int col0
 // and the LDS plan must fit: mlp_wgpw_supported).  Launches mlp_wgpw_blocks(M) workgroups; gslab
 // (blocks x (H + F + T) H fp32) gets each workgroup's partial [gW2 | gW1 | gw3], slab (4 blocks x 2)
 // the per-wave W-loss partials of mlp_wgp_critic.  Every slab element is written.
+// The generator reverse with its parameter gradients accumulated in the kernel (bf16, F in {32, 36}):
+// mlp_gbw_blocks(M) workgroups; gslab rows (one per workgroup) = [W1 F x H][b1 H][W2 H x H][b2 H]
+// [W3 H x F][b3 F] partials, lnslab (4 rows per workgroup, 4 H) = the LayerNorm partials of
+// launch_mlp_gen_bwd.  Every slab element is written.
+// The GAN discriminator update with its gradients in the kernel (fp32 / bf16): mlp_slab_rows(M) rows of
+// gslab ([s1 F | s2 H | s3 H | S], the per-wave dz-weighted column sums of x, h1, h2 and dz) and of the
+// loss slab (2 columns, as launch_mlp_gan_critic).  launch_mlp_gan_grad_finish adds the gradients
+// gW1 = s1 (x) W2 w3, gb1 = S W2 w3, gW2 = s2 (x) w3, gb2 = S w3, gw3 = s3, gb3 = S from the REDUCED
+// sums v (F + 2 H + 1 floats).
+void launch_mlp_gan_critic_g(int dt, const void* x, const MlpCritic& cr, float label, float* gslab, float* slab,
+                             int64_t M, int F, hipStream_t s);
+void launch_mlp_gan_grad_finish(const float* v, const MlpCritic& cr, int F, int H, float* gW1, float* gb1, float* gW2,
+                                float* gb2, float* gw3, float* gb3, hipStream_t s);
+int mlp_gbw_blocks(int64_t M);
+void launch_mlp_gen_bwd_w(const void* noise, const void* dfake, const MlpGen& g, float* gslab, float* lnslab, int64_t M,
+                          int F, hipStream_t s);
 bool mlp_wgpw_supported(int F, int Tn);
 int mlp_wgpw_blocks(int64_t M);
 void launch_mlp_wgp_critic_w(const void* real, const void* fake, const float* c, const MlpCritic& cr, float* gslab,

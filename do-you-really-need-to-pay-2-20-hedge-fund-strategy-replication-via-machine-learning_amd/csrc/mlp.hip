@@ -205,13 +205,14 @@ __device__ __forceinline__ void store_rows(T* __restrict__ y, int64_t row, int64
 template <int N>
 __device__ __forceinline__ void head_rows(f32x16* a, const float* __restrict__ w, float sc, bool ok, int h) {
   constexpr int NT = (N + 31) / 32;
+  const float* wh = w + 4 * h;  // lane-half base: the per-(t, g) offsets below fold into immediates
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int f0 = 32 * t + 8 * g + 4 * h;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok && f0 < N) v = *reinterpret_cast<const float4*>(w + f0);
+      if (ok && f0 < N) v = *reinterpret_cast<const float4*>(wh + 32 * t + 8 * g);
       a[t][4 * g] = sc * v.x; a[t][4 * g + 1] = sc * v.y; a[t][4 * g + 2] = sc * v.z; a[t][4 * g + 3] = sc * v.w;
     }
 }
@@ -219,6 +220,7 @@ __device__ __forceinline__ void head_rows(f32x16* a, const float* __restrict__ w
 template <int N>
 __device__ __forceinline__ float rowdot(const f32x16* a, const float* __restrict__ w, bool ok, int h) {
   constexpr int NT = (N + 31) / 32;
+  const float* wh = w + 4 * h;
   float s = 0.f;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -226,7 +228,7 @@ __device__ __forceinline__ float rowdot(const f32x16* a, const float* __restrict
     for (int g = 0; g < 4; ++g) {
       const int f0 = 32 * t + 8 * g + 4 * h;
       if (ok && f0 < N) {
-        const float4 v = *reinterpret_cast<const float4*>(w + f0);
+        const float4 v = *reinterpret_cast<const float4*>(wh + 32 * t + 8 * g);
         s = fmaf(a[t][4 * g], v.x, s); s = fmaf(a[t][4 * g + 1], v.y, s);
         s = fmaf(a[t][4 * g + 2], v.z, s); s = fmaf(a[t][4 * g + 3], v.w, s);
       }
@@ -237,12 +239,13 @@ __device__ __forceinline__ float rowdot(const f32x16* a, const float* __restrict
 template <int N>
 __device__ __forceinline__ void bias_act(f32x16* a, const float* b, int act, int h) {
   constexpr int NT = (N + 31) / 32;
+  const float* bh = b + 4 * h;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int f0 = 32 * t + 8 * g + 4 * h;
-      const float4 bv = *reinterpret_cast<const float4*>(b + f0);
+      const float4 bv = *reinterpret_cast<const float4*>(bh + 32 * t + 8 * g);
       const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -265,6 +268,7 @@ template <int N>
 __device__ __forceinline__ void lrelu_ln(f32x16* a, const float* gam, const float* bet, int h, float& mean,
                                          float& rstd) {
   constexpr int NT = (N + 31) / 32;
+  const float *gh = gam + 4 * h, *beh = bet + 4 * h;
   float s = 0.f;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -290,7 +294,8 @@ __device__ __forceinline__ void lrelu_ln(f32x16* a, const float* gam, const floa
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int f0 = 32 * t + 8 * g + 4 * h;
-      const float4 gv = *reinterpret_cast<const float4*>(gam + f0), bv = *reinterpret_cast<const float4*>(bet + f0);
+      const float4 gv = *reinterpret_cast<const float4*>(gh + 32 * t + 8 * g),
+                   bv = *reinterpret_cast<const float4*>(beh + 32 * t + 8 * g);
       const float gg[4] = {gv.x, gv.y, gv.z, gv.w}, bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -851,6 +856,171 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_gan_critic_kernel(const T* __
   slab_put(slab, 2, 1, 0.f);
 }
 
+// LayerNorm -> LeakyReLU -> sigmoid reverse of one row (the generator's Dense(sigmoid) + LReLU + LN
+// blocks): g = dL/du (LN output gradient), y = the sigmoid outputs, (mean, rstd) of lrelu(y); writes
+// dL/dz into out (may alias g or y: element-wise after the row sums) and adds the gamma-gradient
+// column sums (sum_r g * xhat) into pg
+template <int N>
+__device__ __forceinline__ void ln_reverse(const f32x16* g, const f32x16* y, f32x16* out, const float* gam, float mean,
+                                           float rstd, int h, int lane, float* pg) {
+  constexpr int NT = (N + 31) / 32;
+  const float* gh = gam + 4 * h;
+  float m1 = 0.f, m2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int f0 = 32 * t + 8 * gq + 4 * h;
+      const float4 gv = *reinterpret_cast<const float4*>(gh + 32 * t + 8 * gq);
+      const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int q = 4 * gq + e;
+        const bool in = f0 + e < N;
+        const float xh = in ? (lrelu(y[t][q]) - mean) * rstd : 0.f;
+        const float gd = in ? g[t][q] * gg[e] : 0.f;
+        m1 += gd;
+        m2 = fmaf(gd, xh, m2);
+      }
+    }
+  m1 += __shfl_xor(m1, 32, 64);
+  m2 += __shfl_xor(m2, 32, 64);
+  m1 *= 1.f / N;
+  m2 *= 1.f / N;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    f32x16 px;
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int f0 = 32 * t + 8 * gq + 4 * h;
+      const float4 gv = *reinterpret_cast<const float4*>(gh + 32 * t + 8 * gq);
+      const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int q = 4 * gq + e;
+        const bool in = f0 + e < N;
+        const float yv = y[t][q];
+        const float xh = in ? (lrelu(yv) - mean) * rstd : 0.f;
+        const float dv = in ? g[t][q] : 0.f;
+        px[q] = dv * xh;
+        float dl = rstd * (dv * gg[e] - m1 - xh * m2);
+        dl *= yv >= 0.f ? 1.f : LRELU_ALPHA_F;
+        out[t][q] = in ? dl * yv * (1.f - yv) : 0.f;
+      }
+    }
+    pg[t] += colsum(px, lane);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// The same discriminator update with its six parameter gradients taken in the kernel.  The hidden
+// layers are linear, so every adjoint of a row is that row's scalar dz times a fixed vector:
+//   dh2 = dz w3,  dh1 = dz u (u = W2 w3)
+// and each weight gradient factorises into a dz-weighted column sum of the layer's own input:
+//   gW1 = s1 (x) u,  gW2 = s2 (x) w3,  gw3 = s3,  gb1 = S u,  gb2 = S w3,  gb3 = S
+//   s1 = sum_r dz_r x_r,  s2 = sum_r dz_r h1_r,  s3 = sum_r dz_r h2_r,  S = sum_r dz_r.
+// Each lane accumulates dz * (x, h1, h2) of its rows in registers over all its tiles (fp32); one
+// transpose-reduce butterfly per tile set at the end gives the wave's column sums (slab row of the
+// wave: [s1 F | s2 H | s3 H | S]); mlp_gan_grad_finish reduces the slab in a fixed order and forms
+// the outer products.  The per-row forward and BCE are the same as mlp_gan_critic's.
+// ---------------------------------------------------------------------------------------------------
+template <typename T, int F, int H>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_gan_critic_g_kernel(const T* __restrict__ x, MlpCritic c, float label,
+                                                                       float* __restrict__ gslab,
+                                                                       float* __restrict__ slab, int64_t M, float inv) {
+  using Fr = typename MP<T>::frag;
+  constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  Fr* f1 = reinterpret_cast<Fr*>(lds);
+  Fr* f2 = f1 + fwd_entries<T, F, H>() * 64;
+  float* vec = reinterpret_cast<float*>(f2 + fwd_entries<T, H, H>() * 64);
+  build_fwd<T, F, H>(f1, c.W1);
+  build_fwd<T, H, H>(f2, c.W2);
+  load_vec(vec, c.b1, H);
+  load_vec(vec + VEC, c.b2, H);
+  load_vec(vec + 2 * VEC, c.w3, H);
+  __syncthreads();
+  const float b3 = c.b3 ? c.b3[0] : 0.f;
+  float acc = 0.f, sdz = 0.f;
+  f32x16 ax[NTF], a1[NTH], a2[NTH];
+#pragma unroll
+  for (int t = 0; t < NTF; ++t) ax[t] = zero16();
+#pragma unroll
+  for (int t = 0; t < NTH; ++t) a1[t] = a2[t] = zero16();
+  MLP_LOOP {
+    const int64_t row = tile * 32 + (lane & 31);
+    const bool ok = row < M;
+    f32x16 A[NTH], Bv[NTH], X[NTF];
+    load_rows<T, F>(X, x, row, M, h);
+    dense<T, F, H>(X, A, f1, lane);
+    bias_act<H>(A, vec, ACT_LINEAR, h);         // h1
+    dense<T, H, H>(A, Bv, f2, lane);
+    bias_act<H>(Bv, vec + VEC, ACT_LINEAR, h);  // h2
+    const float p = sigmoidf_(rowdot<H>(Bv, vec + 2 * VEC, true, h) + b3);
+    float lo, gp;
+    bce(p, label, inv, lo, gp);
+    const float dz = ok ? gp * p * (1.f - p) : 0.f;
+    if (ok && h == 0) {
+      acc += lo;
+      sdz += dz;
+    }
+#pragma unroll
+    for (int t = 0; t < NTF; ++t) ax[t] += dz * X[t];
+#pragma unroll
+    for (int t = 0; t < NTH; ++t) {
+      a1[t] += dz * A[t];
+      a2[t] += dz * Bv[t];
+    }
+  }
+  constexpr int L = F + 2 * H + 1;
+  float* out = gslab + ((int64_t)blockIdx.x * MLP_WAVES + (threadIdx.x >> 6)) * L;
+  const int fq = featq(colsum_q(lane), h);
+#pragma unroll
+  for (int t = 0; t < NTF; ++t) {
+    const float v = colsum(ax[t], lane);
+    if ((lane & 1) == 0 && 32 * t + fq < F) out[32 * t + fq] = v;
+  }
+#pragma unroll
+  for (int t = 0; t < NTH; ++t) {
+    const float v1 = colsum(a1[t], lane), v2 = colsum(a2[t], lane);
+    if ((lane & 1) == 0 && 32 * t + fq < H) {
+      out[F + 32 * t + fq] = v1;
+      out[F + H + 32 * t + fq] = v2;
+    }
+  }
+  sdz = wave_sum(sdz);
+  if ((threadIdx.x & 63) == 0) out[F + 2 * H] = sdz;
+  slab_put(slab, 2, 0, acc);
+  slab_put(slab, 2, 1, 0.f);
+}
+
+// the six gradients from the reduced sums v = [s1 F | s2 H | s3 H | S] (one workgroup, fp32)
+__global__ void __launch_bounds__(256) mlp_gan_grad_finish_kernel(const float* __restrict__ v, MlpCritic c, int F, int H,
+                                                                  float* __restrict__ gW1, float* __restrict__ gb1,
+                                                                  float* __restrict__ gW2, float* __restrict__ gb2,
+                                                                  float* __restrict__ gw3, float* __restrict__ gb3) {
+  __shared__ float u[128], w3[128];
+  const float* s1 = v;
+  const float* s2 = v + F;
+  const float* s3 = v + F + H;
+  const float S = v[F + 2 * H];
+  for (int i = threadIdx.x; i < H; i += blockDim.x) {
+    float a = 0.f;
+    for (int o = 0; o < H; ++o) a = fmaf(c.W2[i * H + o], c.w3[o], a);  // u = W2 w3
+    u[i] = a;
+    w3[i] = c.w3[i];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < F * H; e += blockDim.x) gW1[e] += s1[e / H] * u[e % H];
+  for (int e = threadIdx.x; e < H * H; e += blockDim.x) gW2[e] += s2[e / H] * w3[e % H];
+  for (int o = threadIdx.x; o < H; o += blockDim.x) {
+    gb1[o] += S * u[o];
+    gb2[o] += S * w3[o];
+    gw3[o] += s3[o];
+  }
+  if (threadIdx.x == 0) gb3[0] += S;
+}
+
 // ===================================================================================================
 // generator reverse pass (GAN/WGAN_GP.py:178-189 / GAN/GAN.py:195-198: the combined model's update)
 // from dfake = dL/dG(z): recomputes the forward in registers and writes the weight-gradient operands
@@ -903,53 +1073,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_gen_bwd_kernel(const T* __res
     dense<T, F, H>(x, d, d3, lane);
 #pragma unroll
     for (int t = 0; t < NTH; ++t) pb2[t] += colsum(d[t], lane);
-    {
-      float m1 = 0.f, m2 = 0.f;
-#pragma unroll
-      for (int t = 0; t < NTH; ++t)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int f0 = 32 * t + 8 * gq + 4 * h;
-          const float4 gv = *reinterpret_cast<const float4*>(gam2 + f0);
-          const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int q = 4 * gq + e;
-            const bool in = f0 + e < H;
-            const float xh = in ? (lrelu(y2[t][q]) - mean2) * rstd2 : 0.f;
-            const float gd = in ? d[t][q] * gg[e] : 0.f;
-            m1 += gd;
-            m2 = fmaf(gd, xh, m2);
-          }
-        }
-      m1 += __shfl_xor(m1, 32, 64);
-      m2 += __shfl_xor(m2, 32, 64);
-      m1 *= 1.f / H;
-      m2 *= 1.f / H;
-#pragma unroll
-      for (int t = 0; t < NTH; ++t) {
-        f32x16 px;
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int f0 = 32 * t + 8 * gq + 4 * h;
-          const float4 gv = *reinterpret_cast<const float4*>(gam2 + f0);
-          const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int q = 4 * gq + e;
-            const bool in = f0 + e < H;
-            const float yv = y2[t][q];
-            const float xh = in ? (lrelu(yv) - mean2) * rstd2 : 0.f;
-            const float dv = in ? d[t][q] : 0.f;
-            px[q] = dv * xh;
-            float dl = rstd2 * (dv * gg[e] - m1 - xh * m2);
-            dl *= yv >= 0.f ? 1.f : LRELU_ALPHA_F;
-            d[t][q] = in ? dl * yv * (1.f - yv) : 0.f;
-          }
-        }
-        pg2[t] += colsum(px, lane);
-      }
-    }
+    ln_reverse<H>(d, y2, d, gam2, mean2, rstd2, h, lane, pg2);
     store_rows<T, H>(dz2o, row, M, d, h);
     // ---- du1 = dz2 W2^T; recompute y1; LN1 / LReLU / sigmoid reverse -> dz1
     dense<T, H, H>(d, y2, d2, lane);  // y2 now holds du1
@@ -958,57 +1082,229 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_gen_bwd_kernel(const T* __res
     load_rows<T, F>(x, z, row, M, h);
     dense<T, F, H>(x, a, f1, lane);
     bias_act<H>(a, vec + 0 * VEC, ACT_SIGMOID, h);  // y1
-    {
-      float m1 = 0.f, m2 = 0.f;
-#pragma unroll
-      for (int t = 0; t < NTH; ++t)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int f0 = 32 * t + 8 * gq + 4 * h;
-          const float4 gv = *reinterpret_cast<const float4*>(gam1 + f0);
-          const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int q = 4 * gq + e;
-            const bool in = f0 + e < H;
-            const float xh = in ? (lrelu(a[t][q]) - mean1) * rstd1 : 0.f;
-            const float gd = in ? y2[t][q] * gg[e] : 0.f;
-            m1 += gd;
-            m2 = fmaf(gd, xh, m2);
-          }
-        }
-      m1 += __shfl_xor(m1, 32, 64);
-      m2 += __shfl_xor(m2, 32, 64);
-      m1 *= 1.f / H;
-      m2 *= 1.f / H;
-#pragma unroll
-      for (int t = 0; t < NTH; ++t) {
-        f32x16 px;
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int f0 = 32 * t + 8 * gq + 4 * h;
-          const float4 gv = *reinterpret_cast<const float4*>(gam1 + f0);
-          const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int q = 4 * gq + e;
-            const bool in = f0 + e < H;
-            const float yv = a[t][q];
-            const float xh = in ? (lrelu(yv) - mean1) * rstd1 : 0.f;
-            const float dv = in ? y2[t][q] : 0.f;
-            px[q] = dv * xh;
-            float dl = rstd1 * (dv * gg[e] - m1 - xh * m2);
-            dl *= yv >= 0.f ? 1.f : LRELU_ALPHA_F;
-            a[t][q] = in ? dl * yv * (1.f - yv) : 0.f;
-          }
-        }
-        pg1[t] += colsum(px, lane);
-      }
-    }
+    ln_reverse<H>(y2, a, a, gam1, mean1, rstd1, h, lane, pg1);
     store_rows<T, H>(dz1o, row, M, a, h);
   }
   // per-wave LN partials: lanes with bit 0 clear own feature featq(colsum_q(lane), h) of every tile
   float* out = lnslab + ((int64_t)blockIdx.x * MLP_WAVES + (threadIdx.x >> 6)) * 4 * H;
+  if ((lane & 1) == 0) {
+#pragma unroll
+    for (int t = 0; t < NTH; ++t) {
+      const int f = 32 * t + featq(colsum_q(lane), h);
+      if (f < H) {
+        out[f] = pg1[t];
+        out[H + f] = pb1[t];
+        out[2 * H + f] = pg2[t];
+        out[3 * H + f] = pb2[t];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// The generator reverse with its six parameter gradients (W1, b1, W2, b2, W3, b3) accumulated in the
+// kernel (bf16), the scheme of mlp_wgp_critic_w: 4 waves walk 128-row block tiles together, stage the
+// X / dY operands of each weight transposed in LDS and run the block's rows as the k dimension of
+// gW = X^T dY on v_mfma_f32_32x32x16_bf16.  The bias gradients come out of the same MFMAs: every X
+// image has a row of ones after its last feature (written once), so C row K of gW is sum_r dY[r].
+// Four staging buffers, reused as the chain produces operands (two barriers per weight):
+//   A: u1 -> dz1     B: u2 -> dz2     C: dfake     D: noise
+//   gW3 (+ gb3): X = u2 (B), dY = dfake (C); wave w owns input tile w, every output tile
+//   gW2 (+ gb2): X = u1 (A), dY = dz2 (B);   wave w owns output tile w
+//   gW1 (+ gb1): X = noise (D), dY = dz1 (A); wave w owns output tile w
+// LayerNorm parameter gradients stay the per-wave colsum partials of mlp_gen_bwd (lnslab).
+// ---------------------------------------------------------------------------------------------------
+template <int F, int H> constexpr size_t gbw_images() {
+  return (size_t)(fwd_entries<bf16_t, F, H>() + fwd_entries<bf16_t, H, H>() + dgrad_entries<bf16_t, H, F>() +
+                  dgrad_entries<bf16_t, H, H>()) *
+             frag_bytes<bf16_t>() +
+         6 * VEC * 4;
+}
+template <int F, int H> constexpr size_t gbw_off_a() { return gbw_images<F, H>(); }
+template <int F, int H> constexpr size_t gbw_off_b() { return gbw_off_a<F, H>() + (size_t)(H + 1) * WQ * 2; }
+template <int F, int H> constexpr size_t gbw_off_c() { return gbw_off_b<F, H>() + (size_t)(H + 1) * WQ * 2; }
+template <int F, int H> constexpr size_t gbw_off_d() { return gbw_off_c<F, H>() + (size_t)F * WQ * 2; }
+template <int F, int H> constexpr size_t gbw_lds() { return gbw_off_d<F, H>() + (size_t)(F + 1) * WQ * 2; }
+static_assert(gbw_lds<36, 100>() <= 160 * 1024, "generator reverse staging exceeds LDS");
+static_assert(gbw_off_b<36, 100>() % 16 == 0 && gbw_off_c<36, 100>() % 16 == 0 && gbw_off_d<36, 100>() % 16 == 0,
+              "16-byte aligned staging images");
+static_assert(gbw_off_b<32, 100>() % 16 == 0 && gbw_off_c<32, 100>() % 16 == 0 && gbw_off_d<32, 100>() % 16 == 0,
+              "16-byte aligned staging images");
+
+// rows past M stage zeros
+template <int N>
+__device__ __forceinline__ void stage_t_ok(unsigned short* img, f32x16* a, int rr, int h, bool ok) {
+  if (!ok) {
+#pragma unroll
+    for (int t = 0; t < (N + 31) / 32; ++t) a[t] = zero16();
+  }
+  stage_t<N>(img, a, rr, h);
+}
+// gW[tile] += X^T dY over the block's 128 rows: A = rows of the X image (clamped to row KX: the ones
+// row or a discarded one), B = row `col` of the dY image
+template <int NI>
+__device__ __forceinline__ void wgrad_block(f32x16* acc, const unsigned short* X, int i0, int KX,
+                                            const unsigned short* Y, int col, int cl, int h) {
+#pragma unroll 2
+  for (int ks = 0; ks < 8; ++ks) {
+    const int r0 = 16 * ks + 8 * h;
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(Y + col * WQ + r0);
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int i = min(i0 + 32 * it + cl, KX);
+      acc[it] = MF<bf16_t>::mma(*reinterpret_cast<const bf16x8*>(X + i * WQ + r0), b, acc[it]);
+    }
+  }
+}
+
+// acc[ot] += X^T dY for ONE input row i of X and NO output tiles (B = rows 32 ot + lane of the dY
+// image, clamped to KY - 1)
+template <int NO>
+__device__ __forceinline__ void wgrad_block_out(f32x16* acc, const unsigned short* X, int i, const unsigned short* Y,
+                                                int KY, int cl, int h) {
+#pragma unroll 2
+  for (int ks = 0; ks < 8; ++ks) {
+    const int r0 = 16 * ks + 8 * h;
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(X + i * WQ + r0);
+#pragma unroll
+    for (int ot = 0; ot < NO; ++ot) {
+      const int o = min(32 * ot + cl, KY - 1);
+      acc[ot] = MF<bf16_t>::mma(a, *reinterpret_cast<const bf16x8*>(Y + o * WQ + r0), acc[ot]);
+    }
+  }
+}
+
+template <int F, int H>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_gen_bwd_w_kernel(const bf16_t* __restrict__ z,
+                                                                    const bf16_t* __restrict__ dfake, MlpGen g,
+                                                                    float* __restrict__ gslab,
+                                                                    float* __restrict__ lnslab, int64_t M) {
+  using T = bf16_t;
+  using Fr = bf16x8;
+  constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32, NX1 = (F + 1 + 31) / 32;
+  static_assert((H + 1 + 31) / 32 == NTH, "the ones row of the H-wide images fits the last input tile");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  Fr* f1 = reinterpret_cast<Fr*>(lds);
+  Fr* f2 = f1 + fwd_entries<T, F, H>() * 64;
+  Fr* d3 = f2 + fwd_entries<T, H, H>() * 64;
+  Fr* d2 = d3 + dgrad_entries<T, H, F>() * 64;
+  float* vec = reinterpret_cast<float*>(d2 + dgrad_entries<T, H, H>() * 64);
+  unsigned short* bA = reinterpret_cast<unsigned short*>(lds + gbw_off_a<F, H>());
+  unsigned short* bB = reinterpret_cast<unsigned short*>(lds + gbw_off_b<F, H>());
+  unsigned short* bC = reinterpret_cast<unsigned short*>(lds + gbw_off_c<F, H>());
+  unsigned short* bD = reinterpret_cast<unsigned short*>(lds + gbw_off_d<F, H>());
+  build_fwd<T, F, H>(f1, g.W1);
+  build_fwd<T, H, H>(f2, g.W2);
+  build_dgrad<T, H, F>(d3, g.W3);
+  build_dgrad<T, H, H>(d2, g.W2);
+  load_vec(vec + 0 * VEC, g.b1, H); load_vec(vec + 1 * VEC, g.g1, H); load_vec(vec + 2 * VEC, g.be1, H);
+  load_vec(vec + 3 * VEC, g.b2, H); load_vec(vec + 4 * VEC, g.g2, H); load_vec(vec + 5 * VEC, g.be2, H);
+  for (int r = threadIdx.x; r < 128; r += blockDim.x) {  // the ones rows (bf16 1.0)
+    bA[H * WQ + r] = 0x3F80;
+    bB[H * WQ + r] = 0x3F80;
+    bD[F * WQ + r] = 0x3F80;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, h = lane >> 5, w = threadIdx.x >> 6, cl = lane & 31;
+  const int rr = 32 * w + cl;
+  const float* gam1 = vec + 1 * VEC;
+  const float* gam2 = vec + 4 * VEC;
+  float pg1[NTH], pb1[NTH], pg2[NTH], pb2[NTH];
+#pragma unroll
+  for (int t = 0; t < NTH; ++t) pg1[t] = pb1[t] = pg2[t] = pb2[t] = 0.f;
+  f32x16 gW3[NTF], gW2[NTH], gW1[NX1];
+#pragma unroll
+  for (int i = 0; i < NTF; ++i) gW3[i] = zero16();
+#pragma unroll
+  for (int i = 0; i < NTH; ++i) gW2[i] = zero16();
+#pragma unroll
+  for (int i = 0; i < NX1; ++i) gW1[i] = zero16();
+  const int64_t nbt = (M + 127) / 128;
+  for (int64_t bt = blockIdx.x; bt < nbt; bt += gridDim.x) {
+    const int64_t row = bt * 128 + rr;
+    const bool ok = row < M;
+    f32x16 x[NTF], a[NTH], y2[NTH], d[NTH];
+    float mean1, rstd1, mean2, rstd2;
+    __syncthreads();  // S0: the previous block tile's gW1 reads (A, D) are done
+    load_rows<T, F>(x, z, row, M, h);
+    stage_t_ok<F>(bD, x, rr, h, ok);
+    dense<T, F, H>(x, a, f1, lane);
+    bias_act<H>(a, vec + 0 * VEC, ACT_SIGMOID, h);
+    lrelu_ln<H>(a, vec + 1 * VEC, vec + 2 * VEC, h, mean1, rstd1);  // u1
+    dense<T, H, H>(a, y2, f2, lane);
+    stage_t_ok<H>(bA, a, rr, h, ok);
+    bias_act<H>(y2, vec + 3 * VEC, ACT_SIGMOID, h);
+#pragma unroll
+    for (int t = 0; t < NTH; ++t) a[t] = y2[t];
+    lrelu_ln<H>(a, vec + 4 * VEC, vec + 5 * VEC, h, mean2, rstd2);  // u2
+    stage_t_ok<H>(bB, a, rr, h, ok);
+    load_rows<T, F>(x, dfake, row, M, h);  // zeros past M
+    stage_t<F>(bC, x, rr, h);
+    dense<T, F, H>(x, d, d3, lane);        // du2 = dfake W3^T
+#pragma unroll
+    for (int t = 0; t < NTH; ++t) pb2[t] += colsum(d[t], lane);
+    ln_reverse<H>(d, y2, d, gam2, mean2, rstd2, h, lane, pg2);  // dz2 (y2 dead from here)
+    __syncthreads();  // S1: u1, u2, dfake, noise staged
+    __builtin_amdgcn_sched_barrier(0);
+    wgrad_block_out<NTF>(gW3, bB, min(32 * w + cl, H), bC, F, cl, h);  // gW3[i in tile w][o = 32 ot + cl]
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();  // S2: the gW3 reads of B are done
+    stage_t_ok<H>(bB, d, rr, h, ok);
+    dense<T, H, H>(d, y2, d2, lane);  // y2 now holds du1
+    __syncthreads();  // S2b: dz2 staged
+    __builtin_amdgcn_sched_barrier(0);
+    wgrad_block<NTH>(gW2, bA, 0, H, bB, min(32 * w + cl, H - 1), cl, h);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < NTH; ++t) pb1[t] += colsum(y2[t], lane);
+    load_rows<T, F>(x, z, row, M, h);
+    dense<T, F, H>(x, a, f1, lane);
+    bias_act<H>(a, vec + 0 * VEC, ACT_SIGMOID, h);  // y1
+    ln_reverse<H>(y2, a, a, gam1, mean1, rstd1, h, lane, pg1);  // dz1
+    __syncthreads();  // S3: the gW2 reads of A are done
+    stage_t_ok<H>(bA, a, rr, h, ok);
+    __syncthreads();  // S3b: dz1 staged
+    __builtin_amdgcn_sched_barrier(0);
+    wgrad_block<NX1>(gW1, bD, 0, F, bA, min(32 * w + cl, H - 1), cl, h);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // partial gradients of this workgroup: [W1 F x H][b1 H][W2 H x H][b2 H][W3 H x F][b3 F]
+  constexpr int oB1 = F * H, oW2 = oB1 + H, oB2 = oW2 + H * H, oW3 = oB2 + H, oB3 = oW3 + H * F, L = oB3 + F;
+  float* gs = gslab + (int64_t)blockIdx.x * L;
+  {
+    const int o = 32 * w + cl;  // gW2 / gW1 output column
+    if (o < H) {
+#pragma unroll
+      for (int it = 0; it < NTH; ++it)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int i = 32 * it + featq(q, h);
+          if (i < H) gs[oW2 + i * H + o] = gW2[it][q];
+          else if (i == H) gs[oB2 + o] = gW2[it][q];
+        }
+#pragma unroll
+      for (int it = 0; it < NX1; ++it)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int i = 32 * it + featq(q, h);
+          if (i < F) gs[i * H + o] = gW1[it][q];
+          else if (i == F) gs[oB1 + o] = gW1[it][q];
+        }
+    }
+#pragma unroll
+    for (int ot = 0; ot < NTF; ++ot) {
+      const int o3 = 32 * ot + cl;
+      if (o3 < F) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int i = 32 * w + featq(q, h);
+          if (i < H) gs[oW3 + i * F + o3] = gW3[ot][q];
+          else if (i == H) gs[oB3 + o3] = gW3[ot][q];
+        }
+      }
+    }
+  }
+  float* out = lnslab + ((int64_t)blockIdx.x * MLP_WAVES + w) * 4 * H;
   if ((lane & 1) == 0) {
 #pragma unroll
     for (int t = 0; t < NTH; ++t) {
@@ -1296,6 +1592,42 @@ void launch_mlp_slab_sum4(const float* slab, int P, int L, float* o0, float* o1,
 void launch_mlp_slab_sum_cols(const float* slab, int P, int64_t stride, int col0, int L, float* out, hipStream_t s) {
   hipLaunchKernelGGL(mlp_slab_sum_kernel, dim3((L + 63) / 64), dim3(1024), 0, s, slab, P, stride, col0, L, 1, out,
                      nullptr, nullptr, nullptr);
+}
+
+// ---- GAN discriminator update with in-kernel gradients (both dtypes) ----
+void launch_mlp_gan_critic_g(int dt, const void* x, const MlpCritic& cr, float label, float* gslab, float* slab,
+                             int64_t M, int F, hipStream_t s) {
+  if (M <= 0) return;
+  MLP_DISPATCH(dt, F, {
+    auto k = mlp_gan_critic_g_kernel<T, FF, 100>;
+    constexpr size_t lds = (size_t)(fwd_entries<T, FF, 100>() + fwd_entries<T, 100, 100>()) * frag_bytes<T>() +
+                           3 * VEC * 4;
+    set_lds(k, lds);
+    hipLaunchKernelGGL(k, dim3(slab_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, (const T*)x, cr, label, gslab, slab, M,
+                       1.f / (float)M);
+  });
+}
+
+void launch_mlp_gan_grad_finish(const float* v, const MlpCritic& cr, int F, int H, float* gW1, float* gb1, float* gW2,
+                                float* gb2, float* gw3, float* gb3, hipStream_t s) {
+  hipLaunchKernelGGL(mlp_gan_grad_finish_kernel, dim3(1), dim3(256), 0, s, v, cr, F, H, gW1, gb1, gW2, gb2, gw3, gb3);
+}
+
+// ---- generator reverse with in-kernel parameter gradients (bf16) ----
+int mlp_gbw_blocks(int64_t M) { return mlp_wgpw_blocks(M); }
+
+void launch_mlp_gen_bwd_w(const void* noise, const void* dfake, const MlpGen& g, float* gslab, float* lnslab, int64_t M,
+                          int F, hipStream_t s) {
+  if (M <= 0) return;
+  const int P = mlp_gbw_blocks(M);
+  auto go = [&](auto kern, size_t lds) {
+    set_lds(kern, lds);
+    hipLaunchKernelGGL(kern, dim3(P), dim3(MLP_THREADS), lds, s, (const bf16_t*)noise, (const bf16_t*)dfake, g, gslab,
+                       lnslab, M);
+  };
+  if (F == 32) go(mlp_gen_bwd_w_kernel<32, 100>, gbw_lds<32, 100>());
+  else if (F == 36) go(mlp_gen_bwd_w_kernel<36, 100>, gbw_lds<36, 100>());
+  else throw std::runtime_error("mlp_gen_bwd_w: F in {32, 36}");
 }
 
 // ---- GP critic update with in-kernel weight gradients (bf16) ----

