@@ -308,11 +308,21 @@ __device__ __forceinline__ void lrelu_ln(f32x16* a, const float* gam, const floa
 // Sum over the 32 rows of one lane half of every feature of tile v (transpose-reduce butterfly: 16
 // shuffles instead of 80).  Lane l ends with the column sum of register q(l) = 8 b4 + 4 b3 + 2 b2 + b1
 // (bk = bit k of l), i.e. feature featq(q(l), h); lanes l and l ^ 1 hold the same value.
+// The element reads go through an empty asm: otherwise InstCombine folds select(b, v[8 + i], v[i]) into
+// a DYNAMIC extractelement v[b ? 8 + i : i], which the backend lowers as a 16-way v_cmp / v_cndmask
+// chain per element (16 live lane masks, spilled to VGPR lanes: 100 VALU per MFMA in mlp_gen_bwd_w).
+__device__ __forceinline__ float opaque(float x) {
+  asm("" : "+v"(x));
+  return x;
+}
 __device__ __forceinline__ float colsum(const f32x16& v, int lane) {
   float a8[8], a4[4], a2[2];
   bool b = lane & 16;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) a8[i] = (b ? v[8 + i] : v[i]) + __shfl_xor(b ? v[i] : v[8 + i], 16, 64);
+  for (int i = 0; i < 8; ++i) {
+    const float lo = opaque(v[i]), hi = opaque(v[8 + i]);
+    a8[i] = (b ? hi : lo) + __shfl_xor(b ? lo : hi, 16, 64);
+  }
   b = lane & 8;
 #pragma unroll
   for (int i = 0; i < 4; ++i) a4[i] = (b ? a8[4 + i] : a8[i]) + __shfl_xor(b ? a8[i] : a8[4 + i], 8, 64);
@@ -556,19 +566,40 @@ __device__ __forceinline__ float dpp_xor1(float v) {
   // quad_perm [1, 0, 3, 2]: the value of lane ^ 1
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
 }
-// this lane's row rr (block-local, 0..127) of accumulator tiles a -> img[f][rr] for f < N; even lanes
-// write the (rr, rr + 1) pair as one dword
+// this lane's row rr (block-local, 0..127) of accumulator tiles a -> img[f][rr] for f < N.  The
+// (even, odd) row pair of a feature is one dword: both lanes of the pair write it (same address, same
+// value; the odd lane's halves are rotated into place by one v_alignbit), so there is no per-store
+// exec mask.  Feature validity is compile-time except the last tile's features fb .. fb + 3 < N <=
+// fb + 7, which only lane half 0 holds (one masked group).
 template <int N>
 __device__ __forceinline__ void stage_t(unsigned short* img, const f32x16* a, int rr, int h) {
+  constexpr int NT = (N + 31) / 32, REM = N - 32 * (NT - 1);
+  unsigned short* base = img + (rr & ~1) + 4 * h * WQ;
+  const uint32_t rot = (rr & 1) * 16;
+  uint32_t part[4];
+  int pf[4], np = 0;
 #pragma unroll
-  for (int t = 0; t < (N + 31) / 32; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
+      const int fb = 8 * (q >> 2) + (q & 3);  // feature (in the tile) of this register in lane half 0
+      if (t == NT - 1 && fb >= REM) continue;
       const float v = a[t][q];
       const float p = dpp_xor1(v);
-      const int f = 32 * t + featq(q, h);
-      if (f < N && !(rr & 1)) *reinterpret_cast<uint32_t*>(img + f * WQ + rr) = pk2bf(v, p);
+      const uint32_t w0 = pk2bf(v, p);
+      const uint32_t w = __builtin_amdgcn_alignbit(w0, w0, rot);
+      if (t < NT - 1 || fb + 4 < REM) {
+        *reinterpret_cast<uint32_t*>(base + (32 * t + fb) * WQ) = w;
+      } else {
+        pf[np & 3] = fb;  // at most 4 such features (REM - 4 .. REM - 1)
+        part[np++ & 3] = w;
+      }
     }
+  if (np && h == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < np) *reinterpret_cast<uint32_t*>(base + (32 * (NT - 1) + pf[q]) * WQ) = part[q];
+  }
 }
 // a per-t table row (bf16, 128 features) from accumulator tiles; zeros past N come from a
 template <int N>
