@@ -682,11 +682,20 @@ void launch_interpolate(int dt, const void* real, const void* fake, const float*
 }
 
 // ------------------------------------------------------------------ Philox RNG
+// four consecutive values as one 16-byte (fp32) / 8-byte (bf16) store; same RNE conversion as st_f
+__device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ void st4(bf16_t* p, float a, float b, float c, float d) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pk2bf(a, b), pk2bf(c, d));
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) philox_fill_kernel(T* __restrict__ out, int64_t n, uint64_t seed,
                                                           const int64_t* __restrict__ ctr, int dist) {
   const uint64_t base = (uint64_t)ctr[0];
   const int64_t nq = (n + 3) / 4;
+  const bool vec = (reinterpret_cast<uintptr_t>(out) & (4 * sizeof(T) - 1)) == 0;
   for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
     const uint4 r = Philox::gen(seed, base + (uint64_t)q, 0x5EEDu);
     float v[4];
@@ -700,10 +709,14 @@ __global__ void __launch_bounds__(256) philox_fill_kernel(T* __restrict__ out, i
     } else {
       v[0] = u0; v[1] = u1; v[2] = u2; v[3] = u3;
     }
+    if (vec && q * 4 + 3 < n) {
+      st4(out + q * 4, v[0], v[1], v[2], v[3]);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t i = q * 4 + k;
-      if (i < n) st_f(out + i, v[k]);
+      for (int k = 0; k < 4; ++k) {
+        const int64_t i = q * 4 + k;
+        if (i < n) st_f(out + i, v[k]);
+      }
     }
   }
 }
@@ -722,24 +735,42 @@ void launch_philox_fill(int dt, void* out, int64_t n, uint64_t seed, int64_t* ct
 }
 
 // ------------------------------------------------------------------ batch sampling: out[b] = data[randint(N)]
+// One wave per window (grid-stride; a window is D = T * F values, 768 at the bench shape), 16-byte
+// loads and 16- / 8-byte stores when D % 4 == 0 and both buffers are aligned.  The window index of
+// sample b is Philox(seed, ctr + b) as before, so the draws do not depend on the launch shape.
 template <typename T>
 __global__ void __launch_bounds__(256) sample_windows_kernel(const float* __restrict__ data, int64_t N, int64_t D,
-                                                             T* __restrict__ out, uint64_t seed,
+                                                             T* __restrict__ out, int64_t B, uint64_t seed,
                                                              const int64_t* __restrict__ ctr) {
-  const int b = blockIdx.x;
-  const uint4 r = Philox::gen(seed, (uint64_t)ctr[0] + (uint64_t)b, 0xB47Cu);
-  const uint64_t idx = (((uint64_t)r.x << 32) | r.y) % (uint64_t)N;
-  const float* src = data + (int64_t)idx * D;
-  T* dst = out + (int64_t)b * D;
-  for (int64_t j = threadIdx.x; j < D; j += 256) st_f(dst + j, src[j]);
+  const int lane = threadIdx.x & 63;
+  const uint64_t c0 = (uint64_t)ctr[0];
+  const bool vec = (D & 3) == 0 && (reinterpret_cast<uintptr_t>(data) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(out) & (4 * sizeof(T) - 1)) == 0;
+  for (int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b < B; b += (int64_t)gridDim.x * 4) {
+    const uint4 r = Philox::gen(seed, c0 + (uint64_t)b, 0xB47Cu);
+    const uint64_t idx = (((uint64_t)r.x << 32) | r.y) % (uint64_t)N;
+    const float* src = data + (int64_t)idx * D;
+    T* dst = out + b * D;
+    if (vec) {
+      for (int64_t j = 4 * lane; j < D; j += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(src + j);
+        st4(dst + j, v.x, v.y, v.z, v.w);
+      }
+    } else {
+      for (int64_t j = lane; j < D; j += 64) st_f(dst + j, src[j]);
+    }
+  }
 }
 
 void launch_sample_windows(int dt, const float* data, int64_t N, int64_t D, void* out, int B, uint64_t seed,
                            int64_t* ctr, hipStream_t s) {
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)B + 3) / 4, 8192));
   if (dt == DT_BF16)
-    hipLaunchKernelGGL(sample_windows_kernel<bf16_t>, dim3(B), dim3(256), 0, s, data, N, D, (bf16_t*)out, seed, ctr);
+    hipLaunchKernelGGL(sample_windows_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, data, N, D, (bf16_t*)out, (int64_t)B,
+                       seed, ctr);
   else
-    hipLaunchKernelGGL(sample_windows_kernel<float>, dim3(B), dim3(256), 0, s, data, N, D, (float*)out, seed, ctr);
+    hipLaunchKernelGGL(sample_windows_kernel<float>, dim3(grid), dim3(256), 0, s, data, N, D, (float*)out, (int64_t)B,
+                       seed, ctr);
   hipLaunchKernelGGL(ctr_advance_kernel, dim3(1), dim3(64), 0, s, ctr, (int64_t)B);
 }
 

@@ -64,8 +64,8 @@ void launch_mlp_slab_sum4(const float* slab, int P, int L, float* o0, float* o1,
 // out[j] += sum_p slab[p * stride + col0 + j], j < L (fixed order)
 void launch_mlp_slab_sum_cols(const float* slab, int P, int64_t stride, int col0, int L, float* out, hipStream_t s);
 
-// The GP critic update with its three weight gradients accumulated in the kernel (bf16 only; T <= 64
-// and the LDS plan must fit: mlp_wgpw_supported).  Launches mlp_wgpw_blocks(M) workgroups; gslab
+// The GP critic update with its three weight gradients accumulated in the kernel (bf16 only; the LDS
+// plan must fit: T <= 34 at F = 32, T <= 18 at F = 36, mlp_wgpw_supported).  Launches mlp_wgpw_blocks(M) workgroups; gslab
 // (blocks x (H + F + T) H fp32) gets each workgroup's partial [gW2 | gW1 | gw3], slab (4 blocks x 2)
 // the per-wave W-loss partials of mlp_wgp_critic.  Every slab element is written.
 // The generator reverse with its parameter gradients accumulated in the kernel (bf16, F in {32, 36}):

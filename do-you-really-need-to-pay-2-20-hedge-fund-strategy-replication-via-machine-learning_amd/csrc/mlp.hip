@@ -558,7 +558,8 @@ template <int F, int H> constexpr size_t wgpw_off_img3() { return wgpw_off_img2<
 template <int F, int H> constexpr size_t wgpw_off_img1() { return wgpw_off_img3<F, H>() + (size_t)H * WQ * 2; }
 template <int F, int H> constexpr size_t wgpw_off_toff() { return wgpw_off_img1<F, H>() + (size_t)F * WQ * 2; }
 template <int F, int H> constexpr size_t wgpw_off_tab() { return wgpw_off_toff<F, H>() + 128 * 4; }
-template <int F, int H> constexpr size_t wgpw_lds(int Tn) { return wgpw_off_tab<F, H>() + 2 * (size_t)Tn * 128 * 2; }
+// tables: w3_t fp32 [Tn][128] (head_rows / rowdot / the gW2 gathers), then dh1'_t bf16 [Tn][128]
+template <int F, int H> constexpr size_t wgpw_lds(int Tn) { return wgpw_off_tab<F, H>() + (size_t)Tn * 128 * (4 + 2); }
 static_assert(wgpw_off_img3<36, 100>() % 16 == 0 && wgpw_off_toff<36, 100>() % 16 == 0, "16-byte aligned images");
 static_assert(wgpw_off_img3<32, 100>() % 16 == 0 && wgpw_off_toff<32, 100>() % 16 == 0, "16-byte aligned images");
 
@@ -621,6 +622,39 @@ __device__ __forceinline__ bf16x8 gather8(const unsigned short* tab, const int* 
   for (int e = 0; e < 4; ++e) u[e] = (uint32_t)tab[ofs[2 * e] + col] | ((uint32_t)tab[ofs[2 * e + 1] + col] << 16);
   return __builtin_bit_cast(bf16x8, u);
 }
+__device__ __forceinline__ bf16x8 gather8(const float* tab, const int* ofs, int col) {
+  u32x4_t u;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) u[e] = pk2bf(tab[ofs[2 * e] + col], tab[ofs[2 * e + 1] + col]);
+  return __builtin_bit_cast(bf16x8, u);
+}
+// raw bf16 rows (4 features per (tile, g) as one uint2), loaded ahead of their use
+template <int K> struct RawRows {
+  uint2 v[(K + 31) / 32 * 4];
+};
+template <int K>
+__device__ __forceinline__ void load_raw(RawRows<K>& r, const bf16_t* __restrict__ x, int64_t row, int64_t M, int h) {
+#pragma unroll
+  for (int t = 0; t < (K + 31) / 32; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * t + 8 * g + 4 * h;
+      r.v[4 * t + g] = (row < M && f0 < K) ? *reinterpret_cast<const uint2*>(x + row * K + f0) : make_uint2(0u, 0u);
+    }
+}
+template <int K>
+__device__ __forceinline__ void raw_to_acc(f32x16* a, const RawRows<K>& r) {
+#pragma unroll
+  for (int t = 0; t < (K + 31) / 32; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const uint2 v = r.v[4 * t + g];
+      a[t][4 * g] = __uint_as_float(v.x << 16);
+      a[t][4 * g + 1] = __uint_as_float(v.x & 0xffff0000u);
+      a[t][4 * g + 2] = __uint_as_float(v.y << 16);
+      a[t][4 * g + 3] = __uint_as_float(v.y & 0xffff0000u);
+    }
+}
 
 template <int F, int H, int NTT>
 __global__ void __launch_bounds__(MLP_THREADS) mlp_wgp_critic_w_kernel(
@@ -639,28 +673,29 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_wgp_critic_w_kernel(
   unsigned short* img3 = reinterpret_cast<unsigned short*>(lds + wgpw_off_img3<F, H>());
   unsigned short* img1 = reinterpret_cast<unsigned short*>(lds + wgpw_off_img1<F, H>());
   int* toff = reinterpret_cast<int*>(lds + wgpw_off_toff<F, H>());
-  unsigned short* tabw = reinterpret_cast<unsigned short*>(lds + wgpw_off_tab<F, H>());
-  unsigned short* tabd = tabw + Tn * 128;
+  float* tabw = reinterpret_cast<float*>(lds + wgpw_off_tab<F, H>());
+  unsigned short* tabd = reinterpret_cast<unsigned short*>(tabw + Tn * 128);
   build_fwd<T, F, H>(f1, c.W1);
   build_fwd<T, H, H>(f2, c.W2);
   build_dgrad<T, H, H>(d2, c.W2);
   build_dgrad<T, F, H>(d1, c.W1);
   load_vec(vec, c.b1, H);
   load_vec(vec + VEC, c.b2, H);
+  for (int e = threadIdx.x; e < Tn * 128; e += blockDim.x) {  // w3_t, fp32, 128 wide (zeros past H)
+    const int t = e >> 7, o = e & 127;
+    tabw[e] = o < H ? c.w3[t * H + o] : 0.f;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63, h = lane >> 5, w = threadIdx.x >> 6, cl = lane & 31;
-  // per-t tables: wave w < NTT computes t = 32 w + lane (the chain's own head_rows / dense, so the table
+  // dh1' table: wave w < NTT computes t = 32 w + lane (the chain's own head_rows / dense, so the table
   // holds exactly the bf16 values the operand path stored per row)
   if (w < NTT) {
     const int t = 32 * w + cl;
     const bool ok = t < Tn;
     f32x16 A[NTH], Bv[NTH];
-    head_rows<H>(A, c.w3 + (int64_t)(ok ? t : 0) * H, 1.f, ok, h);
+    head_rows<H>(A, tabw + (ok ? t : 0) * 128, 1.f, ok, h);
     dense<T, H, H>(A, Bv, d2, lane);
-    if (ok) {
-      table_put<H>(tabw + t * 128, A, h);
-      table_put<H>(tabd + t * 128, Bv, h);
-    }
+    if (ok) table_put<H>(tabd + t * 128, Bv, h);
   }
   f32x16 gW2[NTH], gW1[NTF], gw3[NTT];
 #pragma unroll
@@ -677,7 +712,10 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_wgp_critic_w_kernel(
     const bool ok = row < M;
     const int64_t bidx = ok ? row / Tn : 0;
     const int tr = ok ? (int)(row - bidx * Tn) : 0;
-    const float* w3t = c.w3 + (int64_t)tr * H;
+    const float* w3t = tabw + tr * 128;
+    RawRows<F> xr, xf;  // this tile's windows, loaded first: the head chain below hides their latency
+    load_raw<F>(xr, real, row, M, h);
+    load_raw<F>(xf, fake, row, M, h);
     f32x16 A[NTH], Bv[NTH], X2[NTH], X1[NTF], x[NTF];
     head_rows<H>(A, w3t, 1.f, ok, h);
     dense<T, H, H>(A, Bv, d2, lane);            // dh1' = W2 w3_t
@@ -689,7 +727,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_wgp_critic_w_kernel(
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
       const float sg = pass ? invB : -invB;
-      load_rows<T, F>(x, pass ? fake : real, row, M, h);
+      raw_to_acc<F>(x, pass ? xf : xr);
       axpy<F>(X1, sg, x);
       dense<T, F, H>(x, A, f1, lane);
       bias_act<H>(A, vec, ACT_LINEAR, h);       // h1

@@ -254,6 +254,31 @@ def test_rng_and_sampling(cuda):
     assert torch.equal(a.normal((1000,)), b.normal((1000,)))
 
 
+def test_rng_and_sampling_vector_paths(cuda):
+    """The 16-byte paths of the sampler (one wave per window, D % 4 == 0: the bench's 24 x 32 windows)
+    and of the Philox fill: bf16 draws are the RNE rounding of the fp32 draws of the same stream (odd
+    length: vector body + scalar tail), and sample b's window depends only on (seed, counter + b), not
+    on the launch shape."""
+    from hfrep.utils.rng import DeviceRNG
+
+    for dt in (torch.float32, torch.bfloat16):
+        zf = DeviceRNG(5, cuda).normal((1001,))
+        zb = DeviceRNG(5, cuda).normal((1001,), dtype=dt)
+        assert zb.dtype == dt and torch.equal(zb, zf.to(dt))
+        uf, ub = DeviceRNG(6, cuda).uniform((333,)), DeviceRNG(6, cuda).uniform((333,), dtype=dt)
+        assert torch.equal(ub, uf.to(dt))
+    data = torch.randn(300, 24, 32, device=cuda)
+    for dt in (torch.float32, torch.bfloat16):
+        a, b = DeviceRNG(9, cuda), DeviceRNG(9, cuda)
+        sa = a.sample_windows(data, 100, out_dtype=dt)
+        sb = b.sample_windows(data, 5000, out_dtype=dt)
+        assert sa.dtype == dt and torch.equal(sa, sb[:100])
+        # recover each sample's window index from its first two values, then compare whole windows
+        ref = data.to(dt).float().reshape(300, -1)[:, :2]
+        idx = (sb.float().reshape(5000, 1, -1)[:, :, :2] - ref[None]).abs().sum(-1).argmin(-1)
+        assert torch.equal(sb, data.to(dt)[idx])
+
+
 def test_optimizers_match_cpu(cuda):
     from hfrep.train.optim import KerasOptimizer
 
