@@ -16,6 +16,24 @@ static inline int ew_grid(int64_t n) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, 4096));
 }
 
+// four consecutive values as one 16-byte (fp32) / 8-byte (bf16) store; same RNE conversion as st_f
+__device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ void st4(bf16_t* p, float a, float b, float c, float d) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pk2bf(a, b), pk2bf(c, d));
+}
+__device__ __forceinline__ void ld4(const float* p, float (&x)[4]) {
+  const float4 q = *reinterpret_cast<const float4*>(p);
+  x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+}
+__device__ __forceinline__ void ld4(const bf16_t* p, float (&x)[4]) {
+  const uint2 q = *reinterpret_cast<const uint2*>(p);
+  x[0] = __uint_as_float(q.x << 16); x[1] = __uint_as_float(q.x & 0xffff0000u);
+  x[2] = __uint_as_float(q.y << 16); x[3] = __uint_as_float(q.y & 0xffff0000u);
+}
+
+
 // ------------------------------------------------------------------ activations
 template <typename T>
 __global__ void __launch_bounds__(256) act_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n, int act) {
@@ -531,20 +549,48 @@ void launch_layernorm_tbwd(int dt, const void* dy, const void* dyd, const void* 
 // ------------------------------------------------------------------ gradient penalty coefficient
 // One wave per sample row: the per-row penalty term goes to its own slot and a single-workgroup
 // reduce sums them (a per-row atomicAdd on one address serialised 16k adds: 212 us at B = 16384).
+// one wave per row (grid-stride).  Rows with D % 4 == 0, D <= 1024 and aligned buffers are read once
+// with 8-byte (bf16) / 16-byte (fp32) loads into registers (<= 16 values per lane) and scaled from there;
+// other shapes take the scalar two-pass loop
 template <typename T>
 __global__ void __launch_bounds__(256) gp_coef_kernel(const T* __restrict__ g, T* __restrict__ v,
                                                       float* __restrict__ rowpen, int B, int64_t D, float weight) {
   const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
-  const T* gr = g + (int64_t)b * D;
-  float s = 0.f;
-  for (int64_t j = lane; j < D; j += 64) { const float x = ld_f(gr + j); s += x * x; }
-  const float nrm = sqrtf(wave_sum(s));
-  const float one_m = 1.f - nrm;
-  const float scale = -(2.f * weight / B) * one_m / fmaxf(nrm, 1e-30f);
-  for (int64_t j = lane; j < D; j += 64) st_f(v + (int64_t)b * D + j, ld_f(gr + j) * scale);
-  if (lane == 0) rowpen[b] = one_m * one_m / B;
+  const bool vec = (D & 3) == 0 && D <= 1024 && (reinterpret_cast<uintptr_t>(g) & (4 * sizeof(T) - 1)) == 0 &&
+                   (reinterpret_cast<uintptr_t>(v) & (4 * sizeof(T) - 1)) == 0;
+  for (int b = blockIdx.x * 4 + (threadIdx.x >> 6); b < B; b += gridDim.x * 4) {
+    const T* gr = g + (int64_t)b * D;
+    T* vr = v + (int64_t)b * D;
+    float s = 0.f;
+    if (vec) {
+      float x[4][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t j = 4 * (lane + 64 * c);
+        if (j < D) {
+          ld4(gr + j, x[c]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) s = fmaf(x[c][e], x[c][e], s);
+        }
+      }
+      const float nrm = sqrtf(wave_sum(s));
+      const float one_m = 1.f - nrm;
+      const float scale = -(2.f * weight / B) * one_m / fmaxf(nrm, 1e-30f);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t j = 4 * (lane + 64 * c);
+        if (j < D) st4(vr + j, x[c][0] * scale, x[c][1] * scale, x[c][2] * scale, x[c][3] * scale);
+      }
+      if (lane == 0) rowpen[b] = one_m * one_m / B;
+    } else {
+      for (int64_t j = lane; j < D; j += 64) { const float x = ld_f(gr + j); s += x * x; }
+      const float nrm = sqrtf(wave_sum(s));
+      const float one_m = 1.f - nrm;
+      const float scale = -(2.f * weight / B) * one_m / fmaxf(nrm, 1e-30f);
+      for (int64_t j = lane; j < D; j += 64) st_f(vr + j, ld_f(gr + j) * scale);
+      if (lane == 0) rowpen[b] = one_m * one_m / B;
+    }
+  }
 }
 
 // pen = sum of the row penalties (fixed order: bitwise reproducible); with w (the critic's two W terms)
@@ -552,8 +598,15 @@ __global__ void __launch_bounds__(256) gp_coef_kernel(const T* __restrict__ g, T
 __global__ void __launch_bounds__(1024) gp_sum_kernel(const float* __restrict__ x, int n, float* __restrict__ out,
                                                       const float* __restrict__ w, float weight, float* __restrict__ pack) {
   __shared__ float red[16];
-  float s = 0.f;
-  for (int i = threadIdx.x; i < n; i += 1024) s += x[i];
+  // four independent 16-byte streams per thread (fixed order), then the scalar tail
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  const int n4 = (reinterpret_cast<uintptr_t>(x) & 15) == 0 ? n / 4 : 0;
+  for (int i = threadIdx.x; i < n4; i += 1024) {
+    const float4 q = reinterpret_cast<const float4*>(x)[i];
+    a0 += q.x; a1 += q.y; a2 += q.z; a3 += q.w;
+  }
+  for (int i = 4 * n4 + threadIdx.x; i < n; i += 1024) a0 += x[i];
+  float s = (a0 + a1) + (a2 + a3);
   s = block_sum<16>(s, red);
   if (threadIdx.x == 0) {
     out[0] = s;
@@ -585,7 +638,7 @@ void launch_gp_pack(const float* pen, const float* w, float weight, float* pack,
 
 void launch_gp_coef(int dt, const void* g, void* v, float* pen, float* rowpen, int B, int64_t D, float weight,
                     hipStream_t s, const float* w, float* pack) {
-  const int grid = (B + 3) / 4;
+  const int grid = std::max(1, std::min((B + 3) / 4, 8192));
   if (dt == DT_BF16)
     hipLaunchKernelGGL(gp_coef_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)g, (bf16_t*)v, rowpen, B, D,
                        weight);
@@ -682,13 +735,6 @@ void launch_interpolate(int dt, const void* real, const void* fake, const float*
 }
 
 // ------------------------------------------------------------------ Philox RNG
-// four consecutive values as one 16-byte (fp32) / 8-byte (bf16) store; same RNE conversion as st_f
-__device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
-  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
-}
-__device__ __forceinline__ void st4(bf16_t* p, float a, float b, float c, float d) {
-  *reinterpret_cast<uint2*>(p) = make_uint2(pk2bf(a, b), pk2bf(c, d));
-}
 
 template <typename T>
 __global__ void __launch_bounds__(256) philox_fill_kernel(T* __restrict__ out, int64_t n, uint64_t seed,

@@ -510,8 +510,10 @@ def test_skinny_dense_ops(cuda, dt, M, K, N):
     assert (gb.cpu().double() - rb).abs().max().item() < tol * max(1.0, d.double().abs().sum(0).max().item())
 
 
-@pytest.mark.parametrize("B,D", [(7, 768), (16384, 768), (33, 100)])
+@pytest.mark.parametrize("B,D", [(7, 768), (16384, 768), (33, 100), (40000, 768), (5, 1680), (9, 102)])
 def test_gp_coef_many_rows(cuda, B, D):
+    """Vector path (D % 4 == 0, D <= 1024; B = 40 000 takes several grid-stride rounds) and the scalar
+    two-pass path (D = 1680: the T = 48, F = 35 preset; D = 102) against fp64."""
     from hfrep.ops import functional as Fn
 
     g = torch.Generator().manual_seed(41)
