@@ -125,7 +125,14 @@ class Dense(Layer):
     def forward(self, x):
         return R.dense(x, self.w("kernel"), self.w("bias") if self.use_bias else None, self.act)
 
-    def efwd(self, x, save, out=None):
+    def efwd(self, x, save, out=None, compute=True):
+        """``compute=False`` (linear head whose value the caller never reads, e.g. D(x_hat) of the
+        gradient penalty: only its input adjoint is used): no kernel runs and ``y`` is an uninitialised
+        placeholder of the output's shape -- the linear backward / tangent passes never read it."""
+        if not compute:
+            assert self.act_code == 0, "only a linear Dense output can be left uncomputed"
+            y = torch.empty(tuple(x.shape[:-1]) + (self.units,), dtype=x.dtype, device=x.device)
+            return y, ({"x": x, "y": y} if save else None)
         y = Fn.linear(x, self.p("kernel"), self.p("bias") if self.use_bias else None, self.act_code, out=out)
         return y, ({"x": x, "y": y} if save else None)
 
@@ -142,7 +149,11 @@ class Dense(Layer):
             Fn.run_wgrad(Fn.linear_wgrad_, ctx["x"], dz, self.g("kernel"), self.g("bias") if self.use_bias else None)
         return self._dgrad(dz) if need_dx else None
 
-    def etfwd(self, ctx, xd):
+    def etfwd(self, ctx, xd, compute=True):
+        if not compute:  # linear head, tangent value unused (see efwd): shape-only placeholder
+            assert self.act_code == 0, "only a linear Dense output can be left uncomputed"
+            zd = torch.empty(tuple(xd.shape[:-1]) + (self.units,), dtype=xd.dtype, device=xd.device)
+            return zd, {"xd": xd, "zd": zd}
         zd = Fn.linear(xd, self.p("kernel"), None, 0)
         yd = Fn.act_backward(zd, ctx["y"], self.act_code)  # act'(z) * zdot
         return yd, {"xd": xd, "zd": zd}
@@ -486,9 +497,16 @@ class Sequential(torch.nn.Module):
         return x
 
     # ---- explicit engine -----------------------------------------------------------------
-    def efwd(self, x, save: bool = True, out=None):
+    def _head_skippable(self) -> bool:
+        last = self.layers[-1] if self.layers else None
+        return isinstance(last, Dense) and last.act_code == 0
+
+    def efwd(self, x, save: bool = True, out=None, head_out: bool = True):
         """``out``: destination of the model output, used when the last layer can write into it
-        (Dense); otherwise the output is copied there."""
+        (Dense); otherwise the output is copied there.  ``head_out=False``: the caller only needs the
+        tape (e.g. the gradient penalty's forward on x_hat, whose score nothing reads): a linear Dense
+        head is not evaluated and the returned output is a shape-only placeholder."""
+        skip_head = not head_out and self._head_skippable()
         tape = []
         i, n = 0, len(self.layers)
         while i < n:
@@ -504,7 +522,9 @@ class Sequential(torch.nn.Module):
                 x = y
                 i += 2
                 continue
-            if out is not None and i == n - 1 and isinstance(l, Dense):
+            if skip_head and i == n - 1:
+                x, ctx = l.efwd(x, save, compute=False)
+            elif out is not None and i == n - 1 and isinstance(l, Dense):
                 x, ctx = l.efwd(x, save, out=out)
             else:
                 x, ctx = l.efwd(x, save)
@@ -534,10 +554,17 @@ class Sequential(torch.nn.Module):
                 hook(i)
         return Fn._mat(dy)
 
-    def etfwd(self, tape, xd):
+    def etfwd(self, tape, xd, head_out: bool = True):
+        """``head_out=False``: the tangent of a linear Dense head is not evaluated (placeholder), as in
+        ``efwd``."""
+        skip_head = not head_out and self._head_skippable()
         ttape = []
-        for l, ctx in zip(self.layers, tape):
-            xd, tctx = l.etfwd(ctx, xd)
+        n = len(self.layers)
+        for i, (l, ctx) in enumerate(zip(self.layers, tape)):
+            if skip_head and i == n - 1:
+                xd, tctx = l.etfwd(ctx, xd, compute=False)
+            else:
+                xd, tctx = l.etfwd(ctx, xd)
             ttape.append(tctx)
         return xd, ttape
 

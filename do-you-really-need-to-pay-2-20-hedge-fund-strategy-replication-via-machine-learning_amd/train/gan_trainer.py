@@ -282,10 +282,10 @@ class GANTrainer:
             cur = torch.cuda.current_stream(self.device)
             side.wait_stream(cur)
             with torch.cuda.stream(side), trange("critic/gp_input_grad"):
-                sh, tape_h = C.efwd(xh, save=True)
+                sh, tape_h = C.efwd(xh, save=True, head_out=False)  # D(x_hat) itself is never read
                 g = C.ebwd(tape_h, self._ones(sh), need_dx=True, wgrad=False)
                 pen, v = Fn.gp_coef(g, self.gp_weight)
-                sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
+                sd, ttape = C.etfwd(tape_h, v.to(xh.dtype), head_out=False)
         hook = self._hook(C)
         # (concurrent, no per-layer all-reduce hook: every layer's weight gradient runs on side stream
         # 2 beside the next layer's backward, in the sequential order; joined before the return)
@@ -302,11 +302,11 @@ class GANTrainer:
             # theta-gradient of <v, g> as reverse-over-tangent
             if side is None:
                 with trange("critic/gp_input_grad"):
-                    sh, tape_h = C.efwd(xh, save=True)
+                    sh, tape_h = C.efwd(xh, save=True, head_out=False)  # D(x_hat) itself is never read
                     g = C.ebwd(tape_h, self._ones(sh), need_dx=True, wgrad=False)
                     pack, v = Fn.gp_coef_pack(g, self.gp_weight, w)  # [total, W real, W fake, GP]
                 with trange("critic/gp_second_order"):
-                    sd, ttape = C.etfwd(tape_h, v.to(xh.dtype))
+                    sd, ttape = C.etfwd(tape_h, v.to(xh.dtype), head_out=False)
             else:
                 pack = Fn.gp_pack(pen, self.gp_weight, w)
             with trange("critic/gp_second_order"):

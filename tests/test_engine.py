@@ -170,3 +170,33 @@ def test_generator_forward_reuse_is_exact(loss):
             tr.train_step()
         runs.append(torch.cat([tr.generator.flat.detach(), tr.critic.flat.detach(), tr._g_acc.reshape(-1)]))
     assert torch.equal(runs[0], runs[1])
+
+
+def test_head_out_false_skips_only_dead_work():
+    """The gradient penalty's forward on x_hat and its tangent forward never read the linear head's
+    value: with head_out=False the head is not evaluated (shape-only placeholder) and the input
+    gradient and the reverse-over-tangent parameter gradient are bitwise the same."""
+    import numpy as np
+
+    from hfrep.train.gan_trainer import GANConfig, GANTrainer
+
+    ds = np.random.RandomState(3).rand(20, 8, 4).astype(np.float32)
+    tr = GANTrainer(GANConfig(arch="lstm", loss="wgan_gp", window=8, features=4, batch_size=6, hidden=8), ds)
+    C = tr.critic
+    x = torch.randn(6, 8, 4, generator=torch.Generator().manual_seed(1))
+    s1, t1 = C.efwd(x, save=True)
+    s2, t2 = C.efwd(x, save=True, head_out=False)
+    assert s2.shape == s1.shape and s2.dtype == s1.dtype
+    g1 = C.ebwd(t1, torch.ones_like(s1), need_dx=True, wgrad=False)
+    g2 = C.ebwd(t2, torch.ones_like(s2), need_dx=True, wgrad=False)
+    assert torch.equal(g1, g2)
+    v = torch.randn_like(x)
+    sd1, tt1 = C.etfwd(t1, v)
+    sd2, tt2 = C.etfwd(t2, v, head_out=False)
+    assert sd2.shape == sd1.shape
+    C.zero_grad()
+    C.etbwd(t1, tt1, None, torch.ones_like(sd1))
+    ga = C.flat.grad.clone()
+    C.zero_grad()
+    C.etbwd(t2, tt2, None, torch.ones_like(sd2))
+    assert torch.equal(ga, C.flat.grad)
