@@ -324,35 +324,68 @@ std::tuple<Tensor, Tensor> lstmf_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape
   return {hds, ttape};
 }
 
-Tensor lstmf_bwd(optional<Tensor> dH, Tensor tape, Tensor U, int64_t act, int64_t B, int64_t Tn) {
+// the critic head's outer-product adjoint (d (B) x w (Tn H)) as kernel operands: fp32, on the tape's device
+static void check_head(const optional<Tensor>& d, const optional<Tensor>& w, const Tensor& like, int64_t B, int64_t n) {
+  if (d.has_value()) {
+    CHECK_F32(*d);
+    TORCH_CHECK(d->numel() == B && d->device() == like.device(), "head adjoint factor: B fp32 values");
+  }
+  if (w.has_value()) {
+    CHECK_F32(*w);
+    TORCH_CHECK(w->numel() == n && w->device() == like.device(), "head weight: Tn H fp32 values");
+  }
+}
+
+Tensor lstmf_bwd(optional<Tensor> dH, Tensor tape, Tensor U, int64_t act, int64_t B, int64_t Tn, optional<Tensor> hd,
+                 optional<Tensor> hw) {
   CHECK_F32(tape);
   const int H = U.size(0);
   check_lstm_U(U, H);
   TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstmf_tape_elems(B, Tn), "lstmf_bwd: tape size");
   if (dH.has_value()) { CHECK_F32(*dH); TORCH_CHECK(dH->numel() == B * Tn * H, "lstmf_bwd: dH shape"); }
+  TORCH_CHECK(hd.has_value() == hw.has_value() && !(hd.has_value() && dH.has_value()),
+              "lstmf_bwd: dH or the head factors (hd, hw)");
+  check_head(hd, hw, tape, B, Tn * H);
   GUARD(tape);
   Tensor dZ = out_empty({B, Tn, 4 * H}, tape.options());
-  const bool ok = hfrep::launch_lstmf_bwd(dH.has_value() ? dH->data_ptr<float>() : nullptr, tape.data_ptr<float>(),
-                                          U.data_ptr<float>(), dZ.data_ptr<float>(), B, Tn, H, (int)act,
-                                          cur_stream(tape));
+  Tensor dHm;
+  if (hd.has_value() && !hfrep::lstmf_head_supported()) {  // exact-fp32 BPTT: materialise hd (x) hw
+    dHm = out_empty({B, Tn * H}, tape.options());
+    // (M rows, K = Tn H input features, N = 1 head column): linear_dgrad's skinny call for this head
+    hfrep::launch_skinny_dgrad(hfrep::DT_F32, hd->data_ptr<float>(), hw->data_ptr<float>(), dHm.data_ptr(), B,
+                               (int)(Tn * H), 1, cur_stream(tape));
+  }
+  const bool head = hd.has_value() && !dHm.defined();
+  const float* dhp = dHm.defined() ? dHm.data_ptr<float>() : dH.has_value() ? dH->data_ptr<float>() : nullptr;
+  const bool ok = hfrep::launch_lstmf_bwd(dhp, tape.data_ptr<float>(), U.data_ptr<float>(), dZ.data_ptr<float>(), B, Tn,
+                                          H, (int)act, cur_stream(tape), head ? hd->data_ptr<float>() : nullptr,
+                                          head ? hw->data_ptr<float>() : nullptr);
   TORCH_CHECK(ok, "lstmf_bwd: unsupported H / act");
   return dZ;
 }
 
 std::tuple<Tensor, Tensor> lstmf_tbwd(optional<Tensor> dH, optional<Tensor> dHd, Tensor tape, Tensor ttape, Tensor U,
-                                      int64_t act, int64_t B, int64_t Tn) {
+                                      int64_t act, int64_t B, int64_t Tn, optional<Tensor> hd, optional<Tensor> hdd,
+                                      optional<Tensor> hw) {
   CHECK_F32(tape); CHECK_F32(ttape);
   const int H = U.size(0);
   check_lstm_U(U, H);
   TORCH_CHECK(tape.numel() == (int64_t)hfrep::lstmf_tape_elems(B, Tn) && ttape.numel() == tape.numel(), "tape size");
   for (const auto* d : {&dH, &dHd})
     if (d->has_value()) { CHECK_F32(**d); TORCH_CHECK((*d)->numel() == B * Tn * H, "lstmf_tbwd: adjoint shape"); }
+  const bool head = hw.has_value();
+  TORCH_CHECK(!head || (!dH.has_value() && !dHd.has_value()), "lstmf_tbwd: adjoints (dH, dHd) or head factors, not both");
+  check_head(hd, hw, tape, B, Tn * H);
+  check_head(hdd, {}, tape, B, Tn * H);
   GUARD(tape);
   Tensor dZ = out_empty({B, Tn, 4 * H}, tape.options()), dZd = out_empty({B, Tn, 4 * H}, tape.options());
   const bool ok = hfrep::launch_lstmf_tbwd(dH.has_value() ? dH->data_ptr<float>() : nullptr,
                                            dHd.has_value() ? dHd->data_ptr<float>() : nullptr, tape.data_ptr<float>(),
                                            ttape.data_ptr<float>(), U.data_ptr<float>(), dZ.data_ptr<float>(),
-                                           dZd.data_ptr<float>(), B, Tn, H, (int)act, cur_stream(tape));
+                                           dZd.data_ptr<float>(), B, Tn, H, (int)act, cur_stream(tape),
+                                           head && hd.has_value() ? hd->data_ptr<float>() : nullptr,
+                                           head && hdd.has_value() ? hdd->data_ptr<float>() : nullptr,
+                                           head ? hw->data_ptr<float>() : nullptr);
   TORCH_CHECK(ok, "lstmf_tbwd: unsupported H / act");
   return {dZ, dZd};
 }
@@ -960,8 +993,9 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("set_lstmf_fwd_impl(int v) -> int", &set_lstmf_fwd_impl);
   m.def("set_lstmf_bwd_impl(int v) -> int", &set_lstmf_bwd_impl);
   m.def("lstmf_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
-  m.def("lstmf_bwd(Tensor? dH, Tensor tape, Tensor U, int act, int B, int T) -> Tensor");
-  m.def("lstmf_tbwd(Tensor? dH, Tensor? dHd, Tensor tape, Tensor ttape, Tensor U, int act, int B, int T) -> (Tensor, Tensor)");
+  m.def("lstmf_bwd(Tensor? dH, Tensor tape, Tensor U, int act, int B, int T, Tensor? hd=None, Tensor? hw=None) -> Tensor");
+  m.def("lstmf_tbwd(Tensor? dH, Tensor? dHd, Tensor tape, Tensor ttape, Tensor U, int act, int B, int T, Tensor? hd=None, "
+        "Tensor? hdd=None, Tensor? hw=None) -> (Tensor, Tensor)");
   m.def("lstmf_tfwd(Tensor xd, Tensor W, Tensor U, Tensor tape, int act) -> (Tensor, Tensor)");
   m.def("lstmf_dgrad(Tensor dz, Tensor W, int impl=0) -> Tensor");
   m.def("lstm2_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");

@@ -48,10 +48,15 @@ bool launch_lstmf_fwd(const float* x, const float* W, const float* b, const floa
 bool launch_lstmf_tfwd(const float* xd, const float* W, const float* U, const float* tape, float* hds, float* ttape,
                        int B, int Tn, int K, int H, int act, hipStream_t s);
 // BPTT / tangent reverse on those tapes (dH / dHd may be null = zeros); dZ / dZd row-major (B,T,4H)
+// hd / hw (HEAD): dH = hd (x) hw generated in the kernel (the critic head's adjoint: hd (B), hw (Tn H));
+// dH is then unused.  Not with the exact-fp32 BPTT (lstmf_head_supported() false: materialise dH).
 bool launch_lstmf_bwd(const float* dH, const float* tape, const float* U, float* dZ, int B, int Tn, int H, int act,
-                      hipStream_t s);
+                      hipStream_t s, const float* hd = nullptr, const float* hw = nullptr);
+bool lstmf_head_supported();
+// hw (HEAD): dH = hd (x) hw, dHd = hdd (x) hw generated in the kernel (a null factor: that adjoint is 0)
 bool launch_lstmf_tbwd(const float* dH, const float* dHd, const float* tape, const float* ttape, const float* U, float* dZ,
-                       float* dZd, int B, int Tn, int H, int act, hipStream_t s);
+                       float* dZd, int B, int Tn, int H, int act, hipStream_t s, const float* hd = nullptr,
+                       const float* hdd = nullptr, const float* hw = nullptr);
 // fused fp32 LSTM weight gradients (K in {32, 36, 100}, H = 100, N = 400): gW += X^T dZ (+ Xd^T dZd),
 // gU += Hprev^T dZ (+ Hdprev^T dZd), gb += colsum dZ, through per-workgroup slabs in ws
 // (lstmf_wgrad_workspace_floats) and one fixed-order reduce

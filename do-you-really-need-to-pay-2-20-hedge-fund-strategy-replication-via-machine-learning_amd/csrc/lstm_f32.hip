@@ -435,11 +435,19 @@ __device__ __forceinline__ void bwdf_tape_load(f32x4& tg, float& tcp, float& tdh
 // the same loads with the per-lane part of each offset in voffset (tl / tcl / vp) and the uniform part
 // (step and slot) in soffset: no per-cell offset arithmetic on the VALU (the split BPTT is VALU-bound,
 // profiles/r03_end/pmc_fp32.txt).  Out-of-range lanes: voffset kOOB (the range check is on voffset)
+// HEAD: dH is the critic head's outer-product adjoint dH[b, t, u] = hdm * w[t, u] (hdm = the lane row's
+// d[b], w = the head weight, (Tn, H) like one row of dH: same soffset, voffset hvo = the unit's
+// offset), generated here instead of read from a materialised (B, Tn, H) tensor
+template <bool HEAD>
 __device__ __forceinline__ void bwdf_tape_load_u(f32x4& tg, float& tcp, float& tdh, rsrc_t rt, rsrc_t rdh, int tl, int tcl,
-                                                 int vp, int sg, int sc, int sd, bool tok, bool prev) {
+                                                 int vp, int sg, int sc, int sd, bool tok, bool prev, float hdm,
+                                                 rsrc_t rhw, int hvo) {
   tg = ld4s(rt, tok ? tl : kOOB, sg);
   tcp = ld1(rt, (tok && prev) ? tcl : kOOB, sc);
-  tdh = ld1(rdh, tok ? vp : kOOB, sd);
+  // (the product may contract into the consumer's add: one rounding fewer than a materialised dH, i.e.
+  // within an ulp of it; an empty-asm barrier against that breaks the step schedule, +40 % per call)
+  if constexpr (HEAD) tdh = hdm * ld1(rhw, tok ? hvo : kOOB, sd);
+  else tdh = ld1(rdh, tok ? vp : kOOB, sd);
 }
 // the dz tile (32 rows x [q][u'], u' < 100) -> dZ[:, t, :] (row-major, 4H per row) in 16-byte chunks:
 // threads 0..199 own chunk (tid % 100) of rows 2 k + tid / 100 (k < 16); the row step lives in the
@@ -658,11 +666,12 @@ lstmf_bwdp_kernel(const float* __restrict__ dH, const float* __restrict__ tape, 
 #ifndef HFREP_TBWD_CELLGROUP
 #define HFREP_TBWD_CELLGROUP 2
 #endif
-template <int ACT>
+template <int ACT, bool HEAD = false>
 __global__ void __launch_bounds__(512, 1)
 lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, const float* __restrict__ tape,
                    const float* __restrict__ ttape, const float* __restrict__ U, float* __restrict__ dZ,
-                   float* __restrict__ dZd, int B, int Tn) {
+                   float* __restrict__ dZd, int B, int Tn, const float* __restrict__ hd, const float* __restrict__ hdd,
+                   const float* __restrict__ hw) {
   extern __shared__ __attribute__((aligned(16))) float fsm[];
   float* zt = fsm;                   // dz tile     [32][BZ_LR]
   float* zdt = zt + 32 * BZ_LR;      // dzdot tile  [32][BZ_LR]
@@ -773,6 +782,18 @@ lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, 
       int vp1[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) vp1[m] = ((16 * m + 4 * g + q) * Tn * FH + ub) * 4;
+      // HEAD: dH = hd (x) w, dHd = hdd (x) w generated per cell (a null factor: that adjoint is zero)
+      float hdv[2] = {0.f, 0.f}, hddv[2] = {0.f, 0.f};
+      const rsrc_t rhw = make_rsrc(hw, HEAD ? Tn * FH * 4 : 0);
+      if constexpr (HEAD) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const int r = row0 + 16 * m + 4 * g + q;
+          hdv[m] = (hd && r < B) ? hd[r] : 0.f;
+          hddv[m] = (hdd && r < B) ? hdd[r] : 0.f;
+        }
+      }
+      const int hvo = ub * 4;
       float tc[2][FNT], tcd[2][FNT], acn[2][FNT], acdn[2][FNT];
       f32x4 tg[FNT], tz[FNT];
       float tcp[FNT], tcdp[FNT], tdh[FNT], tdhd[FNT];
@@ -792,8 +813,14 @@ lstmf_tbwdp_kernel(const float* __restrict__ dH, const float* __restrict__ dHd, 
           tz[n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rtt, tok ? tl : kOOB, sg, 0));
           tcp[n] = ld1(rt, (tok && tt > 0) ? tcl : kOOB, sc);
           tcdp[n] = ld1(rtt, (tok && tt > 0) ? tcl : kOOB, sc);
-          tdh[n] = ld1(rdh, tok ? vp1[m] : kOOB, sd);
-          tdhd[n] = ld1(rdhd, tok ? vp1[m] : kOOB, sd);
+          if constexpr (HEAD) {
+            const float wv = ld1(rhw, tok ? hvo : kOOB, sd);
+            tdh[n] = hdv[m] * wv;
+            tdhd[n] = hddv[m] * wv;
+          } else {
+            tdh[n] = ld1(rdh, tok ? vp1[m] : kOOB, sd);
+            tdhd[n] = ld1(rdhd, tok ? vp1[m] : kOOB, sd);
+          }
         }
       };
 #pragma unroll
@@ -2015,10 +2042,10 @@ lstmf_fwds_kernel(const float* __restrict__ x, const float* __restrict__ W, cons
 constexpr int BS_LZ = 432;             // dz plane row stride (bf16 elements): 216 dwords
 constexpr int BS_PL = 32 * BS_LZ * 2;  // bytes per dz plane (32 rows)
 
-template <int ACT>
+template <int ACT, bool HEAD = false>
 __global__ void __launch_bounds__(256, 1)
 lstmf_bwds_kernel(const float* __restrict__ dH, const float* __restrict__ tape, const float* __restrict__ U,
-                  float* __restrict__ dZ, int B, int Tn) {
+                  float* __restrict__ dZ, int B, int Tn, const float* __restrict__ hd, const float* __restrict__ hw) {
   extern __shared__ __attribute__((aligned(16))) float fsm[];
   float* zt = fsm;                                     // fp32 dz tile [32][BZ_LR]: [q][u'] per row
   float* ht = zt + 32 * BZ_LR;                         // dh_rec tile [32][BH_LR]
@@ -2073,6 +2100,17 @@ lstmf_bwds_kernel(const float* __restrict__ dH, const float* __restrict__ tape, 
     int vp1[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) vp1[m] = ((16 * m + 4 * g + q) * Tn * FH + ub) * 4;
+    // HEAD: the lane rows' head adjoint factors d[row] (0 past B) and the head weight's descriptor
+    float hdv[2] = {0.f, 0.f};
+    const rsrc_t rhw = make_rsrc(hw, HEAD ? Tn * FH * 4 : 0);
+    if constexpr (HEAD) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int r = row0 + 16 * m + 4 * g + q;
+        hdv[m] = r < B ? hd[r] : 0.f;
+      }
+    }
+    const int hvo = ub * 4;
     float dc[2][FNT], tc[2][FNT];
     f32x4 tg[FNT];
     float tcp[FNT], tdh[FNT];
@@ -2085,8 +2123,9 @@ lstmf_bwds_kernel(const float* __restrict__ dH, const float* __restrict__ tape, 
         dc[m][n] = 0.f;
         tc[m][n] = ld1(rt, tok ? tcl + T1 * FT_STEP * 4 + ftape_slot(m, n) : kOOB, 0);  // c_{T-1}
       }
-      bwdf_tape_load_u(tg[n], tcp[n], tdh[n], rt, rdh, tl, tcl, vp1[0], T1 * FT_STEP * 4 + ftape_slot(0, n),
-                       max(T1 - 1, 0) * FT_STEP * 4 + ftape_slot(0, n), T1 * FH * 4 + 16 * n, tok, T1 > 0);
+      bwdf_tape_load_u<HEAD>(tg[n], tcp[n], tdh[n], rt, rdh, tl, tcl, vp1[0], T1 * FT_STEP * 4 + ftape_slot(0, n),
+                             max(T1 - 1, 0) * FT_STEP * 4 + ftape_slot(0, n), T1 * FH * 4 + 16 * n, tok, T1 > 0, hdv[0],
+                             rhw, hvo);
     }
     // dz_T = 0 (planes, pad columns k >= 400 included), dh_rec(T - 1) = 0
     for (int i = tid; i < 3 * BS_PL / 16; i += 256)
@@ -2129,12 +2168,14 @@ lstmf_bwds_kernel(const float* __restrict__ dH, const float* __restrict__ tape, 
         *reinterpret_cast<__attribute__((address_space(3))) u32x2_t*>(pd + pp * ps) = u32x2_t{p[pp][0], p[pp][1]};
       tc[m][n] = tcp[n];  // c_{t-1} is the next step's c
       if constexpr (m == 0) {  // next use: B(1, t)
-        bwdf_tape_load_u(tg[n], tcp[n], tdh[n], rt, rdh, tl, tcl, vp1[1], t * FT_STEP * 4 + ftape_slot(1, n),
-                         max(t - 1, 0) * FT_STEP * 4 + ftape_slot(1, n), t * FH * 4 + 16 * n, tok, t > 0);
+        bwdf_tape_load_u<HEAD>(tg[n], tcp[n], tdh[n], rt, rdh, tl, tcl, vp1[1], t * FT_STEP * 4 + ftape_slot(1, n),
+                               max(t - 1, 0) * FT_STEP * 4 + ftape_slot(1, n), t * FH * 4 + 16 * n, tok, t > 0, hdv[1],
+                               rhw, hvo);
       } else {  // next use: B(0, t - 1)
         const int tp = t > 0 ? t - 1 : 0;
-        bwdf_tape_load_u(tg[n], tcp[n], tdh[n], rt, rdh, tl, tcl, vp1[0], tp * FT_STEP * 4 + ftape_slot(0, n),
-                         max(tp - 1, 0) * FT_STEP * 4 + ftape_slot(0, n), tp * FH * 4 + 16 * n, tok && t > 0, tp > 0);
+        bwdf_tape_load_u<HEAD>(tg[n], tcp[n], tdh[n], rt, rdh, tl, tcl, vp1[0], tp * FT_STEP * 4 + ftape_slot(0, n),
+                               max(tp - 1, 0) * FT_STEP * 4 + ftape_slot(0, n), tp * FH * 4 + 16 * n, tok && t > 0,
+                               tp > 0, hdv[0], rhw, hvo);
       }
     };
     // one half-phase: dz rows of half MA out to HBM, the cells of half 1 - MA at step t, and rows MA of
@@ -2603,50 +2644,62 @@ static std::atomic<int>& bwdf_impl() {
   return v;
 }
 template <int ACT>
-void bwdf_launch(const float* dH, const float* tape, const float* U, float* dZ, int B, int Tn, hipStream_t s) {
+void bwdf_launch(const float* dH, const float* tape, const float* U, float* dZ, int B, int Tn, hipStream_t s,
+                 const float* hd, const float* hw) {
   const int ver = bwdf_impl().load(std::memory_order_relaxed);
   const int nrb = (B + 31) / 32, cus = device_cu_count();
   const size_t sm = (size_t)(32 * BZ_LR + 32 * BH_LR + 4 * BZ_KQ) * 4;
   if (ver != 2) {
-    auto k = lstmf_bwds_kernel<ACT>;
-    allow_lds(reinterpret_cast<const void*>(k));
-    hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(256), sm + 16 + 3 * BS_PL, s, dH, tape, U, dZ, B, Tn);
+    auto go = [&](auto k) {
+      allow_lds(reinterpret_cast<const void*>(k));
+      hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(256), sm + 16 + 3 * BS_PL, s, dH, tape, U, dZ, B, Tn, hd,
+                         hw);
+    };
+    if (hd) go(lstmf_bwds_kernel<ACT, true>);
+    else go(lstmf_bwds_kernel<ACT, false>);
     return;
   }
+  if (hd) throw std::runtime_error("lstmf_bwd: the exact-fp32 BPTT takes a materialised dH (lstmf_head_supported)");
   auto k = lstmf_bwdp_kernel<ACT>;
   allow_lds(reinterpret_cast<const void*>(k));
   hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(512), sm, s, dH, tape, U, dZ, B, Tn);
 }
 static_assert((32 * BZ_LR + 32 * BH_LR + 4 * BZ_KQ) * 4 + 16 + 3 * BS_PL <= F_LDS_MAX, "split BPTT LDS");
 int set_lstmf_bwd_impl(int v) { return bwdf_impl().exchange(v); }
+bool lstmf_head_supported() { return bwdf_impl().load(std::memory_order_relaxed) != 2; }
 bool launch_lstmf_bwd(const float* dH, const float* tape, const float* U, float* dZ, int B, int Tn, int H, int act,
-                      hipStream_t s) {
+                      hipStream_t s, const float* hd, const float* hw) {
   if (H != FH || B <= 0 || Tn <= 0) return false;
   switch (act) {
-    case ACT_LINEAR: bwdf_launch<ACT_LINEAR>(dH, tape, U, dZ, B, Tn, s); return true;
-    case ACT_SIGMOID: bwdf_launch<ACT_SIGMOID>(dH, tape, U, dZ, B, Tn, s); return true;
-    case ACT_TANH: bwdf_launch<ACT_TANH>(dH, tape, U, dZ, B, Tn, s); return true;
+    case ACT_LINEAR: bwdf_launch<ACT_LINEAR>(dH, tape, U, dZ, B, Tn, s, hd, hw); return true;
+    case ACT_SIGMOID: bwdf_launch<ACT_SIGMOID>(dH, tape, U, dZ, B, Tn, s, hd, hw); return true;
+    case ACT_TANH: bwdf_launch<ACT_TANH>(dH, tape, U, dZ, B, Tn, s, hd, hw); return true;
     default: return false;
   }
 }
 
 template <int ACT>
 void tbwdf_launch(const float* dH, const float* dHd, const float* tape, const float* ttape, const float* U, float* dZ,
-                  float* dZd, int B, int Tn, hipStream_t s) {
+                  float* dZd, int B, int Tn, hipStream_t s, const float* hd, const float* hdd, const float* hw) {
   const int cus = device_cu_count();
-  auto k = lstmf_tbwdp_kernel<ACT>;
-  allow_lds(reinterpret_cast<const void*>(k));
   const size_t sm = (size_t)(2 * 32 * BZ_LR + 2 * 32 * BH_LR + 4 * BZ_KQ) * 4;
   const int nrb = (B + 31) / 32;
-  hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(512), sm, s, dH, dHd, tape, ttape, U, dZ, dZd, B, Tn);
+  auto go = [&](auto k) {
+    allow_lds(reinterpret_cast<const void*>(k));
+    hipLaunchKernelGGL(k, dim3(nrb < cus ? nrb : cus), dim3(512), sm, s, dH, dHd, tape, ttape, U, dZ, dZd, B, Tn, hd, hdd,
+                       hw);
+  };
+  if (hw) go(lstmf_tbwdp_kernel<ACT, true>);
+  else go(lstmf_tbwdp_kernel<ACT, false>);
 }
 bool launch_lstmf_tbwd(const float* dH, const float* dHd, const float* tape, const float* ttape, const float* U, float* dZ,
-                       float* dZd, int B, int Tn, int H, int act, hipStream_t s) {
+                       float* dZd, int B, int Tn, int H, int act, hipStream_t s, const float* hd, const float* hdd,
+                       const float* hw) {
   if (H != FH || B <= 0 || Tn <= 0) return false;
   switch (act) {
-    case ACT_LINEAR: tbwdf_launch<ACT_LINEAR>(dH, dHd, tape, ttape, U, dZ, dZd, B, Tn, s); return true;
-    case ACT_SIGMOID: tbwdf_launch<ACT_SIGMOID>(dH, dHd, tape, ttape, U, dZ, dZd, B, Tn, s); return true;
-    case ACT_TANH: tbwdf_launch<ACT_TANH>(dH, dHd, tape, ttape, U, dZ, dZd, B, Tn, s); return true;
+    case ACT_LINEAR: tbwdf_launch<ACT_LINEAR>(dH, dHd, tape, ttape, U, dZ, dZd, B, Tn, s, hd, hdd, hw); return true;
+    case ACT_SIGMOID: tbwdf_launch<ACT_SIGMOID>(dH, dHd, tape, ttape, U, dZ, dZd, B, Tn, s, hd, hdd, hw); return true;
+    case ACT_TANH: tbwdf_launch<ACT_TANH>(dH, dHd, tape, ttape, U, dZ, dZd, B, Tn, s, hd, hdd, hw); return true;
     default: return false;
   }
 }

@@ -357,9 +357,10 @@ def lstm_layer_fwd(x, W, b, U, act: int, save: bool):
 
 class OuterAdjoint:
     """Lazy input adjoint of a linear Dense(1) head: dX[b, j] = d[b, 0] * w[j, 0], viewed with
-    ``shape`` (after Flatten: (B, T, H)).  The bf16 LSTM reverse kernels generate it inside the
-    kernel (csrc/lstm2.hip TileSrc), so the (B, T*H) head adjoint never exists in HBM; every other
-    consumer calls :meth:`materialize` (the skinny dgrad kernel, same rounding)."""
+    ``shape`` (after Flatten: (B, T, H)).  The LSTM reverse kernels generate it inside the kernel (bf16:
+    csrc/lstm2.hip TileSrc; fp32: the HEAD instantiations of lstmf_bwds / lstmf_tbwdp), so the
+    (B, T*H) head adjoint never exists in HBM; every other consumer calls :meth:`materialize` (the
+    skinny dgrad kernel, same rounding)."""
 
     def __init__(self, d: torch.Tensor, w: torch.Tensor, shape=None):
         self.d, self.w = d, w
@@ -374,8 +375,10 @@ class OuterAdjoint:
 
 
 def outer_adjoint_ok(dz: torch.Tensor) -> bool:
-    """Whether a Dense(1) head may hand its input adjoint on lazily (bf16 on the native path)."""
-    return dz.dtype == torch.bfloat16 and _nat(dz) and not _native.fallback_allowed()
+    """Whether a Dense(1) head may hand its input adjoint on lazily (bf16 and fp32 on the native path:
+    the LSTM reverse kernels of both precisions generate it; the exact-fp32 BPTT materialises it in the
+    binding)."""
+    return dz.dtype in (torch.bfloat16, torch.float32) and _nat(dz) and not _native.fallback_allowed()
 
 
 def _mat(a):
@@ -388,8 +391,12 @@ def lstm_layer_bwd(dH, tape, U, act: int, W=None, need_dz: bool = True):
     ``need_dz=False`` (only dX wanted, e.g. the gradient penalty's dD/dx) lets the v2 kernel skip
     writing dZ to HBM; the returned dZ is then None."""
     if isinstance(tape, FTape):
-        dH = _mat(dH)
-        dZ = _ops().lstmf_bwd(None if dH is None else dH.contiguous(), tape.t, U, int(act), tape.B, tape.T)
+        if isinstance(dH, OuterAdjoint) and dH.d.dtype == torch.float32:  # head adjoint generated in-kernel
+            dZ = _ops().lstmf_bwd(None, tape.t, U, int(act), tape.B, tape.T, dH.d.contiguous(),
+                                  dH.w.reshape(-1).contiguous())
+        else:
+            dH = _mat(dH)
+            dZ = _ops().lstmf_bwd(None if dH is None else dH.contiguous(), tape.t, U, int(act), tape.B, tape.T)
         return dZ if W is None else (dZ, linear_dgrad(dZ, W))
     if isinstance(tape, torch.Tensor):
         nd = bool(need_dz or W is None)
@@ -446,9 +453,16 @@ def lstm_wgrad_(x, hs, dZ, gW, gU, gb, xd=None, hds=None, dZd=None, impl: int = 
 def lstm_layer_tbwd(dH, dHd, tape, ttape, U, act: int, W=None):
     """(dZ, dZd) of the reverse-over-tangent pass; with ``W`` also (dX, dXd) = (dZ W^T, dZd W^T)."""
     if isinstance(tape, FTape):
-        dH, dHd = _mat(dH), _mat(dHd)
-        dZ, dZd = _ops().lstmf_tbwd(None if dH is None else dH.contiguous(), None if dHd is None else dHd.contiguous(),
-                                    tape.t, ttape.t, U, int(act), tape.B, tape.T)
+        heads = [a for a in (dH, dHd) if isinstance(a, OuterAdjoint)]
+        if heads and all(a is None or (isinstance(a, OuterAdjoint) and a.w is heads[0].w and a.d.dtype == torch.float32)
+                         for a in (dH, dHd)):  # head adjoints generated in-kernel
+            dZ, dZd = _ops().lstmf_tbwd(None, None, tape.t, ttape.t, U, int(act), tape.B, tape.T,
+                                        None if dH is None else dH.d.contiguous(),
+                                        None if dHd is None else dHd.d.contiguous(), heads[0].w.reshape(-1).contiguous())
+        else:
+            dH, dHd = _mat(dH), _mat(dHd)
+            dZ, dZd = _ops().lstmf_tbwd(None if dH is None else dH.contiguous(), None if dHd is None else dHd.contiguous(),
+                                        tape.t, ttape.t, U, int(act), tape.B, tape.T)
         return (dZ, dZd) if W is None else (dZ, dZd, linear_dgrad(dZ, W), linear_dgrad(dZd, W))
     if isinstance(tape, torch.Tensor):
         heads = [a for a in (dH, dHd) if isinstance(a, OuterAdjoint)]

@@ -1106,6 +1106,61 @@ def test_lstmf_split_forward_vs_exact(cuda, act, B, T, K):
         assert e2 <= 2 * e1 + 2e-6, (errs[1], errs[2])
 
 
+@pytest.mark.parametrize("B,T", [(70, 24), (8192 + 45, 6)])
+def test_lstmf_head_adjoint_in_kernel(cuda, B, T):
+    """fp32: the critic head's adjoint dH = d (x) w generated inside lstmf_bwds / lstmf_tbwdp (HEAD
+    instantiations) vs the materialised dH (skinny dgrad + the plain kernels), for the BPTT (split impl 3;
+    the exact impl 2 materialises in the binding: bitwise) and the tangent reverse with a primal head
+    seed, a tangent one, or both.  The in-kernel product may contract into its consumer's add (one
+    rounding fewer), so the two agree to fp32 rounding and both are checked against fp64."""
+    from hfrep.ops import functional as Fn
+
+    H, K, act = 100, 100, 2
+    g = torch.Generator().manual_seed(71)
+    x, xd = torch.randn(B, T, K, generator=g) * 0.5, torch.randn(B, T, K, generator=g) * 0.5
+    W = torch.randn(K, 4 * H, generator=g) * (1.0 / K ** 0.5)
+    b = torch.randn(4 * H, generator=g) * 0.1
+    U = torch.randn(H, 4 * H, generator=g) * (1.0 / H ** 0.5)
+    d1, d2 = torch.randn(B, 1, generator=g), torch.randn(B, 1, generator=g)
+    w = torch.randn(T * H, 1, generator=g)
+    xg, xdg, Wg, bg, Ug, d1g, d2g, wg = (t_.to(cuda) for t_ in (x, xd, W, b, U, d1, d2, w))
+    o1, o2 = Fn.OuterAdjoint(d1g, wg, (B, T, H)), Fn.OuterAdjoint(d2g, wg, (B, T, H))
+    m1, m2 = o1.materialize(), o2.materialize()
+    # fp64 reference of the BPTT with the exact outer-product adjoint
+    zx = x.double() @ W.double() + b.double()
+    _, rg, rc = R.lstm_seq_fwd(zx, U.double(), act)
+    rdz = R.lstm_seq_bwd((d1.double() * w.double().reshape(1, -1)).reshape(B, T, H), rg, rc, U.double(), act)
+
+    def close(a, c, what):
+        scale = c.abs().max().item()
+        assert (a - c).abs().max().item() <= 1e-5 * scale, what
+
+    ops = _ops()
+    pb = ops.set_lstmf_bwd_impl(3)
+    try:
+        _, tape = Fn.lstm_layer_fwd(xg, Wg, bg, Ug, act, True)
+        for impl in (3, 2):
+            ops.set_lstmf_bwd_impl(impl)
+            a, c = Fn.lstm_layer_bwd(o1, tape, Ug, act), Fn.lstm_layer_bwd(m1, tape, Ug, act)
+            if impl == 2:
+                assert torch.equal(a, c)
+            else:
+                close(a, c, "bwd")
+                ea = (a.double().cpu() - rdz).abs().max().item()
+                ec = (c.double().cpu() - rdz).abs().max().item()
+                assert ea <= 1.05 * ec + 1e-7, (ea, ec)
+            assert torch.equal(a, Fn.lstm_layer_bwd(o1, tape, Ug, act))  # run to run
+        ops.set_lstmf_bwd_impl(3)
+        _, ttape = Fn.lstm_layer_tfwd(xdg, Wg, tape, Ug, act)
+        for a, c in (((None, o2), (None, m2)), ((o1, None), (m1, None)), ((o1, o2), (m1, m2))):
+            za, zad = Fn.lstm_layer_tbwd(a[0], a[1], tape, ttape, Ug, act)
+            zc, zcd = Fn.lstm_layer_tbwd(c[0], c[1] if c[1] is not None else torch.zeros_like(m1), tape, ttape, Ug, act)
+            close(za, zc, "tbwd dZ")
+            close(zad, zcd, "tbwd dZd")
+    finally:
+        ops.set_lstmf_bwd_impl(pb)
+
+
 @pytest.mark.parametrize("act", [2, 1, 0])
 @pytest.mark.parametrize("B,T", [(70, 24), (8192 + 45, 6), (33, 1), (40, 5)])
 def test_lstmf_split_bptt_vs_exact(cuda, act, B, T):
