@@ -96,6 +96,32 @@ Tensor linear(Tensor x, Tensor W, optional<Tensor> b, int64_t act, optional<Tens
   return y;
 }
 
+// linear Dense(1) head forward + its weight gradient for a known per-row loss gradient (wa for the
+// first `split` rows, wb after): y = x W + b, gW += sum_r ds_r x_r, gb += sum_r ds_r in one pass over x
+Tensor linear_head_cs(Tensor x, Tensor W, optional<Tensor> b, int64_t split, double wa, double wb, Tensor gW,
+                      optional<Tensor> gb) {
+  CHECK_GPU(x); CHECK_F32(W); CHECK_F32(gW);
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && x.size(1) == W.size(0) && W.size(1) == 1, "linear_head_cs: (M, K) x (K, 1)");
+  TORCH_CHECK(x.is_contiguous() && W.is_contiguous() && gW.is_contiguous() && gW.numel() == W.numel() &&
+                  gW.device() == x.device(),
+              "linear_head_cs: contiguous operands, gW like W on x's device");
+  if (b.has_value()) { CHECK_F32(*b); TORCH_CHECK(b->numel() == 1, "linear_head_cs: bias size"); }
+  if (gb.has_value()) {
+    CHECK_F32(*gb);
+    TORCH_CHECK(gb->numel() == 1 && gb->device() == x.device(), "linear_head_cs: gb size");
+  }
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(hfrep::skinny_fwd_cs_supported(K), "linear_head_cs: K % 8 == 0 and K <= 4096");
+  GUARD(x);
+  Tensor y = out_empty({M, 1}, x.options());
+  Tensor ws = out_empty({(int64_t)hfrep::skinny_fwd_cs_workspace_floats(M, K)}, x.options().dtype(at::kFloat));
+  hfrep::launch_skinny_fwd_cs(dt_of(x), x.data_ptr(), W.data_ptr<float>(), b.has_value() ? b->data_ptr<float>() : nullptr,
+                              y.data_ptr(), M, K, (int)split, (float)wa, (float)wb, gW.data_ptr<float>(),
+                              gb.has_value() ? gb->data_ptr<float>() : nullptr, ws.data_ptr<float>(), cur_stream(x));
+  return y;
+}
+bool linear_head_cs_supported(int64_t K) { return hfrep::skinny_fwd_cs_supported((int)K); }
+
 Tensor linear_dgrad(Tensor dz, Tensor W) {
   CHECK_GPU(dz); CHECK_F32(W);
   TORCH_CHECK(dz.dim() == 2 && W.dim() == 2 && dz.size(1) == W.size(1), "linear_dgrad: shape mismatch");
@@ -993,6 +1019,8 @@ TORCH_LIBRARY(hfrep, m) {
   m.def("set_lstmf_fwd_impl(int v) -> int", &set_lstmf_fwd_impl);
   m.def("set_lstmf_bwd_impl(int v) -> int", &set_lstmf_bwd_impl);
   m.def("lstmf_fwd(Tensor x, Tensor W, Tensor? b, Tensor U, int act, bool save) -> (Tensor, Tensor)");
+  m.def("linear_head_cs(Tensor x, Tensor W, Tensor? b, int split, float wa, float wb, Tensor(a!) gW, Tensor(b!)? gb) -> Tensor");
+  m.def("linear_head_cs_supported(int K) -> bool", &linear_head_cs_supported);
   m.def("lstmf_bwd(Tensor? dH, Tensor tape, Tensor U, int act, int B, int T, Tensor? hd=None, Tensor? hw=None) -> Tensor");
   m.def("lstmf_tbwd(Tensor? dH, Tensor? dHd, Tensor tape, Tensor ttape, Tensor U, int act, int B, int T, Tensor? hd=None, "
         "Tensor? hdd=None, Tensor? hw=None) -> (Tensor, Tensor)");
@@ -1051,6 +1079,7 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("lstm_fwd", &lstm_fwd);
   m.impl("lstmf_fwd", &lstmf_fwd);
   m.impl("lstmf_tfwd", &lstmf_tfwd);
+  m.impl("linear_head_cs", &linear_head_cs);
   m.impl("lstmf_bwd", &lstmf_bwd);
   m.impl("lstmf_tbwd", &lstmf_tbwd);
   m.impl("lstmf_dgrad", &lstmf_dgrad);

@@ -147,6 +147,13 @@ size_t skinny_wgrad_workspace_floats(int M, int K, int N);
 void launch_skinny_wgrad(int dt, const void* x, const void* d, float* gW, float* gb, int M, int K, int N, float* ws,
                          hipStream_t s);
 void launch_skinny_dgrad(int dt, const void* d, const float* W, void* dx, int M, int K, int N, hipStream_t s);
+// linear Dense(1) head forward y = x W + b that also adds gW += sum_r ds_r x_r, gb += sum_r ds_r for the
+// known per-row loss gradient ds_r = wa (r < split) / wb (the Wasserstein critic loss): one pass over x.
+// ws: skinny_fwd_cs_workspace_floats(M, K) floats (every element written).
+bool skinny_fwd_cs_supported(int K);
+size_t skinny_fwd_cs_workspace_floats(int M, int K);
+void launch_skinny_fwd_cs(int dt, const void* x, const float* W, const float* b, void* y, int M, int K, int split,
+                          float wa, float wb, float* gW, float* gb, float* ws, hipStream_t s);
 // a[0..na) += sum_z slab[z][0..na), b[0..nb) += sum_z slab[z][na..na+nb)  (fixed order; a/b may be null)
 void launch_split_reduce(const float* slab, float* a, float* b, int splits, int na, int nb, hipStream_t s);
 

@@ -16,6 +16,7 @@
 #include "mfma.h"
 
 #include <algorithm>
+#include <stdexcept>
 
 namespace hfrep {
 
@@ -106,6 +107,80 @@ __global__ void __launch_bounds__(256) skinny_fwd_kernel(const T* __restrict__ x
         if (lane == 0 && m0 + r < M) y[(m0 + r) * N + n] = Cvt<T>::from_f(act_f(act, s + (b ? b[n] : 0.f)));
       }
   }
+}
+
+// Linear Dense(1) head forward on rows whose loss gradient is known before the forward: the
+// Wasserstein critic loss (W(real, -1) + W(fake, +1), GAN/MTSS_WGAN_GP.py) gives every row of the
+// [real; fake] batch the constant ds = wa (rows < split) or wb.  The head's weight gradient
+// gW = sum_r ds_r x_r (and gb = sum_r ds_r) is then a signed column sum of the rows the forward streams
+// anyway: each lane keeps the sums of its NC column chunks (c = lane + 64 k) in registers and every wave
+// writes one slab row [K column sums | weight sum], reduced by skinny_reduce_kernel in a fixed order.
+// One pass over x instead of the forward's and skinny_wgrad's two.
+template <typename T, int NC>
+__global__ void __launch_bounds__(256) skinny_fwd_cs_kernel(const T* __restrict__ x, const float* __restrict__ W,
+                                                            const float* __restrict__ b, T* __restrict__ y, int M, int K,
+                                                            int split, float wa, float wb, float* __restrict__ slab) {
+  extern __shared__ float wsh[];  // [K]
+  for (int i = threadIdx.x; i < K; i += 256) wsh[i] = W[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int KC = K / 8;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  float cs[NC][8];
+#pragma unroll
+  for (int k = 0; k < NC; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs[k][j] = 0.f;
+  float ws = 0.f;
+  for (int64_t m0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * SK_ROWS; m0 < M; m0 += nw * SK_ROWS) {
+    float acc[SK_ROWS], wr[SK_ROWS];
+#pragma unroll
+    for (int r = 0; r < SK_ROWS; ++r) {
+      acc[r] = 0.f;
+      wr[r] = m0 + r < M ? (m0 + r < split ? wa : wb) : 0.f;
+      ws += wr[r];
+    }
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = lane + 64 * k;
+      if (c < KC) {
+        Chunk8<T> v[SK_ROWS];
+#pragma unroll
+        for (int r = 0; r < SK_ROWS; ++r) {
+          if (m0 + r < M) v[r].load(x + (m0 + r) * K + 8 * c);
+          else v[r].zero();
+        }
+        float w8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w8[j] = wsh[8 * c + j];
+#pragma unroll
+        for (int r = 0; r < SK_ROWS; ++r) {
+          float f[8];
+          v[r].get(f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            acc[r] = fmaf(f[j], w8[j], acc[r]);
+            cs[k][j] = fmaf(f[j], wr[r], cs[k][j]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < SK_ROWS; ++r) {
+      const float sv = wave_sum(acc[r]);
+      if (lane == 0 && m0 + r < M) y[m0 + r] = Cvt<T>::from_f(sv + (b ? b[0] : 0.f));
+    }
+  }
+  float* out = slab + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (K + 1);
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    const int c = lane + 64 * k;
+    if (c < KC) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out[8 * c + j] = cs[k][j];
+    }
+  }
+  if (lane == 0) out[K] = ws;  // (every lane summed the same row weights)
 }
 
 template <int N, typename T>
@@ -554,6 +629,35 @@ void launch_skinny_fwd(int dt, const void* x, const float* W, const float* b, vo
   else
     HFREP_SKINNY_N(N, skinny_fwd_kernel, float, dim3(grid), dim3(256), (size_t)K * N * sizeof(float), s, (const float*)x,
                    W, b, (float*)y, M, K, act)
+}
+
+// the fused head forward + signed column sum (N = 1, K % 8 == 0, K <= 4096)
+bool skinny_fwd_cs_supported(int K) { return K > 0 && K % 8 == 0 && K <= 4096; }
+static int skinny_cs_grid(int M) {
+  const int64_t groups = ((int64_t)M + 4 * SK_ROWS - 1) / (4 * SK_ROWS);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(groups, (int64_t)device_cu_count() * 2));
+}
+size_t skinny_fwd_cs_workspace_floats(int M, int K) { return (size_t)skinny_cs_grid(M) * 4 * (K + 1); }
+
+void launch_skinny_fwd_cs(int dt, const void* x, const float* W, const float* b, void* y, int M, int K, int split,
+                          float wa, float wb, float* gW, float* gb, float* ws, hipStream_t s) {
+  if (M <= 0) return;
+  if (!skinny_fwd_cs_supported(K)) throw std::runtime_error("skinny_fwd_cs: K % 8 == 0 and K <= 4096");
+  const int grid = skinny_cs_grid(M);
+  const size_t sm = (size_t)K * sizeof(float);
+  auto go = [&](auto kern, auto* xp, auto* yp) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), sm, s, xp, W, b, yp, M, K, split, wa, wb, ws);
+  };
+  const int kc = K / 8;
+  if (dt == DT_BF16) {
+    if (kc <= 320) go(skinny_fwd_cs_kernel<bf16_t, 5>, (const bf16_t*)x, (bf16_t*)y);
+    else go(skinny_fwd_cs_kernel<bf16_t, 8>, (const bf16_t*)x, (bf16_t*)y);
+  } else {
+    if (kc <= 320) go(skinny_fwd_cs_kernel<float, 5>, (const float*)x, (float*)y);
+    else go(skinny_fwd_cs_kernel<float, 8>, (const float*)x, (float*)y);
+  }
+  const int total = K + 1;
+  hipLaunchKernelGGL(skinny_reduce_kernel, dim3((total + 63) / 64), dim3(1024), 0, s, ws, gW, gb, grid * 4, K, 1);
 }
 
 size_t skinny_wgrad_workspace_floats(int M, int K, int N) {

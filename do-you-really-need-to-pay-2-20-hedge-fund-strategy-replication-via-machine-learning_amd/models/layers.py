@@ -125,7 +125,7 @@ class Dense(Layer):
     def forward(self, x):
         return R.dense(x, self.w("kernel"), self.w("bias") if self.use_bias else None, self.act)
 
-    def efwd(self, x, save, out=None, compute=True):
+    def efwd(self, x, save, out=None, compute=True, wgrad_rows=None):
         """``compute=False`` (linear head whose value the caller never reads, e.g. D(x_hat) of the
         gradient penalty: only its input adjoint is used): no kernel runs and ``y`` is an uninitialised
         placeholder of the output's shape -- the linear backward / tangent passes never read it."""
@@ -133,7 +133,16 @@ class Dense(Layer):
             assert self.act_code == 0, "only a linear Dense output can be left uncomputed"
             y = torch.empty(tuple(x.shape[:-1]) + (self.units,), dtype=x.dtype, device=x.device)
             return y, ({"x": x, "y": y} if save else None)
-        y = Fn.linear(x, self.p("kernel"), self.p("bias") if self.use_bias else None, self.act_code, out=out)
+        b = self.p("bias") if self.use_bias else None
+        if (wgrad_rows is not None and save and out is None and self.units == 1 and self.act_code == 0
+                and Fn.head_cs_ok(x, self.p("kernel"))):
+            # the loss gradient of every row is known before the forward (Wasserstein segments): the
+            # head's weight gradient is accumulated in the same pass over x and ebwd skips it
+            split, wa, wb = wgrad_rows
+            y = Fn.linear_head_cs(x, self.p("kernel"), b, split, wa, wb, self.g("kernel"),
+                                  self.g("bias") if self.use_bias else None)
+            return y, {"x": x, "y": y, "wgrad_done": True}
+        y = Fn.linear(x, self.p("kernel"), b, self.act_code, out=out)
         return y, ({"x": x, "y": y} if save else None)
 
     def _dgrad(self, dz):
@@ -145,7 +154,7 @@ class Dense(Layer):
 
     def ebwd(self, ctx, dy, need_dx, wgrad=True):
         dz = Fn.act_backward(dy, ctx["y"], self.act_code)
-        if wgrad:
+        if wgrad and not ctx.get("wgrad_done"):
             Fn.run_wgrad(Fn.linear_wgrad_, ctx["x"], dz, self.g("kernel"), self.g("bias") if self.use_bias else None)
         return self._dgrad(dz) if need_dx else None
 
@@ -501,11 +510,14 @@ class Sequential(torch.nn.Module):
         last = self.layers[-1] if self.layers else None
         return isinstance(last, Dense) and last.act_code == 0
 
-    def efwd(self, x, save: bool = True, out=None, head_out: bool = True):
+    def efwd(self, x, save: bool = True, out=None, head_out: bool = True, head_wgrad=None):
         """``out``: destination of the model output, used when the last layer can write into it
         (Dense); otherwise the output is copied there.  ``head_out=False``: the caller only needs the
         tape (e.g. the gradient penalty's forward on x_hat, whose score nothing reads): a linear Dense
-        head is not evaluated and the returned output is a shape-only placeholder."""
+        head is not evaluated and the returned output is a shape-only placeholder.  ``head_wgrad=(split,
+        wa, wb)``: the loss gradient of the output rows is known already (wa for rows < split, wb after:
+        the Wasserstein critic terms); a linear Dense(1) head then accumulates its own weight gradient
+        in the forward pass (one read of its input) and ``ebwd`` skips it."""
         skip_head = not head_out and self._head_skippable()
         tape = []
         i, n = 0, len(self.layers)
@@ -524,6 +536,8 @@ class Sequential(torch.nn.Module):
                 continue
             if skip_head and i == n - 1:
                 x, ctx = l.efwd(x, save, compute=False)
+            elif head_wgrad is not None and i == n - 1 and isinstance(l, Dense) and out is None:
+                x, ctx = l.efwd(x, save, wgrad_rows=head_wgrad)
             elif out is not None and i == n - 1 and isinstance(l, Dense):
                 x, ctx = l.efwd(x, save, out=out)
             else:

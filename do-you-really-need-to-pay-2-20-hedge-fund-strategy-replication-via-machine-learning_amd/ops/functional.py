@@ -279,6 +279,25 @@ def gan_loss(p: torch.Tensor, split: int, la: float, lb: float, kind: int):
                       acc=torch.float64 if p.dtype == torch.float64 else torch.float32)
 
 
+def head_cs_ok(x: torch.Tensor, W: torch.Tensor) -> bool:
+    """Whether a linear Dense(1) head on x can run as the fused forward + known-gradient column sum."""
+    return (x.dim() == 2 and W.dim() == 2 and W.shape[1] == 1 and x.dtype in (torch.bfloat16, torch.float32)
+            and _nat(x) and not _native.fallback_allowed() and bool(_ops().linear_head_cs_supported(int(W.shape[0]))))
+
+
+def loss_grad_value(label: float, n: int, dtype) -> float:
+    """The per-row gradient gan_loss (kind 0) writes for a segment of n rows with this label: label * (1/n)
+    in fp32, stored in the score dtype."""
+    inv = torch.tensor(1.0, dtype=torch.float32) / torch.tensor(float(n), dtype=torch.float32)
+    return float((torch.tensor(float(label), dtype=torch.float32) * inv).to(dtype).item())
+
+
+def linear_head_cs(x, W, b, split: int, wa: float, wb: float, gW, gb):
+    """y = x W + b for a linear Dense(1) head, and in the same pass gW += sum_r ds_r x_r, gb += sum_r ds_r
+    for the known per-row loss gradient ds_r = wa (r < split) / wb (csrc/skinny.hip skinny_fwd_cs_kernel)."""
+    return _ops().linear_head_cs(x.contiguous(), W, b, int(split), float(wa), float(wb), gW, gb)
+
+
 def gp_coef(g: torch.Tensor, weight: float):
     """(penalty, v): penalty = mean((1-||g_b||)^2); v = d(weight*penalty)/dg."""
     if _nat(g):

@@ -292,8 +292,12 @@ class GANTrainer:
         with Fn.wgrad_on(self._wgrad_side(hook)):
             # W terms on [real; fake]
             with trange("critic/w_terms"):
-                s, tape = C.efwd(xrf, save=True)
-                # W(real, -1) and W(fake, +1): both segment means and the score gradient in one launch
+                # W(real, -1) and W(fake, +1): the score gradient of every row is the known constant
+                # -1/B or +1/B, so the head's weight gradient rides along with the head forward
+                n2 = xrf.shape[0] // 2
+                hw = (n2, Fn.loss_grad_value(-1.0, n2, xrf.dtype), Fn.loss_grad_value(1.0, xrf.shape[0] - n2, xrf.dtype))
+                s, tape = C.efwd(xrf, save=True, head_wgrad=hw)
+                # both segment means and the score gradient in one launch
                 w, ds = Fn.gan_loss(s, s.numel() // 2, -1.0, 1.0, 0)
                 C.ebwd(tape, ds)
             if side is not None:

@@ -1201,3 +1201,41 @@ def test_lstmf_split_bptt_vs_exact(cuda, act, B, T):
     print(f"max abs err exact {errs[2]:.3e} split {errs[3]:.3e}")
     assert torch.isfinite(out[3]).all()
     assert errs[3] <= 2 * errs[2] + 2e-6, errs
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("B", [37, 3000])
+def test_critic_head_wgrad_fused_in_forward(cuda, dtype, B, monkeypatch):
+    """The W terms' critic head: with the loss gradient of every row known (-1/B real, +1/B fake) the
+    head's weight gradient is accumulated by the head forward itself (skinny_fwd_cs_kernel: one pass over
+    the layer-2 output instead of skinny_fwd + skinny_wgrad).  Against the unfused path on the same GP
+    critic step: the loss pack is bitwise equal (same score arithmetic) and the critic gradient agrees to
+    the fp32 summation order; two fused runs are bitwise equal."""
+    import numpy as np
+
+    from hfrep.ops import functional as Fn
+    from hfrep.train.gan_trainer import GANConfig, GANTrainer
+
+    T, F = 24, 32
+    ds = np.random.RandomState(5).rand(64, T, F).astype(np.float32)
+    tr = GANTrainer(GANConfig(arch="lstm", loss="wgan_gp", window=T, features=F, batch_size=B, dtype=dtype), ds,
+                    device=cuda)
+    g = torch.Generator().manual_seed(4)
+    real = torch.rand(B, T, F, generator=g).to(cuda, tr.dtype)
+    fake = torch.rand(B, T, F, generator=g).to(cuda, tr.dtype)
+    alpha = torch.rand(B, generator=g).to(cuda)
+    runs = []
+    for fused in (True, True, False):
+        if not fused:
+            monkeypatch.setattr(Fn, "head_cs_ok", lambda x, W: False)
+        tr.critic.zero_grad()
+        with torch.no_grad():
+            pack = tr.critic_gp_grads(real, fake, alpha)
+        torch.cuda.synchronize()
+        runs.append((pack.clone(), tr.critic.flat.grad.clone()))
+    assert Fn.head_cs_ok is not None
+    (p0, g0), (p1, g1), (p2, g2) = runs
+    assert torch.equal(p0, p1) and torch.equal(g0, g1)
+    assert torch.equal(p0, p2), (p0, p2)
+    rel = ((g0 - g2).norm() / g2.norm()).item()
+    assert rel < 1e-5, rel
