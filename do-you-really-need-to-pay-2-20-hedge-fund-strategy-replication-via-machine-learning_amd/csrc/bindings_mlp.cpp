@@ -125,6 +125,35 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> mlp_wgp_critic(Tensor
 
 bool mlp_wgpw_supported_op(int64_t F, int64_t T) { return hfrep::mlp_wgpw_supported((int)F, (int)T); }
 
+// the GP critic update with per-t column-sum weight gradients (fp32 / bf16): adds gW1, gW2, gw3 into the
+// fp32 gradient views and returns the W-loss slab
+Tensor mlp_wgp_critic_t(Tensor real, Tensor fake, Tensor c, std::vector<Tensor> cp, Tensor gW1, Tensor gW2, Tensor gw3) {
+  const int dt = act_dt(real);
+  TORCH_CHECK(fake.scalar_type() == real.scalar_type() && fake.sizes() == real.sizes(), "mlp_wgp_critic_t: fake like real");
+  act_dt(fake);
+  const int64_t F = real.size(-1), H = hidden_of(cp, F), B = real.size(0), T = real.size(1);
+  rows_of(real, F, "real");
+  const auto cr = critic_of(cp, F, H, T * H);
+  TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kFloat && c.is_contiguous() && c.numel() == B,
+              "mlp_wgp_critic_t: c (B) fp32");
+  for (const Tensor* g : {&gW1, &gW2, &gw3})
+    TORCH_CHECK(g->device() == real.device(), "mlp_wgp_critic_t: gradients on the activations' device");
+  float* pW1 = const_cast<float*>(w(gW1, F * H, "gW1"));
+  float* pW2 = const_cast<float*>(w(gW2, H * H, "gW2"));
+  float* pw3 = const_cast<float*>(w(gw3, T * H, "gw3"));
+  GUARD(real);
+  const int P = hfrep::mlp_wgpt_blocks((int)T);
+  auto f32 = real.options().dtype(at::kFloat);
+  // every tslab / slab row is written by its wave (waves without a tile write zeros)
+  Tensor tslab = at::empty({4 * (int64_t)P, F + 2 * H}, f32);
+  Tensor tsum = at::empty({(int64_t)hfrep::mlp_wgpt_tsum_floats((int)F, (int)T)}, f32);
+  Tensor slab = at::empty({4 * (int64_t)P, 2}, f32);
+  hfrep::launch_mlp_wgp_critic_t(dt, real.data_ptr(), fake.data_ptr(), c.data_ptr<float>(), cr, tslab.data_ptr<float>(),
+                                 tsum.data_ptr<float>(), slab.data_ptr<float>(), B, (int)T, (int)F, pW1, pW2, pw3,
+                                 cur_stream(real));
+  return slab;
+}
+
 // the GP critic update with in-kernel weight gradients (bf16): adds gW1, gW2, gw3 into the given fp32
 // gradient views (bias gradients cancel, as in mlp_wgp_critic) and returns the W-loss slab
 Tensor mlp_wgp_critic_w(Tensor real, Tensor fake, Tensor c, std::vector<Tensor> cp, Tensor gW1, Tensor gW2,
@@ -300,6 +329,8 @@ TORCH_LIBRARY_FRAGMENT(hfrep, m) {
   m.def("mlp_wgp_coef(Tensor gsq, float lam) -> (Tensor, Tensor)");
   m.def("mlp_wgp_critic(Tensor real, Tensor fake, Tensor c, Tensor[] cp) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("mlp_wgpw_supported(int F, int T) -> bool", &mlp_wgpw_supported_op);
+  m.def("mlp_wgp_critic_t(Tensor real, Tensor fake, Tensor c, Tensor[] cp, Tensor(a!) gW1, Tensor(b!) gW2, "
+        "Tensor(c!) gw3) -> Tensor");
   m.def("mlp_wgp_critic_w(Tensor real, Tensor fake, Tensor c, Tensor[] cp, Tensor(a!) gW1, Tensor(b!) gW2, "
         "Tensor(c!) gw3) -> Tensor");
   m.def("mlp_gen_bwd_w(Tensor noise, Tensor dfake, Tensor[] gp, Tensor(a!)[] gg) -> ()");
@@ -315,6 +346,7 @@ TORCH_LIBRARY_FRAGMENT(hfrep, m) {
 TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("mlp_gen_fwd", &mlp_gen_fwd);
   m.impl("mlp_wgp_critic_w", &mlp_wgp_critic_w);
+  m.impl("mlp_wgp_critic_t", &mlp_wgp_critic_t);
   m.impl("mlp_gen_bwd_w", &mlp_gen_bwd_w);
   m.impl("mlp_gan_critic_g", &mlp_gan_critic_g);
   m.impl("mlp_wgp_norm", &mlp_wgp_norm);

@@ -81,6 +81,16 @@ void launch_mlp_gan_critic_g(int dt, const void* x, const MlpCritic& cr, float l
                              int64_t M, int F, hipStream_t s);
 void launch_mlp_gan_grad_finish(const float* v, const MlpCritic& cr, int F, int H, float* gW1, float* gb1, float* gW2,
                                 float* gb2, float* gw3, float* gb3, hipStream_t s);
+// The GP critic update with per-t column-sum weight gradients (fp32 / bf16): rows walked t-major, one t
+// per wave (mlp_wgpt_waves_per_t(T) waves per t, mlp_wgpt_blocks(T) workgroups); tslab: 4 rows per
+// workgroup of F + 2 H floats, tsum: mlp_wgpt_tsum_floats(F, T) floats (scratch), slab: the W-loss partials
+// (4 rows per workgroup x 2); gW1 / gW2 / gw3 accumulate.  Bn = samples (rows = Bn T).
+int mlp_wgpt_waves_per_t(int Tn);
+int mlp_wgpt_blocks(int Tn);
+size_t mlp_wgpt_tsum_floats(int F, int Tn);
+void launch_mlp_wgp_critic_t(int dt, const void* real, const void* fake, const float* c, const MlpCritic& cr,
+                             float* tslab, float* tsum, float* slab, int64_t Bn, int Tn, int F, float* gW1, float* gW2,
+                             float* gw3, hipStream_t s);
 int mlp_gbw_blocks(int64_t M);
 void launch_mlp_gen_bwd_w(const void* noise, const void* dfake, const MlpGen& g, float* gslab, float* lnslab, int64_t M,
                           int F, hipStream_t s);

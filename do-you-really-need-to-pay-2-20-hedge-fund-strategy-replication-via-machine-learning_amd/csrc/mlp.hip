@@ -526,6 +526,155 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_wgp_critic_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------------
+// The same critic update with the weight gradients taken in the kernel by per-t column sums (any dtype;
+// the fp32 path, whose weight images leave no LDS for mlp_wgp_critic_w's staging).
+//
+// Rows are walked t-major: wave wid owns t = wid % Tn and takes 32-SAMPLE tiles (rows b T + t,
+// b = 32 bt + lane) of that t only.  Every adjoint of such a tile lies along the same vectors (w3_t
+// for layer 2, dh1'_t = W2 w3_t for layer 1), so
+//   gW2 = sum_t S2[t] (x) w3_t,  gW1 = sum_t S1[t] (x) dh1'_t,  gw3_t = S3[t],
+//   S1[t] = sum_b X1c[b, t],  S2[t] = sum_b X2c[b, t],  S3[t] = sum_b Y3c[b, t]
+// (X1c, X2c, Y3c the per-row operands of mlp_wgp_critic, computed here in registers as there).  Each
+// tile adds its transpose-reduce column sums to ~10 per-lane registers; a wave writes one slab row
+// [S1 F | S2 H | S3 H] for its t at the end, and mlp_wgp_tsum_finish reduces the rows of each t in a
+// fixed order and forms the outer products.  No per-row operand leaves the kernel.
+// ---------------------------------------------------------------------------------------------------
+template <typename T, int F, int H>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_wgp_critic_t_kernel(
+    const T* __restrict__ real, const T* __restrict__ fake, const float* __restrict__ cvec, MlpCritic c,
+    float* __restrict__ tslab, float* __restrict__ slab, int64_t Bn, int Tn, int kper, float invB) {
+  using Fr = typename MP<T>::frag;
+  constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  Fr* f1 = reinterpret_cast<Fr*>(lds);
+  Fr* f2 = f1 + fwd_entries<T, F, H>() * 64;
+  Fr* d2 = f2 + fwd_entries<T, H, H>() * 64;
+  Fr* d1 = d2 + dgrad_entries<T, H, H>() * 64;
+  float* vec = reinterpret_cast<float*>(d1 + dgrad_entries<T, F, H>() * 64);
+  build_fwd<T, F, H>(f1, c.W1);
+  build_fwd<T, H, H>(f2, c.W2);
+  build_dgrad<T, H, H>(d2, c.W2);
+  build_dgrad<T, F, H>(d1, c.W1);
+  load_vec(vec, c.b1, H);
+  load_vec(vec + VEC, c.b2, H);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int wid = blockIdx.x * MLP_WAVES + (threadIdx.x >> 6);
+  const int tt = wid % Tn, j = wid / Tn;  // this wave's t and its index among the kper waves of that t
+  const float* w3t = c.w3 + (int64_t)tt * H;
+  float s1[NTF], s2[NTH], s3[NTH];
+#pragma unroll
+  for (int i = 0; i < NTF; ++i) s1[i] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NTH; ++i) s2[i] = s3[i] = 0.f;
+  float sr = 0.f, sf = 0.f;
+  const int64_t nbt = (Bn + 31) / 32;
+  for (int64_t bt = j; j < kper && bt < nbt; bt += kper) {
+    const int64_t b = bt * 32 + (lane & 31);
+    const bool ok = b < Bn;
+    const int64_t row = ok ? b * Tn + tt : 0;
+    const int64_t M = ok ? row + 1 : 0;  // load_rows' bound: the lane's own row only
+    f32x16 A[NTH], Bv[NTH], X2[NTH], X1[NTF], x[NTF];
+    head_rows<H>(A, w3t, 1.f, true, h);
+    dense<T, H, H>(A, Bv, d2, lane);            // dh1' = W2 w3_t
+    dense<T, H, F>(Bv, X1, d1, lane);           // g = W1 dh1'
+    const float cb = ok ? cvec[b] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NTF; ++i) X1[i] *= cb;  // v
+    dense<T, F, H>(X1, X2, f1, lane);           // zd1 = v W1
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const float sg = pass ? invB : -invB;
+      load_rows<T, F>(x, pass ? fake : real, row, M, h);
+      axpy<F>(X1, sg, x);
+      dense<T, F, H>(x, A, f1, lane);
+      bias_act<H>(A, vec, ACT_LINEAR, h);       // h1
+      axpy<H>(X2, sg, A);
+      dense<T, H, H>(A, Bv, f2, lane);
+      bias_act<H>(Bv, vec + VEC, ACT_LINEAR, h);  // h2
+      const float sc = rowdot<H>(Bv, w3t, ok, h);
+      if (ok && h == 0) {
+        if (pass) sf += sc;
+        else sr += sc;
+      }
+    }
+    if (!ok) {  // samples past B contribute nothing
+#pragma unroll
+      for (int i = 0; i < NTH; ++i) X2[i] = zero16();
+#pragma unroll
+      for (int i = 0; i < NTF; ++i) X1[i] = zero16();
+    }
+    dense<T, H, H>(X2, A, f2, lane);            // Y3c = X2c W2
+#pragma unroll
+    for (int i = 0; i < NTF; ++i) s1[i] += colsum(X1[i], lane);
+#pragma unroll
+    for (int i = 0; i < NTH; ++i) {
+      s2[i] += colsum(X2[i], lane);
+      s3[i] += colsum(A[i], lane);
+    }
+  }
+  // this wave's per-t partial sums (lanes l, l ^ 1 hold the same column): row wid of tslab
+  constexpr int L = F + 2 * H;
+  float* out = tslab + (int64_t)wid * L;
+  const int fq = featq(colsum_q(lane), h);
+  if ((lane & 1) == 0) {
+#pragma unroll
+    for (int i = 0; i < NTF; ++i)
+      if (32 * i + fq < F) out[32 * i + fq] = s1[i];
+#pragma unroll
+    for (int i = 0; i < NTH; ++i)
+      if (32 * i + fq < H) {
+        out[F + 32 * i + fq] = s2[i];
+        out[F + H + 32 * i + fq] = s3[i];
+      }
+  }
+  slab_put(slab, 2, 0, sr);
+  slab_put(slab, 2, 1, sf);
+}
+
+// (1) S[t][col] = the fixed-order sum of the kper slab rows of t (rows wid = t + Tn j), and
+// D[t][o] = dh1'_t[o] = sum_k W2[o][k] w3_t[k]: tsum = [Tn][L = F + 2 H] then [Tn][H]
+__global__ void __launch_bounds__(256) mlp_wgp_tsum_prep_kernel(const float* __restrict__ tslab, MlpCritic c, int F,
+                                                                int H, int Tn, int kper, float* __restrict__ tsum) {
+  const int L = F + 2 * H;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e < Tn * L) {
+    const int t = e / L, col = e - t * L;
+    float a = 0.f;
+    for (int jj = 0; jj < kper; ++jj) a += tslab[(int64_t)(t + Tn * jj) * L + col];
+    tsum[e] = a;
+  } else if (e < Tn * L + Tn * H) {
+    const int q = e - Tn * L, t = q / H, o = q - t * H;
+    float d = 0.f;
+    for (int k = 0; k < H; ++k) d = fmaf(c.W2[o * H + k], c.w3[t * H + k], d);
+    tsum[e] = d;
+  }
+}
+// (2) gW1 += sum_t S1[t] (x) D[t], gW2 += sum_t S2[t] (x) w3_t, gw3_t += S3[t]: one output per thread
+__global__ void __launch_bounds__(256) mlp_wgp_tsum_finish_kernel(const float* __restrict__ tsum, MlpCritic c, int F,
+                                                                  int H, int Tn, float* __restrict__ gW1,
+                                                                  float* __restrict__ gW2, float* __restrict__ gw3) {
+  const int L = F + 2 * H;
+  const float* D = tsum + Tn * L;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int n1 = F * H, n2 = H * H, n3 = Tn * H;
+  if (e < n1) {
+    const int i = e / H, o = e - i * H;
+    float acc = 0.f;
+    for (int t = 0; t < Tn; ++t) acc = fmaf(tsum[t * L + i], D[t * H + o], acc);
+    gW1[e] += acc;
+  } else if (e < n1 + n2) {
+    const int q = e - n1, i = q / H, o = q - i * H;
+    float acc = 0.f;
+    for (int t = 0; t < Tn; ++t) acc = fmaf(tsum[t * L + F + i], c.w3[t * H + o], acc);
+    gW2[q] += acc;
+  } else if (e < n1 + n2 + n3) {
+    const int q = e - n1 - n2, t = q / H, o = q - t * H;
+    gw3[q] += tsum[t * L + F + H + o];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
 // The same critic update with the three weight gradients accumulated in the kernel (bf16).
 //
 // mlp_wgp_critic writes 5 per-row operands (872 B a row at F = 36) that linear_wgrad_ reads back:
@@ -1680,6 +1829,31 @@ void launch_mlp_gan_critic_g(int dt, const void* x, const MlpCritic& cr, float l
 void launch_mlp_gan_grad_finish(const float* v, const MlpCritic& cr, int F, int H, float* gW1, float* gb1, float* gW2,
                                 float* gb2, float* gw3, float* gb3, hipStream_t s) {
   hipLaunchKernelGGL(mlp_gan_grad_finish_kernel, dim3(1), dim3(256), 0, s, v, cr, F, H, gW1, gb1, gW2, gb2, gw3, gb3);
+}
+
+// ---- GP critic update with per-t column-sum gradients (fp32 / bf16) ----
+int mlp_wgpt_waves_per_t(int Tn) { return std::max(1, device_cu_count() * 2 * MLP_WAVES / std::max(1, Tn)); }
+int mlp_wgpt_blocks(int Tn) { return (mlp_wgpt_waves_per_t(Tn) * Tn + MLP_WAVES - 1) / MLP_WAVES; }
+size_t mlp_wgpt_tsum_floats(int F, int Tn) { return (size_t)Tn * (F + 3 * 100); }
+
+void launch_mlp_wgp_critic_t(int dt, const void* real, const void* fake, const float* c, const MlpCritic& cr,
+                             float* tslab, float* tsum, float* slab, int64_t Bn, int Tn, int F, float* gW1, float* gW2,
+                             float* gw3, hipStream_t s) {
+  if (Bn <= 0) return;
+  const int kper = mlp_wgpt_waves_per_t(Tn), P = mlp_wgpt_blocks(Tn);
+  const float invB = 1.f / (float)Bn;
+  MLP_DISPATCH(dt, F, {
+    auto k = mlp_wgp_critic_t_kernel<T, FF, 100>;
+    constexpr size_t lds = lds_critic4<T, FF, 100>();
+    set_lds(k, lds);
+    hipLaunchKernelGGL(k, dim3(P), dim3(MLP_THREADS), lds, s, (const T*)real, (const T*)fake, c, cr, tslab, slab, Bn, Tn,
+                       kper, invB);
+  });
+  const int H = 100, L = F + 2 * H;
+  const int np = Tn * (L + H), nf = F * H + H * H + Tn * H;
+  hipLaunchKernelGGL(mlp_wgp_tsum_prep_kernel, dim3((np + 255) / 256), dim3(256), 0, s, tslab, cr, F, H, Tn, kper, tsum);
+  hipLaunchKernelGGL(mlp_wgp_tsum_finish_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, tsum, cr, F, H, Tn, gW1, gW2,
+                     gw3);
 }
 
 // ---- generator reverse with in-kernel parameter gradients (bf16) ----

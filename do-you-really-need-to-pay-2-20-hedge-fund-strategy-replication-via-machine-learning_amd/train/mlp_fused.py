@@ -11,7 +11,8 @@ replaces it with one kernel per pass that carries a 32-row tile through every la
 * ``mlp_wgp_critic``  a whole WGAN-GP critic update of the linear critic (GAN/WGAN_GP.py:238-253):
   W terms on real / fake and the reverse-over-tangent of the penalty, as one combined weight-gradient
   operand per weight (see the kernel's comment); in bf16 ``mlp_wgp_critic_w`` also accumulates the
-  three weight gradients in the kernel (128-row block tiles staged transposed in LDS);
+  three weight gradients in the kernel (128-row block tiles staged transposed in LDS), in fp32
+  ``mlp_wgp_critic_t`` (rows walked t-major, per-t column sums in registers);
 * ``mlp_gan_critic``  a vanilla-GAN discriminator update (GAN/GAN.py:144-158, 187-189);
   ``mlp_gan_critic_g`` takes its gradients in the kernel as dz-weighted column sums (the linear hidden
   layers make every adjoint of a row rank-1);
@@ -90,14 +91,17 @@ class FusedMLP:
         self.gw, self.gg = _gen_lists(tr.generator), _gen_lists(tr.generator, grad=True)
         self.cw, self.cg = _critic_lists(tr.critic, self.head), _critic_lists(tr.critic, self.head, grad=True)
         self._ones = {}
-        # bf16 GP critic update with the weight gradients accumulated inside the pass kernel
-        # (mlp_wgp_critic_w): no per-row operands in HBM.  HFREP_MLP_WGRAD_INKERNEL=0 keeps the operand
-        # path (mlp_wgp_critic + linear_wgrad_) for A/B; fp32 always uses it (its LDS images leave no room)
-        # (the generator reverse likewise: mlp_gen_bwd_w)
+        # GP critic update (both dtypes): rows walked t-major, the weight gradients as per-t column sums
+        # in registers (mlp_wgp_critic_t) -- no per-row operands in HBM.  HFREP_MLP_WGRAD_TSUM=0 takes
+        # the bf16 kernel that stages 128-row tiles transposed in LDS instead (mlp_wgp_critic_w, A/B:
+        # 4 % slower on config 4, profiles/r06_wgpw/tsum); HFREP_MLP_WGRAD_INKERNEL=0 keeps the operand
+        # path (mlp_wgp_critic + linear_wgrad_).  The generator reverse: mlp_gen_bwd_w (bf16).
         cfg = tr.cfg
-        inkernel = tr.dtype == torch.bfloat16 and os.environ.get("HFREP_MLP_WGRAD_INKERNEL", "1") != "0"
-        self.wgrad_inkernel = (inkernel and self.head == 0
+        on = os.environ.get("HFREP_MLP_WGRAD_INKERNEL", "1") != "0"
+        inkernel = tr.dtype == torch.bfloat16 and on
+        self.wgrad_inkernel = (inkernel and self.head == 0 and os.environ.get("HFREP_MLP_WGRAD_TSUM", "1") == "0"
                                and bool(_ops().mlp_wgpw_supported(int(cfg.features), int(cfg.window))))
+        self.wgrad_tsum = self.head == 0 and on and not self.wgrad_inkernel
         self.gen_wgrad_inkernel = inkernel
         # GAN discriminator: rank-1 adjoints per row -> gradients as dz-weighted column sums in the
         # kernel (mlp_gan_critic_g, both dtypes); HFREP_MLP_WGRAD_INKERNEL=0 keeps the operand path
@@ -152,8 +156,9 @@ class FusedMLP:
         gsq = ops.mlp_wgp_norm(real, self.cw)
         c, e = ops.mlp_wgp_coef(gsq, float(tr.gp_weight))
         gW1, _gb1, gW2, _gb2, gw3, _gb3 = self.cg
-        if self.wgrad_inkernel:
-            slab = ops.mlp_wgp_critic_w(real, fake, c, self.cw, gW1, gW2, gw3)
+        if self.wgrad_inkernel or self.wgrad_tsum:
+            op = ops.mlp_wgp_critic_w if self.wgrad_inkernel else ops.mlp_wgp_critic_t
+            slab = op(real, fake, c, self.cw, gW1, gW2, gw3)
             return ops.mlp_finish(slab, e, 0, 1.0 / B, self.cw[5], float(tr.gp_weight))
         X2c, dY2, X1c, dY1, Y3c, slab = ops.mlp_wgp_critic(real, fake, c, self.cw)
         # the W terms' bias gradients cancel (-1/B and +1/B per row pair) and the tangent has none

@@ -166,14 +166,14 @@ def test_mlp_wgp_inkernel_wgrad_matches_operand_path(cuda, B, T, F):
     assert not ops.mlp_wgpw_supported(36, 48) and not ops.mlp_wgpw_supported(32, 40)  # the LDS plan
     tg, _ = _pair(cuda, "wgan_gp", "bfloat16", B, T, F)
     fz, dt = tg._fused, tg.dtype
-    assert fz.wgrad_inkernel
+    assert fz.wgrad_tsum and not fz.wgrad_inkernel  # the t-major kernel is the default
     real, noise, _ = _inputs(B, T, F, seed=5)
     grads, packs = [], []
     with torch.no_grad():
         fake = ops.mlp_gen_fwd(noise.to(cuda, dt), fz.gw)
         r = real.to(cuda, dt)
         for inkernel in (True, True, False):
-            fz.wgrad_inkernel = inkernel
+            fz.wgrad_inkernel, fz.wgrad_tsum = inkernel, False
             tg.critic.zero_grad()
             packs.append(fz._wgp_critic_grads(r, fake).clone())
             grads.append(tg.critic.flat.grad.clone())
@@ -238,3 +238,32 @@ def test_mlp_gan_critic_colsum_matches_operand_path(cuda, dtype, B, F):
             rel = _rel(grads[0], grads[2])
             assert rel < (1e-5 if dtype == "float32" else 5e-3), f"label {label}: column-sum vs operand rel {rel:.2e}"
             torch.testing.assert_close(losses[0], losses[2], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("B,T,F", [(37, 24, 32), (300, 40, 32), (45, 48, 36), (6000, 24, 32)])
+def test_mlp_wgp_tsum_matches_operand_path(cuda, dtype, B, T, F):
+    """Config 4: the GP critic update with rows walked t-major and the weight gradients as per-t column
+    sums (mlp_wgp_critic_t: gW2 = sum_t S2[t] (x) w3_t, gW1 = sum_t S1[t] (x) W2 w3_t, gw3_t = S3[t]) vs
+    the operand path on the same batch: the loss pack to fp32 rounding (the score sums run in another
+    order), the gradient to the summation order (fp32) / the operand path's bf16 operand rounding (bf16);
+    two runs bitwise identical."""
+    tg, tc = _pair(cuda, "wgan_gp", dtype, B, T, F)
+    fz, dt = tg._fused, tg.dtype
+    real, noise, alpha = _inputs(B, T, F, seed=7)
+    packs, grads = [], []
+    with torch.no_grad():
+        fake = torch.ops.hfrep.mlp_gen_fwd(noise.to(cuda, dt), fz.gw)
+        r = real.to(cuda, dt)
+        for mode in ("t", "t", "op"):
+            fz.wgrad_inkernel, fz.wgrad_tsum = False, mode == "t"
+            tg.critic.zero_grad()
+            packs.append(fz._wgp_critic_grads(r, fake).clone())
+            grads.append(tg.critic.flat.grad.clone())
+        pack_c = tc.critic_gp_grads(real.double(), fake.double().cpu(), alpha.double())
+        rel_c = _rel(grads[0], tc.critic.flat.grad)
+    assert torch.equal(grads[0], grads[1]) and torch.equal(packs[0], packs[1])
+    torch.testing.assert_close(packs[0], packs[2], rtol=1e-5, atol=1e-6)
+    rel = _rel(grads[0], grads[2])
+    assert rel < (1e-5 if dtype == "float32" else 3e-3), f"per-t sums vs operand path rel {rel:.2e}"
+    assert rel_c < TOL[dtype], f"vs fp64 rel {rel_c:.2e}"
