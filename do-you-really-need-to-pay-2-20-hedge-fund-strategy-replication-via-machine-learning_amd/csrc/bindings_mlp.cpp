@@ -154,6 +154,57 @@ Tensor mlp_wgp_critic_t(Tensor real, Tensor fake, Tensor c, std::vector<Tensor> 
   return slab;
 }
 
+bool mlp_affine_supported_op(int64_t F, int64_t T) { return hfrep::mlp_affine_supported((int)F, (int)T); }
+
+inline void check_affine(const Tensor& x, const char* what) {
+  TORCH_CHECK(hfrep::mlp_affine_supported((int)x.size(2), (int)x.size(1)), what, ": T F must be a multiple of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, what, ": 16-byte aligned rows");
+}
+
+// the affine critic's GP update from batch sums (fp32 / bf16): adds gW1, gW2, gw3 into the fp32 gradient
+// views, returns the score slab (1, 2) and the penalty sum e (1) for mlp_finish
+std::tuple<Tensor, Tensor> mlp_wgp_affine(Tensor real, Tensor fake, std::vector<Tensor> cp, double lam, Tensor gW1,
+                                          Tensor gW2, Tensor gw3) {
+  const int dt = act_dt(real);
+  TORCH_CHECK(fake.scalar_type() == real.scalar_type() && fake.sizes() == real.sizes(), "mlp_wgp_affine: fake like real");
+  act_dt(fake);
+  const int64_t F = real.size(-1), H = hidden_of(cp, F), B = real.size(0), T = real.size(1);
+  rows_of(real, F, "real");
+  check_affine(real, "mlp_wgp_affine");
+  check_affine(fake, "mlp_wgp_affine");
+  const auto cr = critic_of(cp, F, H, T * H);
+  for (const Tensor* g : {&gW1, &gW2, &gw3})
+    TORCH_CHECK(g->device() == real.device(), "mlp_wgp_affine: gradients on the activations' device");
+  float* pW1 = const_cast<float*>(w(gW1, F * H, "gW1"));
+  float* pW2 = const_cast<float*>(w(gW2, H * H, "gW2"));
+  float* pw3 = const_cast<float*>(w(gw3, T * H, "gw3"));
+  GUARD(real);
+  auto f32 = real.options().dtype(at::kFloat);
+  Tensor ws = at::empty({(int64_t)hfrep::mlp_affine_ws_floats(dt, B, (int)T, (int)F)}, f32);
+  Tensor slab = at::empty({1, 2}, f32), e = at::empty({1}, f32);
+  hfrep::launch_mlp_wgp_affine(dt, real.data_ptr(), fake.data_ptr(), cr, B, (int)T, (int)F, (float)lam,
+                               ws.data_ptr<float>(), slab.data_ptr<float>(), e.data_ptr<float>(), pW1, pW2, pw3,
+                               cur_stream(real));
+  return {slab, e};
+}
+
+// the affine critic's input gradient for the generator step: dfake (B, T, F) = -g_t / B per row, and
+// the fake score slab (1, 2) for mlp_finish mode 1
+std::tuple<Tensor, Tensor> mlp_critic_dx_affine(Tensor fake, std::vector<Tensor> cp) {
+  const int dt = act_dt(fake);
+  const int64_t F = fake.size(-1), H = hidden_of(cp, F), B = fake.size(0), T = fake.size(1);
+  rows_of(fake, F, "fake");
+  check_affine(fake, "mlp_critic_dx_affine");
+  const auto cr = critic_of(cp, F, H, T * H);
+  GUARD(fake);
+  auto f32 = fake.options().dtype(at::kFloat);
+  Tensor ws = at::empty({(int64_t)hfrep::mlp_affine_ws_floats(dt, B, (int)T, (int)F)}, f32);
+  Tensor slab = at::empty({1, 2}, f32), dx = at::empty_like(fake);
+  hfrep::launch_mlp_critic_dx_affine(dt, fake.data_ptr(), cr, B, (int)T, (int)F, ws.data_ptr<float>(),
+                                     slab.data_ptr<float>(), dx.data_ptr(), cur_stream(fake));
+  return {dx, slab};
+}
+
 // the GP critic update with in-kernel weight gradients (bf16): adds gW1, gW2, gw3 into the given fp32
 // gradient views (bias gradients cancel, as in mlp_wgp_critic) and returns the W-loss slab
 Tensor mlp_wgp_critic_w(Tensor real, Tensor fake, Tensor c, std::vector<Tensor> cp, Tensor gW1, Tensor gW2,
@@ -329,6 +380,10 @@ TORCH_LIBRARY_FRAGMENT(hfrep, m) {
   m.def("mlp_wgp_coef(Tensor gsq, float lam) -> (Tensor, Tensor)");
   m.def("mlp_wgp_critic(Tensor real, Tensor fake, Tensor c, Tensor[] cp) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("mlp_wgpw_supported(int F, int T) -> bool", &mlp_wgpw_supported_op);
+  m.def("mlp_affine_supported(int F, int T) -> bool", &mlp_affine_supported_op);
+  m.def("mlp_wgp_affine(Tensor real, Tensor fake, Tensor[] cp, float lam, Tensor(a!) gW1, Tensor(b!) gW2, "
+        "Tensor(c!) gw3) -> (Tensor, Tensor)");
+  m.def("mlp_critic_dx_affine(Tensor fake, Tensor[] cp) -> (Tensor, Tensor)");
   m.def("mlp_wgp_critic_t(Tensor real, Tensor fake, Tensor c, Tensor[] cp, Tensor(a!) gW1, Tensor(b!) gW2, "
         "Tensor(c!) gw3) -> Tensor");
   m.def("mlp_wgp_critic_w(Tensor real, Tensor fake, Tensor c, Tensor[] cp, Tensor(a!) gW1, Tensor(b!) gW2, "
@@ -347,6 +402,8 @@ TORCH_LIBRARY_IMPL(hfrep, CUDA, m) {
   m.impl("mlp_gen_fwd", &mlp_gen_fwd);
   m.impl("mlp_wgp_critic_w", &mlp_wgp_critic_w);
   m.impl("mlp_wgp_critic_t", &mlp_wgp_critic_t);
+  m.impl("mlp_wgp_affine", &mlp_wgp_affine);
+  m.impl("mlp_critic_dx_affine", &mlp_critic_dx_affine);
   m.impl("mlp_gen_bwd_w", &mlp_gen_bwd_w);
   m.impl("mlp_gan_critic_g", &mlp_gan_critic_g);
   m.impl("mlp_wgp_norm", &mlp_wgp_norm);

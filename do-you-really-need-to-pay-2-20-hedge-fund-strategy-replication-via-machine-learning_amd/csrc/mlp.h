@@ -91,6 +91,16 @@ size_t mlp_wgpt_tsum_floats(int F, int Tn);
 void launch_mlp_wgp_critic_t(int dt, const void* real, const void* fake, const float* c, const MlpCritic& cr,
                              float* tslab, float* tsum, float* slab, int64_t Bn, int Tn, int F, float* gW1, float* gW2,
                              float* gw3, hipStream_t s);
+// The affine critic's update from batch sums (both dtypes; csrc/mlp.hip mlp_wgp_affine_kernel): per-t
+// column sums of real and fake -> one-workgroup fp32 finish; gW1 / gW2 / gw3 accumulate, slab (1 x 2) =
+// the real / fake score sums, e (1) = B (1 - |g|)^2.  ws: mlp_affine_ws_floats floats of scratch.
+// critic_dx_affine: the generator step's dfake (-g_t / B broadcast over the batch) and its score slab.
+bool mlp_affine_supported(int F, int Tn);
+size_t mlp_affine_ws_floats(int dt, int64_t Bn, int Tn, int F);
+void launch_mlp_wgp_affine(int dt, const void* real, const void* fake, const MlpCritic& cr, int64_t Bn, int Tn, int F,
+                           float lam, float* ws, float* slab, float* e, float* gW1, float* gW2, float* gw3, hipStream_t s);
+void launch_mlp_critic_dx_affine(int dt, const void* fake, const MlpCritic& cr, int64_t Bn, int Tn, int F, float* ws,
+                                 float* slab, void* dx, hipStream_t s);
 int mlp_gbw_blocks(int64_t M);
 void launch_mlp_gen_bwd_w(const void* noise, const void* dfake, const MlpGen& g, float* gslab, float* lnslab, int64_t M,
                           int F, hipStream_t s);

@@ -675,6 +675,194 @@ __global__ void __launch_bounds__(256) mlp_wgp_tsum_finish_kernel(const float* _
 }
 
 // ---------------------------------------------------------------------------------------------------
+// The affine critic's update from batch sums (mlp_wgp_affine, default; GAN/WGAN_GP.py:238-253, loop
+// :255-288).  D(x) = sum_t ((x_t W1 + b1) W2 + b2) . w3_t + b3 is affine in x, so
+//   * its input gradient g_t = W1 W2 w3_t is a function of t alone: every sample has the same |g|, the
+//     same GP coefficient c = -(2 lam / B)(1 - |g|) / |g| and the same tangent v_t = c g_t;
+//   * the per-row operands of mlp_wgp_critic_t enter the gradients only through their sums over the
+//     batch, and those are linear in the per-t sums of the inputs (sum_b (x_b W) = (sum_b x_b) W):
+//       S1[t] = d_t / B + B v_t,  d_t = sum_b (fake - real)[b, t]
+//       S2[t] = S1[t] W1                       (= (d_t W1) / B + B v_t W1: b1 cancels in d)
+//       S3[t] = S2[t] W2
+//     and the W-loss score sums are sum_t (s_t W1 + B b1) . (W2 w3_t) + B b2 . w3_t.
+// So the update reads each input once (mlp_bt_colsum: per-t column sums, HBM-bound) and finishes in
+// fp32 in one workgroup; mlp_wgp_tsum_finish forms the T outer products as for mlp_wgp_critic_t.  Same
+// gradient and loss pack as the per-row path up to fp32 summation order (and without its bf16 rounding
+// of h1 / h2 in the bf16 build).  mode 1 is the generator step's critic input gradient: the per-t
+// dfake row -g_t / B (broadcast over the batch by mlp_bcast_rows) and the fake score sum.
+// ---------------------------------------------------------------------------------------------------
+
+// part[p][k][col] = sum over rows r = p, p + P, ... < B of y_k[r][col]; y_0 = x0, y_1 = x1 - x0 (the
+// difference is formed per row: no cancellation between two large sums).  col < C = T F, 16-byte
+// vectors; thread (p, column group) walks its rows with independent loads in flight.
+template <typename T>
+__global__ void __launch_bounds__(256) mlp_bt_colsum_kernel(const T* __restrict__ x0, const T* __restrict__ x1,
+                                                            int64_t B, int C, int P, float* __restrict__ part) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int G = C / V;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (int64_t)G * P) return;
+  const int cg = (int)(gid % G), p = (int)(gid / G);
+  float a0[V], a1[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) a0[j] = a1[j] = 0.f;
+  auto unpack = [](const uint4& u, float* f) {
+    if constexpr (sizeof(T) == 4) {
+      f[0] = __uint_as_float(u.x); f[1] = __uint_as_float(u.y); f[2] = __uint_as_float(u.z); f[3] = __uint_as_float(u.w);
+    } else {
+      const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[2 * j] = __uint_as_float(w4[j] << 16);
+        f[2 * j + 1] = __uint_as_float(w4[j] & 0xFFFF0000u);
+      }
+    }
+  };
+  const int64_t c0 = (int64_t)cg * V;
+#pragma unroll 4
+  for (int64_t r = p; r < B; r += P) {
+    const uint4 u0 = *reinterpret_cast<const uint4*>(x0 + r * C + c0);
+    float f0[V];
+    unpack(u0, f0);
+    if (x1) {
+      const uint4 u1 = *reinterpret_cast<const uint4*>(x1 + r * C + c0);
+      float f1[V];
+      unpack(u1, f1);
+#pragma unroll
+      for (int j = 0; j < V; ++j) a1[j] += f1[j] - f0[j];
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) a0[j] += f0[j];
+  }
+  const int nk = x1 ? 2 : 1;
+  float* o = part + (int64_t)p * nk * C + c0;
+#pragma unroll
+  for (int j = 0; j < V; j += 4) *reinterpret_cast<f32x4*>(o + j) = f32x4{a0[j], a0[j + 1], a0[j + 2], a0[j + 3]};
+  if (x1) {
+#pragma unroll
+    for (int j = 0; j < V; j += 4)
+      *reinterpret_cast<f32x4*>(o + C + j) = f32x4{a1[j], a1[j + 1], a1[j + 2], a1[j + 3]};
+  }
+}
+
+// One workgroup (1024 threads).  sums: [nk][Tn][F] from mlp_bt_colsum (mode 0: k = 0 real, 1 fake - real;
+// mode 1: k = 0 fake).  W1, W2 (row pitch AFP = 101: odd, so the strided reads are bank-conflict free),
+// w3 and the per-t tables live in LDS (mlp_affine_lds_bytes; Tn <= mlp_affine_max_t).  D = the (Tn, H)
+// table W2 w3_t (also written to the D block of tsum in mode 0).  Mode 0 writes tsum's S1 / S2 / S3 rows,
+// slab[0..1] = the real / fake score sums (without b3) and e[0] = B (1 - |g|)^2 (the penalty's sum over
+// samples); mode 1 writes gdx = -g / B and slab = {fake score sum, 0}.
+constexpr int AFP = 101;
+__host__ __device__ constexpr size_t mlp_affine_lds_floats(int F, int H, int Tn) {
+  return (size_t)F * AFP + (size_t)H * AFP + (size_t)Tn * (3 * H + F);
+}
+__global__ void __launch_bounds__(1024) mlp_wgp_affine_kernel(const float* __restrict__ sums, MlpCritic c, int F, int H,
+                                                             int Tn, float Bf, float lam, int mode, float* __restrict__ Dg,
+                                                             float* __restrict__ tsum, float* __restrict__ slab,
+                                                             float* __restrict__ e, float* __restrict__ gdx) {
+  extern __shared__ __attribute__((aligned(16))) float als[];
+  __shared__ float red[16];
+  float* W1 = als;                    // [F][AFP]
+  float* W2 = W1 + F * AFP;           // [H][AFP]
+  float* w3 = W2 + H * AFP;           // [Tn][H]
+  float* D = w3 + Tn * H;             // [Tn][H]
+  float* S2 = D + Tn * H;             // [Tn][H]
+  float* g = S2 + Tn * H;             // [Tn][F]
+  const int tid = threadIdx.x, NT = blockDim.x, L = F + 2 * H;
+  for (int q = tid; q < F * H; q += NT) W1[(q / H) * AFP + q % H] = c.W1[q];
+  for (int q = tid; q < H * H; q += NT) W2[(q / H) * AFP + q % H] = c.W2[q];
+  for (int q = tid; q < Tn * H; q += NT) w3[q] = c.w3[q];
+  __syncthreads();
+  const float* s0 = sums;           // mode 0: real, mode 1: fake
+  const float* sd = sums + Tn * F;  // mode 0: fake - real
+  // (A) D[t][o] = sum_k W2[o][k] w3_t[k]
+  for (int q = tid; q < Tn * H; q += NT) {
+    const int t = q / H, o = q - t * H;
+    float d = 0.f;
+    for (int k = 0; k < H; ++k) d = fmaf(W2[o * AFP + k], w3[t * H + k], d);
+    D[q] = d;
+    if (Dg) Dg[q] = d;
+  }
+  __syncthreads();
+  // (B) g[t][i] = sum_o W1[i][o] D[t][o] and |g|^2
+  float gs = 0.f;
+  for (int q = tid; q < Tn * F; q += NT) {
+    const int t = q / F, i = q - t * F;
+    float a = 0.f;
+    for (int o = 0; o < H; ++o) a = fmaf(W1[i * AFP + o], D[t * H + o], a);
+    g[q] = a;
+    gs = fmaf(a, a, gs);
+    if (mode == 1) gdx[q] = a * (-1.f / Bf);
+  }
+  const float gsq = block_sum<16>(gs, red);  // (barriers inside: g complete)
+  const float n = sqrtf(gsq);
+  const float cc = -(2.f * lam / Bf) * (1.f - n) / fmaxf(n, 1e-30f);
+  // (C) S1, S2 and the score sums
+  float scr = 0.f, scf = 0.f;
+  for (int q = tid; q < Tn * H; q += NT) {
+    const int t = q / H, o = q - t * H;
+    float z = 0.f, dw = 0.f, h0 = 0.f;
+    for (int i = 0; i < F; ++i) {
+      const float wv = W1[i * AFP + o];
+      h0 = fmaf(s0[t * F + i], wv, h0);
+      if (mode == 0) {
+        z = fmaf(g[t * F + i], wv, z);
+        dw = fmaf(sd[t * F + i], wv, dw);
+      }
+    }
+    const float hb = Bf * c.b1[o], tb = Bf * c.b2[o] * w3[q];
+    scr += fmaf(h0 + hb, D[q], tb);
+    if (mode == 0) {
+      const float s2 = dw / Bf + Bf * (cc * z);
+      S2[q] = s2;
+      tsum[t * L + F + o] = s2;
+      scf += fmaf(h0 + dw + hb, D[q], tb);
+    }
+  }
+  if (mode == 0)
+    for (int q = tid; q < Tn * F; q += NT) {
+      const int t = q / F, i = q - t * F;
+      tsum[t * L + i] = sd[q] / Bf + Bf * (cc * g[q]);
+    }
+  const float sr = block_sum<16>(scr, red);  // (barriers inside: S2 complete)
+  const float sf = block_sum<16>(scf, red);
+  if (tid == 0) {
+    slab[0] = sr;
+    slab[1] = mode == 0 ? sf : 0.f;
+    if (mode == 0) e[0] = Bf * (1.f - n) * (1.f - n);
+  }
+  if (mode != 0) return;
+  // (D) S3[t][k] = sum_o S2[t][o] W2[o][k]
+  for (int q = tid; q < Tn * H; q += NT) {
+    const int t = q / H, k = q - t * H;
+    float a = 0.f;
+    for (int o = 0; o < H; ++o) a = fmaf(S2[t * H + o], W2[o * AFP + k], a);
+    tsum[t * L + F + H + k] = a;
+  }
+}
+
+// out[b][col] = row[col] for every b < B (C = T F columns): thread (p, column group) packs its 16 bytes
+// once and stores them to rows p, p + P, ...
+template <typename T>
+__global__ void __launch_bounds__(256) mlp_bcast_rows_kernel(const float* __restrict__ row, int C, int64_t B, int P,
+                                                             T* __restrict__ out) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int G = C / V;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (int64_t)G * P) return;
+  const int cg = (int)(gid % G), p = (int)(gid / G), col = cg * V;
+  uint4 u;
+  if constexpr (sizeof(T) == 4) {
+    u = make_uint4(__float_as_uint(row[col]), __float_as_uint(row[col + 1]), __float_as_uint(row[col + 2]),
+                   __float_as_uint(row[col + 3]));
+  } else {
+    u = make_uint4(pk2bf(row[col], row[col + 1]), pk2bf(row[col + 2], row[col + 3]), pk2bf(row[col + 4], row[col + 5]),
+                   pk2bf(row[col + 6], row[col + 7]));
+  }
+#pragma unroll 4
+  for (int64_t r = p; r < B; r += P) *reinterpret_cast<uint4*>(out + r * C + col) = u;
+}
+
+// ---------------------------------------------------------------------------------------------------
 // The same critic update with the three weight gradients accumulated in the kernel (bf16).
 //
 // mlp_wgp_critic writes 5 per-row operands (872 B a row at F = 36) that linear_wgrad_ reads back:
@@ -1854,6 +2042,81 @@ void launch_mlp_wgp_critic_t(int dt, const void* real, const void* fake, const f
   hipLaunchKernelGGL(mlp_wgp_tsum_prep_kernel, dim3((np + 255) / 256), dim3(256), 0, s, tslab, cr, F, H, Tn, kper, tsum);
   hipLaunchKernelGGL(mlp_wgp_tsum_finish_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, tsum, cr, F, H, Tn, gW1, gW2,
                      gw3);
+}
+
+// ---- the affine critic's update from batch sums (both dtypes) ----
+// the finish kernel keeps W1, W2, w3 and its per-t tables in LDS
+static constexpr int kAffineLdsMax = 160 * 1024 - 1024;
+bool mlp_affine_supported(int F, int Tn) {
+  return mlp_supported(F, 100) && Tn > 0 && (Tn * F) % 8 == 0 &&
+         mlp_affine_lds_floats(F, 100, Tn) * sizeof(float) <= (size_t)kAffineLdsMax;
+}
+
+// row partitions of mlp_bt_colsum: ~512 threads per CU over the C / V column groups
+static int colsum_parts(int dt, int64_t B, int C) {
+  const int V = dt == DT_BF16 ? 8 : 4, G = C / V;
+  const int64_t want = ((int64_t)device_cu_count() * 512 + G - 1) / G;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(B, want));
+}
+size_t mlp_affine_ws_floats(int dt, int64_t Bn, int Tn, int F) {
+  const int H = 100, C = Tn * F;
+  // part | sums | tsum (S rows + D) | g   (mode 1 needs less: part | sums | D | g | gdx)
+  return (size_t)colsum_parts(dt, Bn, C) * 2 * C + 2 * (size_t)C + (size_t)Tn * (F + 3 * H) + (size_t)Tn * F;
+}
+// sums[k][col] = sum_b y_k[b][col] (y_0 = x0, y_1 = x1 - x0), fixed order
+static void bt_colsum(int dt, const void* x0, const void* x1, int64_t B, int C, float* part, float* sums, hipStream_t s) {
+  const int P = colsum_parts(dt, B, C), V = dt == DT_BF16 ? 8 : 4, nk = x1 ? 2 : 1;
+  const int grid = (int)(((int64_t)(C / V) * P + 255) / 256);
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(mlp_bt_colsum_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x0, (const bf16_t*)x1, B,
+                       C, P, part);
+  else
+    hipLaunchKernelGGL(mlp_bt_colsum_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)x0, (const float*)x1, B, C,
+                       P, part);
+  (void)hipMemsetAsync(sums, 0, sizeof(float) * nk * C, s);
+  launch_mlp_slab_sum_cols(part, P, (int64_t)nk * C, 0, nk * C, sums, s);
+}
+
+void launch_mlp_wgp_affine(int dt, const void* real, const void* fake, const MlpCritic& cr, int64_t Bn, int Tn, int F,
+                           float lam, float* ws, float* slab, float* e, float* gW1, float* gW2, float* gw3, hipStream_t s) {
+  if (Bn <= 0) return;
+  const int H = 100, C = Tn * F, L = F + 2 * H;
+  float* part = ws;
+  float* sums = part + (size_t)colsum_parts(dt, Bn, C) * 2 * C;
+  float* tsum = sums + 2 * C;
+  float* g = tsum + (size_t)Tn * (L + H);
+  (void)g;
+  bt_colsum(dt, real, fake, Bn, C, part, sums, s);
+  const size_t lds = mlp_affine_lds_floats(F, H, Tn) * sizeof(float);
+  set_lds(mlp_wgp_affine_kernel, lds);
+  hipLaunchKernelGGL(mlp_wgp_affine_kernel, dim3(1), dim3(1024), lds, s, sums, cr, F, H, Tn, (float)Bn, lam, 0,
+                     tsum + (size_t)Tn * L, tsum, slab, e, (float*)nullptr);
+  const int nf = F * H + H * H + Tn * H;
+  hipLaunchKernelGGL(mlp_wgp_tsum_finish_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, tsum, cr, F, H, Tn, gW1, gW2,
+                     gw3);
+}
+
+void launch_mlp_critic_dx_affine(int dt, const void* fake, const MlpCritic& cr, int64_t Bn, int Tn, int F, float* ws,
+                                 float* slab, void* dx, hipStream_t s) {
+  if (Bn <= 0) return;
+  const int H = 100, C = Tn * F;
+  float* part = ws;
+  float* sums = part + (size_t)colsum_parts(dt, Bn, C) * C;
+  float* D = sums + C;
+  float* g = D + (size_t)Tn * H;
+  float* gdx = g + (size_t)Tn * F;
+  (void)D; (void)g;
+  bt_colsum(dt, fake, nullptr, Bn, C, part, sums, s);
+  const size_t lds = mlp_affine_lds_floats(F, H, Tn) * sizeof(float);
+  set_lds(mlp_wgp_affine_kernel, lds);
+  hipLaunchKernelGGL(mlp_wgp_affine_kernel, dim3(1), dim3(1024), lds, s, sums, cr, F, H, Tn, (float)Bn, 0.f, 1,
+                     (float*)nullptr, (float*)nullptr, slab, (float*)nullptr, gdx);
+  const int P = colsum_parts(dt, Bn, C), V = dt == DT_BF16 ? 8 : 4;
+  const int grid = (int)(((int64_t)(C / V) * P + 255) / 256);
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(mlp_bcast_rows_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, gdx, C, Bn, P, (bf16_t*)dx);
+  else
+    hipLaunchKernelGGL(mlp_bcast_rows_kernel<float>, dim3(grid), dim3(256), 0, s, gdx, C, Bn, P, (float*)dx);
 }
 
 // ---- generator reverse with in-kernel parameter gradients (bf16) ----

@@ -25,7 +25,12 @@ random draws are the engine path's, in its order (real, noise, alpha per critic 
 see the same batches; ``HFREP_MLP_FUSED=0`` selects the engine path (A/B, tests).
 
 For the affine WGAN-GP critic the penalty's input gradient dD/dx_hat does not depend on x_hat, so
-neither x_hat nor D(x_hat) is formed (alpha is still drawn: the RNG stream stays the engine's).
+neither x_hat nor D(x_hat) is formed (alpha is still drawn: the RNG stream stays the engine's).  Going
+one step further (``mlp_wgp_affine``, default): g_t = W1 W2 w3_t depends on t alone, so every sample has
+the same penalty coefficient, and the W terms enter the weight gradients and the losses only through
+per-t sums over the batch (sum_b (x_b W) = (sum_b x_b) W).  A critic update then reads real and fake
+once (per-t column sums) and finishes in fp32 in one workgroup; the generator step's dfake is -g_t / B
+for every row (``mlp_critic_dx_affine``).  ``HFREP_MLP_AFFINE=0`` keeps the per-row kernels above.
 """
 from __future__ import annotations
 
@@ -102,6 +107,9 @@ class FusedMLP:
         self.wgrad_inkernel = (inkernel and self.head == 0 and os.environ.get("HFREP_MLP_WGRAD_TSUM", "1") == "0"
                                and bool(_ops().mlp_wgpw_supported(int(cfg.features), int(cfg.window))))
         self.wgrad_tsum = self.head == 0 and on and not self.wgrad_inkernel
+        # affine critic: the update from per-t batch sums (mlp_wgp_affine / mlp_critic_dx_affine)
+        self.affine = (self.head == 0 and os.environ.get("HFREP_MLP_AFFINE", "1") != "0"
+                       and bool(_ops().mlp_affine_supported(int(cfg.features), int(cfg.window))))
         self.gen_wgrad_inkernel = inkernel
         # GAN discriminator: rank-1 adjoints per row -> gradients as dz-weighted column sums in the
         # kernel (mlp_gan_critic_g, both dtypes); HFREP_MLP_WGRAD_INKERNEL=0 keeps the operand path
@@ -133,7 +141,10 @@ class FusedMLP:
         tr, ops = self.tr, _ops()
         B = noise.shape[0]
         if self.head == 0:
-            dfake, slab = ops.mlp_critic_dx(fake, self.cw, 0, -1.0)
+            if self.affine:
+                dfake, slab = ops.mlp_critic_dx_affine(fake, self.cw)
+            else:
+                dfake, slab = ops.mlp_critic_dx(fake, self.cw, 0, -1.0)
             loss = ops.mlp_finish(slab, None, 1, 1.0 / B, self.cw[5], 0.0)
         else:
             dfake, slab = ops.mlp_critic_dx(fake, self.cw, 1, 1.0)
@@ -153,6 +164,10 @@ class FusedMLP:
     def _wgp_critic_grads(self, real, fake):
         tr, ops = self.tr, _ops()
         B, T = real.shape[0], real.shape[1]
+        if self.affine:
+            gW1, _gb1, gW2, _gb2, gw3, _gb3 = self.cg
+            slab, e = ops.mlp_wgp_affine(real, fake, self.cw, float(tr.gp_weight), gW1, gW2, gw3)
+            return ops.mlp_finish(slab, e, 0, 1.0 / B, self.cw[5], float(tr.gp_weight))
         gsq = ops.mlp_wgp_norm(real, self.cw)
         c, e = ops.mlp_wgp_coef(gsq, float(tr.gp_weight))
         gW1, _gb1, gW2, _gb2, gw3, _gb3 = self.cg

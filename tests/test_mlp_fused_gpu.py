@@ -167,6 +167,7 @@ def test_mlp_wgp_inkernel_wgrad_matches_operand_path(cuda, B, T, F):
     tg, _ = _pair(cuda, "wgan_gp", "bfloat16", B, T, F)
     fz, dt = tg._fused, tg.dtype
     assert fz.wgrad_tsum and not fz.wgrad_inkernel  # the t-major kernel is the default
+    fz.affine = False  # the per-row kernels under test
     real, noise, _ = _inputs(B, T, F, seed=5)
     grads, packs = [], []
     with torch.no_grad():
@@ -250,6 +251,7 @@ def test_mlp_wgp_tsum_matches_operand_path(cuda, dtype, B, T, F):
     two runs bitwise identical."""
     tg, tc = _pair(cuda, "wgan_gp", dtype, B, T, F)
     fz, dt = tg._fused, tg.dtype
+    fz.affine = False  # the per-row kernels under test
     real, noise, alpha = _inputs(B, T, F, seed=7)
     packs, grads = [], []
     with torch.no_grad():
@@ -267,3 +269,48 @@ def test_mlp_wgp_tsum_matches_operand_path(cuda, dtype, B, T, F):
     rel = _rel(grads[0], grads[2])
     assert rel < (1e-5 if dtype == "float32" else 3e-3), f"per-t sums vs operand path rel {rel:.2e}"
     assert rel_c < TOL[dtype], f"vs fp64 rel {rel_c:.2e}"
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("B,T,F", [(37, 24, 32), (300, 40, 32), (45, 48, 36), (6000, 24, 32), (40000, 24, 32)])
+def test_mlp_wgp_affine_matches_per_row_path(cuda, dtype, B, T, F):
+    """Config 4, the default critic path: the affine critic's update from per-t batch sums
+    (mlp_wgp_affine: column sums of real and fake-real, one-workgroup fp32 finish) and the generator
+    step's broadcast dfake (mlp_critic_dx_affine) vs the per-row kernels (mlp_wgp_critic_t /
+    mlp_critic_dx) on the same batch and vs the fp64 engine: gradient, loss pack, dfake and the
+    generator loss; two runs bitwise identical.  fp32: summation order only; bf16: the per-row kernels
+    also round h1 / h2 to bf16 (the sums path does not), so vs the fp64 engine at the bf16 tolerance."""
+    ops = torch.ops.hfrep
+    tg, tc = _pair(cuda, "wgan_gp", dtype, B, T, F)
+    fz, dt = tg._fused, tg.dtype
+    assert fz.affine and ops.mlp_affine_supported(F, T) and not ops.mlp_affine_supported(36, 7)
+    real, noise, alpha = _inputs(B, T, F, seed=13)
+    packs, grads = [], []
+    with torch.no_grad():
+        fake = ops.mlp_gen_fwd(noise.to(cuda, dt), fz.gw)
+        r = real.to(cuda, dt)
+        for affine in (True, True, False):
+            fz.affine = affine
+            tg.critic.zero_grad()
+            packs.append(fz._wgp_critic_grads(r, fake).clone())
+            grads.append(tg.critic.flat.grad.clone())
+        pack_c = tc.critic_gp_grads(real.double(), fake.double().cpu(), alpha.double())
+        gd_a, sl_a = ops.mlp_critic_dx_affine(fake, fz.cw)
+        gd_b, sl_b = ops.mlp_critic_dx_affine(fake, fz.cw)
+        gd_r, sl_r = ops.mlp_critic_dx(fake, fz.cw, 0, -1.0)
+        la = ops.mlp_finish(sl_a, None, 1, 1.0 / B, fz.cw[5], 0.0)[0]
+        lr = ops.mlp_finish(sl_r, None, 1, 1.0 / B, fz.cw[5], 0.0)[0]
+        fz.affine = True
+    assert torch.equal(grads[0], grads[1]) and torch.equal(packs[0], packs[1])
+    assert torch.equal(gd_a, gd_b) and torch.equal(sl_a, sl_b)
+    rel_c = _rel(grads[0], tc.critic.flat.grad)
+    assert rel_c < TOL[dtype], f"vs fp64 rel {rel_c:.2e}"
+    rel = _rel(grads[0], grads[2])
+    assert rel < (2e-5 if dtype == "float32" else TOL[dtype]), f"sums vs per-row path rel {rel:.2e}"
+    lt = 1e-5 if dtype == "float32" else 2e-2
+    for a, b, c in zip(packs[0].cpu().tolist(), packs[2].cpu().tolist(), pack_c.tolist()):
+        assert abs(a - b) <= lt * max(1.0, abs(b)) and abs(a - c) <= 10 * lt * max(1.0, abs(c)), (packs, pack_c)
+    # dfake: the same per-t row for every sample; the per-row kernel's value to its rounding
+    assert torch.equal(gd_a, gd_a[:1].expand_as(gd_a))
+    assert _rel(gd_a, gd_r) < (1e-5 if dtype == "float32" else 2e-2)
+    assert abs(la.item() - lr.item()) <= lt * max(1.0, abs(lr.item()))
