@@ -15,6 +15,7 @@
 #include "common.h"
 #include "mfma.h"
 #include "kernels.h"
+#include "mlp.h"
 
 namespace hfrep {
 
@@ -170,6 +171,152 @@ wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ gW, floa
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32 weight gradient on the bf16 matrix pipe for the narrow layers (K + 1 <= 128, N <= 128: the MLP
+// generator's / discriminator's Dense layers, GAN/GAN.py:127-158, GAN/WGAN_GP.py:221-253).
+// wgrad_kernel<float> above tiles the output 64 x 64 (each X / D element is read once per opposite
+// tile), stages with one scalar load + div / mod per element and runs the exact fp32 MFMA
+// (v_mfma_f32_32x32x2_f32: 1/16 of the bf16 rate): 2.8 ms per (6.3 M x 100)^T (6.3 M x 100).  Here one
+// workgroup owns the whole output and walks 32-row chunks of its row range once: each chunk of X and D
+// is loaded with coalesced dword loads (lanes over features, 8 rows per task), split exactly into three
+// bf16 planes (hi / mid / lo: 8 mantissa bits each) and stored TRANSPOSED in LDS ([feature][row], 16-byte
+// writes); the 6 plane products with terms >= 2^-24 (hh, hm, mh, hl, lh, mm) run on
+// v_mfma_f32_32x32x16_bf16 -- the LSTM fp32 kernels' split (lstm_f32.hip split3), error within 2x the exact
+// kernel's vs fp64.  The next chunk's loads are issued before the current chunk's MFMAs.  Row K of the X
+// image is the ones row (bias gradient).  Slab rows per workgroup, fixed-order reduce (mlp_slab_sum).
+// ---------------------------------------------------------------------------------------------
+constexpr int WSR = 32;        // rows per chunk
+constexpr int WSQ = WSR + 8;   // image row pitch (bf16): 80 bytes
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& mi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v[j]), h = u & 0xffff0000u;
+    const float r1 = v[j] - __builtin_bit_cast(float, h);
+    const uint32_t m = __builtin_bit_cast(uint32_t, r1) & 0xffff0000u;
+    const float r2 = r1 - __builtin_bit_cast(float, m);
+    hi[j] = (short)(h >> 16);
+    mi[j] = (short)(m >> 16);
+    lo[j] = (short)(__builtin_bit_cast(uint32_t, r2) >> 16);
+  }
+}
+
+template <int NI, int NJ>
+__global__ void __launch_bounds__(256)
+wgrad_f32s_kernel(const float* __restrict__ X, const float* __restrict__ D, float* __restrict__ slab, int M, int K,
+                  int N, int rows_per_split) {
+  constexpr int PX = NI * 32 * WSQ, PD = NJ * 32 * WSQ;  // plane sizes (bf16)
+  constexpr int TX = (NI + 1) / 2, TD = (NJ + 1) / 2;    // (feature, 8-row group) tasks per thread
+  constexpr int TPW = (NI * NJ + 3) / 4;                 // output tiles per wave
+  __shared__ __attribute__((aligned(16))) bf16_t img[3 * PX + 3 * PD];
+  bf16_t* ix = img;
+  bf16_t* id = img + 3 * PX;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, cl = lane & 31;
+  const int mb = blockIdx.x * rows_per_split, me = min(M, mb + rows_per_split);
+  for (int e = tid; e < (3 * PX + 3 * PD) / 8; e += 256) reinterpret_cast<bf16x8*>(img)[e] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  __syncthreads();
+  if (tid < WSR) ix[K * WSQ + tid] = (bf16_t)0x3F80;  // ones row (hi plane): the bias gradient
+  f32x16 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acc[t] = zero16();
+  float vx[TX][8], vd[TD][8];
+  auto load = [&](int m0) {
+#pragma unroll
+    for (int q = 0; q < TX; ++q) {
+      const int e = tid + 256 * q, i = e % K, rg = e / K;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = m0 + 8 * rg + j;
+        vx[q][j] = (rg < 4 && r < me) ? X[(size_t)r * K + i] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < TD; ++q) {
+      const int e = tid + 256 * q, j0 = e % N, rg = e / N;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = m0 + 8 * rg + j;
+        vd[q][j] = (rg < 4 && r < me) ? D[(size_t)r * N + j0] : 0.f;
+      }
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int q = 0; q < TX; ++q) {
+      const int e = tid + 256 * q, i = e % K, rg = e / K;
+      if (rg < 4) {
+        bf16x8 a, b, c;
+        split8(vx[q], a, b, c);
+        const int o = i * WSQ + 8 * rg;
+        *reinterpret_cast<bf16x8*>(ix + o) = a;
+        *reinterpret_cast<bf16x8*>(ix + PX + o) = b;
+        *reinterpret_cast<bf16x8*>(ix + 2 * PX + o) = c;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < TD; ++q) {
+      const int e = tid + 256 * q, j0 = e % N, rg = e / N;
+      if (rg < 4) {
+        bf16x8 a, b, c;
+        split8(vd[q], a, b, c);
+        const int o = j0 * WSQ + 8 * rg;
+        *reinterpret_cast<bf16x8*>(id + o) = a;
+        *reinterpret_cast<bf16x8*>(id + PD + o) = b;
+        *reinterpret_cast<bf16x8*>(id + 2 * PD + o) = c;
+      }
+    }
+  };
+  load(mb);
+  for (int m0 = mb; m0 < me; m0 += WSR) {
+    stage();
+    __syncthreads();
+    load(m0 + WSR);  // the next chunk's loads fly during the MFMAs (past me: zeros, no access)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int tile = w + 4 * t;
+      if (tile < NI * NJ) {
+        const int ti = tile / NJ, tj = tile - ti * NJ;
+#pragma unroll
+        for (int ks = 0; ks < WSR / 16; ++ks) {
+          const int ao = (32 * ti + cl) * WSQ + 16 * ks + 8 * h, bo = (32 * tj + cl) * WSQ + 16 * ks + 8 * h;
+          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(ix + ao);
+          const bf16x8 am = *reinterpret_cast<const bf16x8*>(ix + PX + ao);
+          const bf16x8 al = *reinterpret_cast<const bf16x8*>(ix + 2 * PX + ao);
+          const bf16x8 bh = *reinterpret_cast<const bf16x8*>(id + bo);
+          const bf16x8 bm = *reinterpret_cast<const bf16x8*>(id + PD + bo);
+          const bf16x8 bl = *reinterpret_cast<const bf16x8*>(id + 2 * PD + bo);
+          acc[t] = MF<bf16_t>::mma(am, bm, acc[t]);
+          acc[t] = MF<bf16_t>::mma(al, bh, acc[t]);
+          acc[t] = MF<bf16_t>::mma(ah, bl, acc[t]);
+          acc[t] = MF<bf16_t>::mma(am, bh, acc[t]);
+          acc[t] = MF<bf16_t>::mma(ah, bm, acc[t]);
+          acc[t] = MF<bf16_t>::mma(ah, bh, acc[t]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int Kr = K + 1;
+  float* out = slab + (size_t)blockIdx.x * Kr * N;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int tile = w + 4 * t;
+    if (tile < NI * NJ) {
+      const int ti = tile / NJ, tj = tile - ti * NJ, col = 32 * tj + cl;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * ti + acc32_row(r, lane);
+        if (row < Kr && col < N) out[(size_t)row * N + col] = acc[t][r];
+      }
+    }
+  }
+}
+
+static bool wgrad_f32s_ok(int K, int N) { return K >= 1 && K + 1 <= 128 && N >= 1 && N <= 128; }
+static int wgrad_f32s_splits(int M) {
+  const int want = (M + 1023) / 1024;  // >= 32 chunks per workgroup
+  return std::max(1, std::min(want, device_cu_count() * 2));
+}
+
 static int wgrad_splits(int M, int K, int N) {
   const int Kr = K + 1;
   const int tiles = ((Kr + WBI - 1) / WBI) * ((N + WBJ - 1) / WBJ);
@@ -180,7 +327,8 @@ static int wgrad_splits(int M, int K, int N) {
 }
 
 size_t wgrad_workspace_floats(int M, int K, int N) {
-  return (size_t)wgrad_splits(M, K, N) * (size_t)(K + 1) * (size_t)N;
+  const int splits = std::max(wgrad_splits(M, K, N), wgrad_f32s_ok(K, N) ? wgrad_f32s_splits(M) : 1);
+  return (size_t)splits * (size_t)(K + 1) * (size_t)N;
 }
 
 void launch_linear(int dt, const void* A, const float* W, const float* bias, void* C, int M, int N, int K,
@@ -274,6 +422,37 @@ void launch_wgrad(int dt, const void* X, const void* D, float* gW, float* gb, in
                        gb != nullptr ? 1 : 0, rps);
     const int blocks = (int)std::min<int64_t>(((int64_t)(K + 1) * N + 255) / 256, 1024);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, gW, gb, z, K, N, gb != nullptr ? 1 : 0);
+    return;
+  }
+  if (dt == DT_F32 && shiftT == 0 && wgrad_f32s_ok(K, N)) {
+    const int P = wgrad_f32s_splits(M);
+    const int rps = ((M + P - 1) / P + WSR - 1) / WSR * WSR;
+    const int z = (M + rps - 1) / rps;
+    const int ni = (K + 1 + 31) / 32, nj = (N + 31) / 32;
+    auto go = [&](auto k) {
+      hipLaunchKernelGGL(k, dim3(z), dim3(256), 0, s, (const float*)X, (const float*)D, ws, M, K, N, rps);
+    };
+    switch (ni * 4 + nj) {
+      case 1 * 4 + 1: go(wgrad_f32s_kernel<1, 1>); break;
+      case 1 * 4 + 2: go(wgrad_f32s_kernel<1, 2>); break;
+      case 1 * 4 + 3: go(wgrad_f32s_kernel<1, 3>); break;
+      case 1 * 4 + 4: go(wgrad_f32s_kernel<1, 4>); break;
+      case 2 * 4 + 1: go(wgrad_f32s_kernel<2, 1>); break;
+      case 2 * 4 + 2: go(wgrad_f32s_kernel<2, 2>); break;
+      case 2 * 4 + 3: go(wgrad_f32s_kernel<2, 3>); break;
+      case 2 * 4 + 4: go(wgrad_f32s_kernel<2, 4>); break;
+      case 3 * 4 + 1: go(wgrad_f32s_kernel<3, 1>); break;
+      case 3 * 4 + 2: go(wgrad_f32s_kernel<3, 2>); break;
+      case 3 * 4 + 3: go(wgrad_f32s_kernel<3, 3>); break;
+      case 3 * 4 + 4: go(wgrad_f32s_kernel<3, 4>); break;
+      case 4 * 4 + 1: go(wgrad_f32s_kernel<4, 1>); break;
+      case 4 * 4 + 2: go(wgrad_f32s_kernel<4, 2>); break;
+      case 4 * 4 + 3: go(wgrad_f32s_kernel<4, 3>); break;
+      default: go(wgrad_f32s_kernel<4, 4>); break;
+    }
+    const int64_t stride = (int64_t)(K + 1) * N;
+    launch_mlp_slab_sum_cols(ws, z, stride, 0, K * N, gW, s);
+    if (gb) launch_mlp_slab_sum_cols(ws, z, stride, K * N, N, gb, s);
     return;
   }
   const int has_bias = gb != nullptr;
