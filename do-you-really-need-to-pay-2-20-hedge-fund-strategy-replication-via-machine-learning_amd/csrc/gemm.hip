@@ -311,7 +311,16 @@ wgrad_f32s_kernel(const float* __restrict__ X, const float* __restrict__ D, floa
   }
 }
 
-static bool wgrad_f32s_ok(int K, int N) { return K >= 1 && K + 1 <= 128 && N >= 1 && N <= 128; }
+bool fp32_exact_mode() {
+  static const bool v = [] {
+    const char* e = getenv("HFREP_FP32_EXACT");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+static bool wgrad_f32s_ok(int K, int N) {
+  return !fp32_exact_mode() && K >= 1 && K + 1 <= 128 && N >= 1 && N <= 128;
+}
 static int wgrad_f32s_splits(int M) {
   const int want = (M + 1023) / 1024;  // >= 32 chunks per workgroup
   return std::max(1, std::min(want, device_cu_count() * 2));

@@ -106,6 +106,8 @@ void launch_linear(int dt, const void* A, const float* W, const float* bias, voi
 // gW[K,N] += sum_m X[m,:]^T D[m,:]  (and gb[N] += sum_m D[m,:] when gb != nullptr).
 // shiftT > 0: X row m is replaced by row m-1, and by zeros where m % shiftT == 0 (h_{t-1} trick).
 // Uses split-M fp32 slabs in `ws` (size >= wgrad_workspace_floats) and a reduce launch.
+// HFREP_FP32_EXACT=1: fp32 products on the exact-fp32 MFMA instead of the three-term bf16 split
+bool fp32_exact_mode();
 size_t wgrad_workspace_floats(int M, int K, int N);
 void launch_wgrad(int dt, const void* X, const void* D, float* gW, float* gb, int M, int K, int N, int shiftT,
                   float* ws, hipStream_t s);

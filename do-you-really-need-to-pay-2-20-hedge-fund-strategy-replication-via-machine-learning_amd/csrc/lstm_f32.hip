@@ -2568,11 +2568,7 @@ constexpr size_t fwds_smem() {
 // fp32 accumulation; error <= 2x the exact kernel's vs fp64, tests/test_kernels_gpu.py).
 // HFREP_FP32_EXACT=1: every product on the exact-fp32 MFMA (v_mfma_f32_16x16x4_f32, an fmaf chain).
 static bool fp32_exact() {
-  static const bool v = [] {
-    const char* e = getenv("HFREP_FP32_EXACT");
-    return e && atoi(e) == 1;
-  }();
-  return v;
+  return fp32_exact_mode();
 }
 // forward: 1 exact, 2 the split-recurrent forward for the K <= 36 layers (lstmf_fwds_kernel)
 static std::atomic<int>& fwdf_impl() {

@@ -36,6 +36,41 @@
 
 namespace hfrep {
 
+// fp32 storage with the products on the bf16 matrix pipe: every operand as three exact bf16 planes
+// (hi / mid / lo by truncation, 8 mantissa bits each) and 6 of the 9 plane products (the dropped ones
+// are < 2^-24 of the product) on v_mfma_f32_32x32x16_bf16 -- the LSTM fp32 kernels' split (lstm_f32.hip
+// split3; error within 2x the exact kernel's vs fp64).  Policy tag f32s_t: k-step geometry of bf16.
+struct f32s_t {};
+struct F3 {
+  bf16x8 h, m, l;
+};
+template <> struct MF<f32s_t> {
+  typedef F3 frag;
+  // small terms first: the fp32 accumulator rounds them before the large ones arrive
+  __device__ __forceinline__ static f32x16 mma(const frag& a, const frag& b, f32x16 c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, c, 0, 0, 0);
+  }
+};
+__device__ __forceinline__ F3 split_f3(const float (&v)[8]) {
+  F3 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v[j]), hb = u & 0xffff0000u;
+    const float r1 = v[j] - __builtin_bit_cast(float, hb);
+    const uint32_t mb = __builtin_bit_cast(uint32_t, r1) & 0xffff0000u;
+    const float r2 = r1 - __builtin_bit_cast(float, mb);
+    f.h[j] = (short)(hb >> 16);
+    f.m[j] = (short)(mb >> 16);
+    f.l[j] = (short)(__builtin_bit_cast(uint32_t, r2) >> 16);
+  }
+  return f;
+}
+
 namespace {
 
 constexpr int MLP_WAVES = 4;  // waves per workgroup (one per SIMD; up to 512 registers per wave)
@@ -84,6 +119,24 @@ template <> struct MP<float> {
   __device__ __forceinline__ static int feat(int s, int /*e*/, int h) { return 32 * (s >> 4) + featq(s & 15, h); }
   __device__ __forceinline__ static frag bop(const f32x16* a, int s) { return a[s >> 4][s & 15]; }
   template <class G> __device__ __forceinline__ static frag make(G get) { return get(0); }
+};
+
+template <> struct MP<f32s_t> {
+  typedef F3 frag;
+  static constexpr int steps(int K) { return (K + 15) / 16; }
+  __device__ __forceinline__ static int feat(int s, int e, int h) { return MP<bf16_t>::feat(s, e, h); }
+  __device__ __forceinline__ static frag bop(const f32x16* a, int s) {
+    const f32x16& t = a[s >> 1];
+    const int o = 8 * (s & 1);
+    const float v[8] = {t[o], t[o + 1], t[o + 2], t[o + 3], t[o + 4], t[o + 5], t[o + 6], t[o + 7]};
+    return split_f3(v);
+  }
+  template <class G> __device__ __forceinline__ static frag make(G get) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = get(j);
+    return split_f3(v);
+  }
 };
 
 // ---------------------------------------------------------------------------------------------------
@@ -363,19 +416,20 @@ __device__ __forceinline__ void bce(float p, float y, float inv, float& lo, floa
 // ===================================================================================================
 // generator forward: noise -> fake (GAN/WGAN_GP.py:221-236 build_generator)
 // ===================================================================================================
-template <typename T, int F, int H>
+// P: the product policy (T, or f32s_t for fp32 storage on the split bf16 path)
+template <typename T, int F, int H, typename P = T>
 __global__ void __launch_bounds__(MLP_THREADS) mlp_gen_fwd_kernel(const T* __restrict__ z, MlpGen g,
                                                                   T* __restrict__ out, int64_t M) {
-  using Fr = typename MP<T>::frag;
+  using Fr = typename MP<P>::frag;
   constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   Fr* i1 = reinterpret_cast<Fr*>(lds);
-  Fr* i2 = i1 + fwd_entries<T, F, H>() * 64;
-  Fr* i3 = i2 + fwd_entries<T, H, H>() * 64;
-  float* vec = reinterpret_cast<float*>(i3 + fwd_entries<T, H, F>() * 64);
-  build_fwd<T, F, H>(i1, g.W1);
-  build_fwd<T, H, H>(i2, g.W2);
-  build_fwd<T, H, F>(i3, g.W3);
+  Fr* i2 = i1 + fwd_entries<P, F, H>() * 64;
+  Fr* i3 = i2 + fwd_entries<P, H, H>() * 64;
+  float* vec = reinterpret_cast<float*>(i3 + fwd_entries<P, H, F>() * 64);
+  build_fwd<P, F, H>(i1, g.W1);
+  build_fwd<P, H, H>(i2, g.W2);
+  build_fwd<P, H, F>(i3, g.W3);
   load_vec(vec + 0 * VEC, g.b1, H); load_vec(vec + 1 * VEC, g.g1, H); load_vec(vec + 2 * VEC, g.be1, H);
   load_vec(vec + 3 * VEC, g.b2, H); load_vec(vec + 4 * VEC, g.g2, H); load_vec(vec + 5 * VEC, g.be2, H);
   load_vec(vec + 6 * VEC, g.b3, F);
@@ -385,13 +439,13 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_gen_fwd_kernel(const T* __res
     f32x16 x[NTF], a[NTH], b[NTH];
     float mean, rstd;
     load_rows<T, F>(x, z, row, M, h);
-    dense<T, F, H>(x, a, i1, lane);
+    dense<P, F, H>(x, a, i1, lane);
     bias_act<H>(a, vec + 0 * VEC, ACT_SIGMOID, h);
     lrelu_ln<H>(a, vec + 1 * VEC, vec + 2 * VEC, h, mean, rstd);
-    dense<T, H, H>(a, b, i2, lane);
+    dense<P, H, H>(a, b, i2, lane);
     bias_act<H>(b, vec + 3 * VEC, ACT_SIGMOID, h);
     lrelu_ln<H>(b, vec + 4 * VEC, vec + 5 * VEC, h, mean, rstd);
-    dense<T, H, F>(b, x, i3, lane);
+    dense<P, H, F>(b, x, i3, lane);
     bias_act<F>(x, vec + 6 * VEC, ACT_LINEAR, h);
     store_rows<T, F>(out, row, M, x, h);
   }
@@ -1882,6 +1936,15 @@ int mlp_slab_rows(int64_t M) {
 void launch_mlp_gen_fwd(int dt, const void* noise, const MlpGen& g, void* out, int64_t M, int F, int H,
                         hipStream_t s) {
   if (M <= 0) return;
+  // fp32 at F = 32: the split bf16 products (the three weight planes fit LDS: 136 KB; F = 36 needs 166)
+  if (dt == DT_F32 && F == 32 && !fp32_exact_mode()) {
+    auto k = mlp_gen_fwd_kernel<float, 32, 100, f32s_t>;
+    constexpr size_t lds = lds_gen_fwd<f32s_t, 32, 100>();
+    static_assert(lds <= 160 * 1024, "split generator images exceed LDS");
+    set_lds(k, lds);
+    hipLaunchKernelGGL(k, dim3(mlp_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, (const float*)noise, g, (float*)out, M);
+    return;
+  }
   MLP_DISPATCH(dt, F, {
     auto k = mlp_gen_fwd_kernel<T, FF, 100>;
     constexpr size_t lds = lds_gen_fwd<T, FF, 100>();
