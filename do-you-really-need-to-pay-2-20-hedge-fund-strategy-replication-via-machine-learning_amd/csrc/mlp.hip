@@ -1384,18 +1384,18 @@ __device__ __forceinline__ void ln_reverse(const f32x16* g, const f32x16* y, f32
 // wave: [s1 F | s2 H | s3 H | S]); mlp_gan_grad_finish reduces the slab in a fixed order and forms
 // the outer products.  The per-row forward and BCE are the same as mlp_gan_critic's.
 // ---------------------------------------------------------------------------------------------------
-template <typename T, int F, int H>
+template <typename T, int F, int H, typename P = T>  // P: product policy (f32s_t: fp32 on split bf16)
 __global__ void __launch_bounds__(MLP_THREADS) mlp_gan_critic_g_kernel(const T* __restrict__ x, MlpCritic c, float label,
                                                                        float* __restrict__ gslab,
                                                                        float* __restrict__ slab, int64_t M, float inv) {
-  using Fr = typename MP<T>::frag;
+  using Fr = typename MP<P>::frag;
   constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   Fr* f1 = reinterpret_cast<Fr*>(lds);
-  Fr* f2 = f1 + fwd_entries<T, F, H>() * 64;
-  float* vec = reinterpret_cast<float*>(f2 + fwd_entries<T, H, H>() * 64);
-  build_fwd<T, F, H>(f1, c.W1);
-  build_fwd<T, H, H>(f2, c.W2);
+  Fr* f2 = f1 + fwd_entries<P, F, H>() * 64;
+  float* vec = reinterpret_cast<float*>(f2 + fwd_entries<P, H, H>() * 64);
+  build_fwd<P, F, H>(f1, c.W1);
+  build_fwd<P, H, H>(f2, c.W2);
   load_vec(vec, c.b1, H);
   load_vec(vec + VEC, c.b2, H);
   load_vec(vec + 2 * VEC, c.w3, H);
@@ -1412,9 +1412,9 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_gan_critic_g_kernel(const T* 
     const bool ok = row < M;
     f32x16 A[NTH], Bv[NTH], X[NTF];
     load_rows<T, F>(X, x, row, M, h);
-    dense<T, F, H>(X, A, f1, lane);
+    dense<P, F, H>(X, A, f1, lane);
     bias_act<H>(A, vec, ACT_LINEAR, h);         // h1
-    dense<T, H, H>(A, Bv, f2, lane);
+    dense<P, H, H>(A, Bv, f2, lane);
     bias_act<H>(Bv, vec + VEC, ACT_LINEAR, h);  // h2
     const float p = sigmoidf_(rowdot<H>(Bv, vec + 2 * VEC, true, h) + b3);
     float lo, gp;
@@ -2067,6 +2067,18 @@ void launch_mlp_slab_sum_cols(const float* slab, int P, int64_t stride, int col0
 void launch_mlp_gan_critic_g(int dt, const void* x, const MlpCritic& cr, float label, float* gslab, float* slab,
                              int64_t M, int F, hipStream_t s) {
   if (M <= 0) return;
+  if (dt == DT_F32 && !fp32_exact_mode()) {  // fp32 on the split bf16 products (images: 108 / 117 KB)
+    MLP_DISPATCH(dt, F, {
+      auto k = mlp_gan_critic_g_kernel<float, FF, 100, f32s_t>;
+      constexpr size_t lds =
+          (size_t)(fwd_entries<f32s_t, FF, 100>() + fwd_entries<f32s_t, 100, 100>()) * frag_bytes<f32s_t>() + 3 * VEC * 4;
+      static_assert(lds <= 160 * 1024, "split discriminator images exceed LDS");
+      set_lds(k, lds);
+      hipLaunchKernelGGL(k, dim3(slab_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, (const float*)x, cr, label, gslab,
+                         slab, M, 1.f / (float)M);
+    });
+    return;
+  }
   MLP_DISPATCH(dt, F, {
     auto k = mlp_gan_critic_g_kernel<T, FF, 100>;
     constexpr size_t lds = (size_t)(fwd_entries<T, FF, 100>() + fwd_entries<T, 100, 100>()) * frag_bytes<T>() +
