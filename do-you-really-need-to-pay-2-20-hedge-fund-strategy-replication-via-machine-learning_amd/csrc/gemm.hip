@@ -190,8 +190,9 @@ constexpr int WSQ = WSR + 8;   // image row pitch (bf16): 80 bytes
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& mi, bf16x8& lo) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const uint32_t u = __builtin_bit_cast(uint32_t, v[j]), h = u & 0xffff0000u;
-    const float r1 = v[j] - __builtin_bit_cast(float, h);
+    const float a = v[j];  // (a scalar copy first: tests/test_isa_hazards.py bit_cast lint)
+    const uint32_t u = __builtin_bit_cast(uint32_t, a), h = u & 0xffff0000u;
+    const float r1 = a - __builtin_bit_cast(float, h);
     const uint32_t m = __builtin_bit_cast(uint32_t, r1) & 0xffff0000u;
     const float r2 = r1 - __builtin_bit_cast(float, m);
     hi[j] = (short)(h >> 16);
@@ -293,6 +294,13 @@ wgrad_f32s_kernel(const float* __restrict__ X, const float* __restrict__ D, floa
         }
       }
     }
+    // The accumulators are read after the loop, behind the wave-uniform tile branch and the loop exit,
+    // where LLVM's hazard recognizer does not count the XDL write -> read wait states
+    // (tests/test_isa_hazards.py found 11 of 12): 16 explicit ones after each chunk's MFMAs (16 cycles
+    // against ~1.5k of MFMA per chunk), which no MFMA may pass
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   }
   const int Kr = K + 1;

@@ -60,8 +60,9 @@ __device__ __forceinline__ F3 split_f3(const float (&v)[8]) {
   F3 f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const uint32_t u = __builtin_bit_cast(uint32_t, v[j]), hb = u & 0xffff0000u;
-    const float r1 = v[j] - __builtin_bit_cast(float, hb);
+    const float a = v[j];  // (a scalar copy first: tests/test_isa_hazards.py bit_cast lint)
+    const uint32_t u = __builtin_bit_cast(uint32_t, a), hb = u & 0xffff0000u;
+    const float r1 = a - __builtin_bit_cast(float, hb);
     const uint32_t mb = __builtin_bit_cast(uint32_t, r1) & 0xffff0000u;
     const float r2 = r1 - __builtin_bit_cast(float, mb);
     f.h[j] = (short)(hb >> 16);
