@@ -1264,6 +1264,71 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_critic_dx_kernel(const T* __r
   slab_put(slab, 2, 1, 0.f);
 }
 
+// The generator step's input gradient through the GAN discriminator (head 1), rank-1 form: the hidden
+// layers are linear (Dense -> Dense -> Dense(1, sigmoid); _critic_lists checks it), so every row's
+// adjoint is dx = dz_row g with ONE vector g = W1 W2 w3 -- computed once per workgroup in the prologue
+// instead of two dgrad MFMA passes per row (mlp_critic_dx_kernel<HEAD = 1>).  No dgrad images: the
+// forward images alone leave LDS room for fp32 on the split bf16 products (P = f32s_t).
+template <typename T, int F, int H, typename P = T>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_gan_dx_kernel(const T* __restrict__ x, MlpCritic c, float label,
+                                                                 T* __restrict__ dx, float* __restrict__ slab, int64_t M,
+                                                                 float inv) {
+  using Fr = typename MP<P>::frag;
+  constexpr int NTH = (H + 31) / 32, NTF = (F + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  Fr* f1 = reinterpret_cast<Fr*>(lds);
+  Fr* f2 = f1 + fwd_entries<P, F, H>() * 64;
+  float* vec = reinterpret_cast<float*>(f2 + fwd_entries<P, H, H>() * 64);  // b1 | b2 | w3 | D | g
+  build_fwd<P, F, H>(f1, c.W1);
+  build_fwd<P, H, H>(f2, c.W2);
+  load_vec(vec, c.b1, H);
+  load_vec(vec + VEC, c.b2, H);
+  load_vec(vec + 2 * VEC, c.w3, H);
+  for (int o = threadIdx.x; o < VEC; o += blockDim.x) {  // D = W2 w3
+    float d = 0.f;
+    if (o < H)
+      for (int k = 0; k < H; ++k) d = fmaf(c.W2[o * H + k], c.w3[k], d);
+    vec[3 * VEC + o] = d;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < VEC; i += blockDim.x) {  // g = W1 D
+    float a = 0.f;
+    if (i < F)
+      for (int o = 0; o < H; ++o) a = fmaf(c.W1[i * H + o], vec[3 * VEC + o], a);
+    vec[4 * VEC + i] = a;
+  }
+  __syncthreads();
+  const float b3 = c.b3 ? c.b3[0] : 0.f;
+  const float* gh = vec + 4 * VEC + 4 * ((threadIdx.x & 63) >> 5);  // lane-half base (see head_rows)
+  float acc = 0.f;
+  MLP_LOOP {
+    const int64_t row = tile * 32 + (lane & 31);
+    const bool ok = row < M;
+    f32x16 A[NTH], Bv[NTH], X[NTF];
+    load_rows<T, F>(X, x, row, M, h);
+    dense<P, F, H>(X, A, f1, lane);
+    bias_act<H>(A, vec, ACT_LINEAR, h);
+    dense<P, H, H>(A, Bv, f2, lane);
+    bias_act<H>(Bv, vec + VEC, ACT_LINEAR, h);
+    const float sc = rowdot<H>(Bv, vec + 2 * VEC, ok, h);
+    const float p = sigmoidf_(sc + b3);
+    float lo, gp;
+    bce(p, label, inv, lo, gp);
+    if (ok && h == 0) acc += lo;
+    const float dz = gp * p * (1.f - p);
+#pragma unroll
+    for (int t = 0; t < NTF; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 gv = *reinterpret_cast<const float4*>(gh + 32 * t + 8 * g);
+        X[t][4 * g] = dz * gv.x; X[t][4 * g + 1] = dz * gv.y; X[t][4 * g + 2] = dz * gv.z; X[t][4 * g + 3] = dz * gv.w;
+      }
+    store_rows<T, F>(dx, row, M, X, h);
+  }
+  slab_put(slab, 2, 0, acc);
+  slab_put(slab, 2, 1, 0.f);
+}
+
 // ===================================================================================================
 // vanilla GAN discriminator update (GAN/GAN.py:187-189): forward, BCE(label) per row, reverse to the
 // weight-gradient operands
@@ -2001,6 +2066,30 @@ void launch_mlp_critic_dx(int dt, int head, const void* x, const MlpCritic& cr, 
   if (M <= 0) return;
   // head 0: d/ds_b of the W loss = -1/B (B = M / T samples); head 1: BCE mean over the M rows
   const float inv = head == 0 ? (float)Tn / (float)M : 1.f / (float)M;
+  if (head == 1) {  // rank-1 input gradient (mlp_gan_dx_kernel); fp32 on the split bf16 products
+    constexpr size_t vecb = 5 * VEC * 4;
+    if (dt == DT_F32 && !fp32_exact_mode()) {
+      MLP_DISPATCH(dt, F, {
+        auto k = mlp_gan_dx_kernel<float, FF, 100, f32s_t>;
+        constexpr size_t lds =
+            (size_t)(fwd_entries<f32s_t, FF, 100>() + fwd_entries<f32s_t, 100, 100>()) * frag_bytes<f32s_t>() + vecb;
+        static_assert(lds <= 160 * 1024, "split discriminator images exceed LDS");
+        set_lds(k, lds);
+        hipLaunchKernelGGL(k, dim3(slab_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, (const float*)x, cr, label,
+                           (float*)dx, slab, M, inv);
+      });
+    } else {
+      MLP_DISPATCH(dt, F, {
+        auto k = mlp_gan_dx_kernel<T, FF, 100>;
+        constexpr size_t lds = (size_t)(fwd_entries<T, FF, 100>() + fwd_entries<T, 100, 100>()) * frag_bytes<T>() + vecb;
+        set_lds(k, lds);
+        hipLaunchKernelGGL(k, dim3(slab_grid(k, lds, M)), dim3(MLP_THREADS), lds, s, (const T*)x, cr, label, (T*)dx,
+                           slab, M, inv);
+      });
+    }
+    (void)H;
+    return;
+  }
   MLP_DISPATCH(dt, F, {
     constexpr size_t lds = lds_critic4<T, FF, 100>();
     if (head == 0) {
