@@ -2217,10 +2217,12 @@ bool mlp_affine_supported(int F, int Tn) {
          mlp_affine_lds_floats(F, 100, Tn) * sizeof(float) <= (size_t)kAffineLdsMax;
 }
 
-// row partitions of mlp_bt_colsum: ~512 threads per CU over the C / V column groups
+// row partitions of mlp_bt_colsum over the C / V column groups: ~1024 threads per CU for bf16, 512 for
+// fp32 (measured on config 4: bf16 206 -> 140 us per call at 1024, 2048 no better; fp32 best at 512;
+// profiles/r06_affine/colsum_ab)
 static int colsum_parts(int dt, int64_t B, int C) {
-  const int V = dt == DT_BF16 ? 8 : 4, G = C / V;
-  const int64_t want = ((int64_t)device_cu_count() * 512 + G - 1) / G;
+  const int V = dt == DT_BF16 ? 8 : 4, G = C / V, tpc = dt == DT_BF16 ? 1024 : 512;
+  const int64_t want = ((int64_t)device_cu_count() * tpc + G - 1) / G;
   return (int)std::max<int64_t>(1, std::min<int64_t>(B, want));
 }
 size_t mlp_affine_ws_floats(int dt, int64_t Bn, int Tn, int F) {
